@@ -1,0 +1,232 @@
+"""bench.py — trajectories/sec of the batched minimum-snap solve on MI355X.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1
+launched under torch.distributed.run, one rank per GPU.  Rank 0 prints ONE
+JSON line.
+
+Workload (BASELINE.json configs[1]): a batch of 1024 random 10-segment, N=10,
+3-D minimum-snap problems per GPU (createRandomVertices seeds 105 + global
+index, estimateSegmentTimes(v_max=3, a_max=5)); inputs resident in HBM.  One
+step = one batched solve (mtg_linear_solve: R assembly, block-tridiagonal
+Cholesky of R_pp, coefficient recovery, computeCost) over the rank's batch;
+with N > 1 the ranks also all-gather the per-trajectory costs over RCCL and
+select the global argmin (config 4's selection step).  Weak scaling: each rank
+owns a contiguous shard of trajectories.
+
+`--workload time` runs config 5 instead (time-allocation optimisation, 50
+objective evaluations per trajectory, B=4096); `--workload tube` config 3
+(tube QCQP, B=4096).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
+    p.add_argument("--segments", type=int, default=10)
+    p.add_argument("--workload", choices=["linear", "time", "tube"], default="linear")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline_linear(N, D, r, S, seeds, seconds):
+    """Oracle (reference-faithful C++ port, 1 thread) on a bounded sample."""
+    import ctypes
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    L = pyoracle.lib()
+    K = N // 2
+    B = len(seeds)
+    masks = np.zeros((B, S + 1, K), np.uint8)
+    vals = np.zeros((B, S + 1, K, D))
+    times = np.zeros((B, S))
+    for i, sd in enumerate(seeds):
+        v = pyoracle.random_vertices(N // 2 - 1, S, D, -10.0, 10.0, int(sd))
+        masks[i], vals[i] = v.mask, v.vals
+        times[i] = pyoracle.estimate_segment_times(v, 3.0, 5.0)
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.orc_bench_linear.argtypes = [ctypes.c_int] * 6 + [
+        ctypes.POINTER(ctypes.c_uint8), dp, dp, ctypes.c_int, ctypes.c_double,
+        ctypes.POINTER(ctypes.c_int64), dp]
+    n, sec = ctypes.c_int64(), ctypes.c_double()
+    rc = L.orc_bench_linear(N, D, r, S, K, B, masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                            vals.ctypes.data_as(dp), times.ctypes.data_as(dp), 1, seconds,
+                            ctypes.byref(n), ctypes.byref(sec))
+    if rc != 0:
+        raise RuntimeError(f"oracle baseline failed ({rc})")
+    return n.value / sec.value, n.value, B
+
+
+def load_pmc_traffic(workload, config_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass, if any."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        entry = data.get(workload, {})
+        if entry.get("config") == config_key:
+            return entry.get("bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import mav_tube_trajectory_generation_amd as mtg
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    N, D, r, S = 10, 3, 4, args.segments
+    wl = args.workload
+    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096}[wl]
+    seed0 = 105 + rank * B  # contiguous shard of the global batch
+    mask, fixed, times, pos = mtg.generate_random_problems(N, D, S, B, seed0=seed0)
+    ctx = mtg.Context(local_rank)
+    plan = mtg.LinearPlan(ctx, N, D, r, S, mask)
+    fixed_d = torch.from_numpy(fixed).to(dev)
+    times_d = torch.from_numpy(times).to(dev)
+    nf = plan.n_fixed
+    stream = torch.cuda.current_stream(dev)
+
+    if wl == "linear":
+        out = plan.solve(fixed_d, times_d, free=False)
+        gathered = [torch.empty(B, dtype=torch.float64, device=dev) for _ in range(world)]
+
+        def step():
+            plan.solve(fixed_d, times_d, free=False, out=out)
+            if world > 1:
+                dist.all_gather(gathered, out["cost"])
+                allc = torch.cat(gathered)
+                return torch.argmin(allc)
+            return None
+
+        bytes_per_traj = (D * nf + S) * 8 + (S * D * N + 1) * 8 + 4  # + status
+        metric = "trajectories/sec (10-seg, N=10, 3D minimum-snap) at 1/2/4/8 MI355X"
+        unit = "trajectories/s"
+        units_per_step = B
+    elif wl == "time":
+        max_evals = 50
+
+        def step():
+            return plan.time_optimize(fixed_d, times_d, max_evals=max_evals)
+
+        bytes_per_traj = (D * nf + S) * 8 + (S + 2) * 8
+        metric = "time-allocation optimisations/sec (4096 traj x 50 evals, 10-seg, N=10, 3D)"
+        unit = "trajectories/s"
+        units_per_step = B
+    else:
+        radii = torch.full((B, S, 2), 0.15, dtype=torch.float64, device=dev)
+        pos_d = torch.from_numpy(pos).to(dev)
+        # Tube fixed values: start derivs 0..M-1 then end derivs, per dim.
+        M = N // 2
+        tf = np.zeros((B, 3, N))
+        tf[:, :, 0] = pos[:, 0, :]
+        tf[:, :, M] = pos[:, S, :]
+        tfix = torch.from_numpy(tf).to(dev)
+
+        def step():
+            return mtg.tube_solve(ctx, N, r, pos_d, tfix, times_d, times_d, radii)
+
+        bytes_per_traj = ((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8 + (S * 3 * N + 1) * 8
+        metric = "tube QCQP solves/sec (4096 x 10-seg, N=10, 3D)"
+        unit = "trajectories/s"
+        units_per_step = B
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    # Per-launch HIP events on the stream the kernel runs on.
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    total_units = units_per_step * args.steps * world
+    value = total_units / elapsed
+    alg_bytes = bytes_per_traj * B
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    config_key = f"{wl}:B{B}:S{S}"
+    traffic = load_pmc_traffic(wl, config_key)
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1 and wl == "linear":
+            rate, nsolves, sample = cpu_baseline_linear(N, D, r, S, range(105, 105 + 256),
+                                                        args.cpu_seconds)
+            cpu = {"value": rate, "unit": unit, "cores": 1, "kind": "port",
+                   "sample": f"{nsolves} solves cycling over 256 of the same 10-seg problems "
+                             f"(seeds 105..360), oracle C++ port, 1 thread, "
+                             f"~{args.cpu_seconds:.0f} s"}
+        line = {
+            "metric": metric,
+            "value": value,
+            "unit": unit,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (createRandomVertices seeds 105+i, estimateSegmentTimes v=3 a=5)",
+            "config": {"workload": f"{wl}: {B} x {S}-segment N={N} D={D} r={r} per GPU",
+                       "batch_per_gpu": B, "segments": S, "N": N, "D": D,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

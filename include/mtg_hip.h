@@ -1,0 +1,238 @@
+/*
+ * mtg_hip.h — C ABI of the MI355X-native batched polynomial trajectory
+ * optimizer (libmtg_hip.so, built from mav_tube_trajectory_generation_amd/
+ * csrc/ for gfx950).
+ *
+ * This is the drop-in boundary for the hot path of
+ * NilsFunk/mav_tube_trajectory_generation (BASELINE.json `north_star`).
+ * The reference has no FFI: its boundary is the header-only C++ template API
+ * PolynomialOptimization<N> / PolynomialOptimizationConstrained<N> /
+ * PolynomialOptimizationNonLinear<N>.  Each entry point below
+ * names the reference interface it replaces (file:line relative to the
+ * reference root; "linear_impl" = include/mav_tube_trajectory_generation/
+ * impl/polynomial_optimization_linear_impl.h, "qcqp_impl" / "nonlinear_impl"
+ * likewise).  The C++ host mirror of that API lives in
+ * include/mav_tube_trajectory_generation_amd/ and calls only this ABI.
+ *
+ * Conventions
+ *  - All arithmetic is FP64.
+ *  - int return = status: 0 ok, < 0 error (mtg_status_string).  No C++
+ *    exceptions cross the ABI.  The reference CHECK-aborts on contract
+ *    violations (linear_impl:50-55, 66-67, 281-283, 296); here they are
+ *    reported as MTG_ERR_* codes, per trajectory where they depend on data.
+ *  - "device" pointers are HIP device (HBM) pointers owned by the caller;
+ *    "host" pointers are ordinary host memory.  Batched calls are
+ *    stream-ordered on `stream` (hipStream_t, NULL = default stream) and do
+ *    not synchronise.
+ *  - Layouts are row-major; a batch of B independent trajectories is stored
+ *    trajectory-major (trajectory b occupies one contiguous slice).
+ *  - N = number of polynomial coefficients (even, 4..12); M = N/2 endpoint
+ *    derivatives per vertex; D = spatial dimensions (1..4); S = segments;
+ *    r = derivative to optimise (0..M-1).
+ *  - A constraint pattern is a host byte array fixed_mask[(S+1) * M]:
+ *    fixed_mask[v*M + k] != 0 iff vertex v constrains derivative k
+ *    (Vertex::getConstraint, vertex.cpp:155-163).  Fixed constraints are
+ *    numbered in (vertex, derivative) order, free ones likewise — the
+ *    std::set<Constraint> order of linear_impl:171-252.
+ */
+#ifndef MTG_HIP_H_
+#define MTG_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  MTG_OK = 0,
+  MTG_ERR_INVALID_ARG = -1,  /* bad N/D/r/S/B or NULL pointer */
+  MTG_ERR_NO_DEVICE = -2,    /* no HIP device / runtime error */
+  MTG_ERR_HIP = -3,          /* HIP API call failed */
+  MTG_ERR_UNSUPPORTED = -4,  /* size beyond the kernels' LDS budget */
+  MTG_ERR_NUMERIC = -5       /* at least one trajectory failed (see status) */
+};
+
+/* Per-trajectory status codes written by batched kernels. */
+enum {
+  MTG_TRAJ_OK = 0,
+  MTG_TRAJ_BAD_TIME = 1,     /* a segment time <= 0 (linear_impl:296) */
+  MTG_TRAJ_NOT_SPD = 2,      /* free-derivative system not positive definite */
+  MTG_TRAJ_NOT_CONVERGED = 3 /* interior-point solve hit its iteration cap */
+};
+
+typedef struct mtg_ctx mtg_ctx;
+typedef struct mtg_plan mtg_plan;
+
+const char* mtg_status_string(int status);
+int mtg_version(void);
+
+/* Context = one HIP device.  Replaces nothing in the reference (which has no
+ * device); owns the cached constant tables and constraint patterns. */
+int mtg_ctx_create(int device, mtg_ctx** out);
+int mtg_ctx_destroy(mtg_ctx* ctx);
+int mtg_ctx_device(const mtg_ctx* ctx);
+
+/* ------------------------------------------------------------------------
+ * Plan = one (N, D, r, S, constraint pattern).  Replaces the batch-uniform
+ * part of PolynomialOptimization<N>::setupFromVertices (linear_impl:46-99):
+ * the constraint reordering of setupConstraintReorderingMatrix
+ * (linear_impl:171-252) and the per-(N, r) base / cost tables
+ * (polynomial.cpp:145-161, linear_impl:557-573).  Uploads to the device
+ * synchronously; the solve calls below never allocate or synchronise.
+ */
+int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S,
+                    const uint8_t* fixed_mask /* host (S+1)*M */,
+                    mtg_plan** out);
+int mtg_plan_destroy(mtg_plan* plan);
+/* n_fixed / n_free per dimension (getNumberFixedConstraints /
+ * getNumberFreeConstraints, polynomial_optimization_linear.h:224-226). */
+int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free);
+
+/* Batched linear solve.  Replaces, per trajectory b,
+ *   updateSegmentTimes(times_b)            linear_impl:277-304
+ *   solveLinear()                          linear_impl:337-379
+ *     constructR (R = M^T blkdiag(A^-T Q A^-1) M)   linear_impl:306-335
+ *     d_p = -R_pp^-1 R_pf d_f per dimension         linear_impl:359-375
+ *     updateSegmentsFromCompactConstraints          linear_impl:254-275
+ *   computeCost()                          linear_impl:113-130
+ * Inputs (device):
+ *   fixed_vals  B x D x n_fixed   fixed_constraints_compact_ per dimension
+ *   times       B x S             segment times
+ * Outputs (device; all but coeffs may be NULL):
+ *   coeffs      B x S x D x N     segment polynomial coefficients,
+ *                                 increasing powers (polynomial.h:33-37)
+ *   cost        B                 computeCost() = 0.5 sum c^T Q c
+ *   free_vals   B x D x n_free    free_constraints_compact_ (d_p)
+ *   status      B                 MTG_TRAJ_*
+ */
+int mtg_linear_solve(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                     const double* times, double* coeffs, double* cost,
+                     double* free_vals, int32_t* status, void* stream);
+
+/* Same, host pointers in and out (copies + synchronises).  Used by the C++
+ * single-trajectory shim PolynomialOptimization<N>::solveLinear(). */
+int mtg_linear_solve_host(const mtg_plan* plan, int64_t B,
+                          const double* fixed_vals, const double* times,
+                          double* coeffs, double* cost, double* free_vals,
+                          int32_t* status);
+
+/* Per-segment matrices for a batch of n segment times (device), each N x N:
+ * Q(T) = computeQuadraticCostJacobian (linear_impl:557-573),
+ * A(T) = setupMappingMatrix (linear_impl:101-111),
+ * A^-1(T) = invertMappingMatrix (linear_impl:132-169),
+ * H(T) = A^-T Q A^-1 (linear_impl:318).  Any output may be NULL.
+ * Backs getA / getAInverse / getR (linear_impl:503-544). */
+int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n,
+                         const double* times, double* Q, double* A,
+                         double* Ainv, double* H, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Time-allocation cost callback, batched.  Replaces
+ * PolynomialOptimizationNonLinear<N>::objectiveFunctionTime
+ * (nonlinear_impl:877-945) with w_c = 0 and no soft constraints (SURVEY.md
+ * §8a T6) and a linear inner solve (upstream semantics):
+ *   J(T) = computeCost() + time_penalty * (sum_i T_i)^2
+ * grad_mode (grad may be NULL when 0):
+ *   0  no gradient (objectiveFunctionTime is gradient-free, :881-882)
+ *   1  getCostAndGradientTime (nonlinear_impl:2495-2584):
+ *        grad_n = w_d * dJ_d/dT_n + w_t,  J_d = sum_dims d^T R(T) d with d
+ *        held at the solution for T (getCostAndGradientDerivative,
+ *        :1537-1606), central differences with step `increment`, clamped
+ *        at 0.1 (:2525-2530)
+ *   2  central differences of J itself (re-solved), same step and clamp.
+ * Inputs/outputs are device pointers: fixed_vals B x D x n_fixed,
+ * times B x S, cost B, grad B x S, status B.
+ */
+typedef struct mtg_time_params {
+  double time_penalty; /* NonlinearOptimizationParameters::time_penalty (500) */
+  double increment;    /* ::increment_time (0.1) */
+  double w_d;          /* ::weights.w_d (0.1) */
+  double w_t;          /* ::weights.w_t (1.0) */
+  int grad_mode;       /* see above */
+} mtg_time_params;
+
+int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                  const double* times, const mtg_time_params* params,
+                  double* cost, double* grad, int32_t* status, void* stream);
+
+/* Batched segment-time optimisation.  Replaces optimizeTime
+ * (nonlinear_impl:332-397): bounds [0.1, 2 T0] per segment (:350-358,
+ * 375-378), `max_evals` objective evaluations per trajectory (NLopt maxeval,
+ * :101).  NLopt's SBPLX is not available; the optimiser is a projected
+ * gradient method with backtracking on the grad_mode 2 gradient, run entirely
+ * on the device (one workgroup per trajectory, no host round trips).
+ *   times_io   B x S  in: initial times T0, out: optimised times
+ *   cost       B      final objective
+ *   evals      B      objective evaluations used (nullable)
+ */
+int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                      double* times_io, const mtg_time_params* params,
+                      int max_evals, double* cost, int32_t* evals,
+                      int32_t* status, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Tube QCQP (PolynomialOptimizationConstrained<N>, qcqp_impl).  The tube
+ * pattern is fixed by the reference: start and end vertices fully fixed
+ * (derivatives 0..M-1), every intermediate derivative free, including
+ * positions (setupConstraintReorderingMatrixkDim, qcqp_impl:18-118); D = 3
+ * (hard-coded in qcqp_impl:377-384, 777-781).
+ *
+ * Inputs (device), per trajectory:
+ *   positions   B x (S+1) x 3   vertex positions (tube geometry)
+ *   fixed_vals  B x 3 x N       start derivatives 0..M-1 then end
+ *                               derivatives 0..M-1, per dimension
+ *                               (fixed_constraints_compact_, qcqp_impl:48-65)
+ *   times_cp    B x S           times for the Bezier control-point maps
+ *                               (built once at setup, qcqp_impl:152-157)
+ *   times       B x S           current segment times (Q, A^-1)
+ *   radii       B x S x 2       (tube radius r1, sphere radius r2)
+ *
+ * mtg_tube_residuals evaluates the (S-1) + 3 S (N-2) inequality residuals
+ * g_k(x) = 0.5 x^T Q_k x + l_k x + c_k (feasible iff <= 0) of
+ * compute_sphere/tube/tube_end_constraints (qcqp_impl:357-474) at the free
+ * vector x (B x 3 (S-1) M, dimension-major as qcqp_impl:95-117), in the
+ * reference's constraint order.  resid: B x n_con.
+ *
+ * mtg_tube_solve replaces solveQCQP (qcqp_impl:476-788): minimise
+ * x^T R_pp x + 2 d_f^T R_fp x subject to g_k(x) <= 0 with a batched
+ * primal-dual interior-point method (MOSEK in the reference), then recover
+ * coefficients (qcqp_impl:777-785).  Outputs: x B x 3(S-1)M, coeffs
+ * B x S x 3 x N, cost B (computeCost), iters B, status B (nullable except
+ * coeffs).
+ */
+int mtg_tube_num_constraints(int N, int S);
+int mtg_tube_residuals(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                       const double* positions, const double* fixed_vals,
+                       const double* times_cp, const double* times,
+                       const double* radii, const double* x, double* resid,
+                       void* stream);
+int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                   const double* positions, const double* fixed_vals,
+                   const double* times_cp, const double* times,
+                   const double* radii, double tol, int max_iter, double* x,
+                   double* coeffs, double* cost, int32_t* iters,
+                   int32_t* status, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Host-side input generation (vertex.cpp:27-82, 228-269) for batches:
+ * trajectory b uses createRandomVertices(max_derivative = M-1, S, +/-pos_bound,
+ * seed = seed0 + b) and estimateSegmentTimes(v_max, a_max) (Nfabian, 6.5).
+ * Writes the standard pattern's fixed_vals (B x D x n_fixed, n_fixed =
+ * 2 M + (S-1)) and times (B x S); positions (B x (S+1) x D) nullable.
+ * Bit-identical to the reference generator (std::mt19937 +
+ * std::uniform_real_distribution<double> of libstdc++).
+ */
+int mtg_generate_random_problems(int N, int D, int S, int64_t B,
+                                 uint64_t seed0, double pos_bound,
+                                 double v_max, double a_max,
+                                 uint8_t* fixed_mask /* (S+1)*M */,
+                                 double* fixed_vals, double* times,
+                                 double* positions);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MTG_HIP_H_ */

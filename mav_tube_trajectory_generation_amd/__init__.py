@@ -1,0 +1,14 @@
+"""MI355X-native batched polynomial trajectory optimizer.
+
+Drop-in for the linear-constrained / tube-QCQP solve path of
+NilsFunk/mav_tube_trajectory_generation.  The product is libmtg_hip.so
+(hand-written gfx950 HIP kernels behind the C ABI in include/mtg_hip.h) and
+the C++ host API in include/mav_tube_trajectory_generation_amd/.  This Python
+package is the batched front end used by tests and bench.py.
+"""
+from ._abi import LIB_PATH, MTGError, lib  # noqa: F401
+from .batch import (Context, LinearPlan, generate_random_problems,  # noqa: F401
+                    segment_matrices, tube_num_constraints, tube_residuals, tube_solve)
+
+__all__ = ["Context", "LinearPlan", "MTGError", "generate_random_problems", "segment_matrices",
+           "tube_num_constraints", "tube_residuals", "tube_solve", "lib", "LIB_PATH"]

@@ -1,0 +1,89 @@
+"""ctypes binding of libmtg_hip.so (include/mtg_hip.h).
+
+The shared library is the product: every compute call goes to the gfx950
+kernels.  There is no CPU fallback; loading fails loudly when the library is
+missing or was built without a usable HIP device.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmtg_hip.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_ip = ctypes.POINTER(ctypes.c_int)
+_vp = ctypes.c_void_p
+
+
+class TimeParams(ctypes.Structure):
+    _fields_ = [("time_penalty", ctypes.c_double), ("increment", ctypes.c_double),
+                ("w_d", ctypes.c_double), ("w_t", ctypes.c_double),
+                ("grad_mode", ctypes.c_int)]
+
+
+# Symbol -> (restype, argtypes).  Must match include/mtg_hip.h exactly; the
+# CPU test suite checks that every declared symbol is exported.
+SIGNATURES = {
+    "mtg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "mtg_version": (ctypes.c_int, []),
+    "mtg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "mtg_ctx_destroy": (ctypes.c_int, [_vp]),
+    "mtg_ctx_device": (ctypes.c_int, [_vp]),
+    "mtg_plan_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, _u8p, ctypes.POINTER(_vp)]),
+    "mtg_plan_destroy": (ctypes.c_int, [_vp]),
+    "mtg_plan_counts": (ctypes.c_int, [_vp, _ip, _ip]),
+    "mtg_linear_solve": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mtg_linear_solve_host": (ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, _dp, _dp,
+                                             _i32p]),
+    "mtg_segment_matrices": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                            _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mtg_time_cost": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.POINTER(TimeParams),
+                                     _vp, _vp, _vp, _vp]),
+    "mtg_time_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp,
+                                         ctypes.POINTER(TimeParams), ctypes.c_int, _vp, _vp,
+                                         _vp, _vp]),
+    "mtg_tube_num_constraints": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "mtg_tube_residuals": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _vp]),
+    "mtg_tube_solve": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_double,
+                                      ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mtg_generate_random_problems": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_int64, ctypes.c_uint64,
+                                                    ctypes.c_double, ctypes.c_double,
+                                                    ctypes.c_double, _u8p, _dp, _dp, _dp]),
+}
+
+_lib = None
+
+
+class MTGError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmtg_hip.so (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MTGError(
+                f"{LIB_PATH} not found: build it with `python __graft_entry__.py build` "
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().mtg_status_string(rc).decode()
+        raise MTGError(f"{what} failed: {msg} ({rc})")
+    return rc

@@ -1,0 +1,236 @@
+"""Batched Python front end of libmtg_hip.so.
+
+Device buffers are torch CUDA (HIP) tensors: PyTorch supplies HBM
+allocations and the current stream only; every computation is a gfx950 kernel
+of libmtg_hip.so.  Host-array entry points (numpy) copy through the library's
+own host ABI.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from ._abi import MTGError, TimeParams, check, lib
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require(t, shape, name):
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise MTGError(f"{name} must be a CUDA tensor")
+    if t.dtype != torch.float64:
+        raise MTGError(f"{name} must be float64 (the path computes in FP64)")
+    if tuple(t.shape) != tuple(shape):
+        raise MTGError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+    if not t.is_contiguous():
+        raise MTGError(f"{name} must be contiguous")
+
+
+class Context:
+    """One HIP device (mtg_ctx_create)."""
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        check(lib().mtg_ctx_create(device, ctypes.byref(self._h)), "mtg_ctx_create")
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().mtg_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LinearPlan:
+    """(N, D, r, S, constraint pattern) -> batched solves (mtg_plan_create)."""
+
+    def __init__(self, ctx, N, D, r, S, fixed_mask):
+        mask = np.ascontiguousarray(np.asarray(fixed_mask, dtype=np.uint8).reshape(-1))
+        if mask.size != (S + 1) * (N // 2):
+            raise MTGError(f"fixed_mask must have (S+1)*N/2 = {(S + 1) * (N // 2)} entries")
+        self.ctx, self.N, self.D, self.r, self.S = ctx, N, D, r, S
+        self.mask = mask.reshape(S + 1, N // 2).copy()
+        self._h = ctypes.c_void_p()
+        check(lib().mtg_plan_create(ctx.handle, N, D, r, S,
+                                    mask.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                    ctypes.byref(self._h)), "mtg_plan_create")
+        nf, np_ = ctypes.c_int(), ctypes.c_int()
+        check(lib().mtg_plan_counts(self._h, ctypes.byref(nf), ctypes.byref(np_)), "counts")
+        self.n_fixed, self.n_free = nf.value, np_.value
+
+    def close(self):
+        if self._h:
+            lib().mtg_plan_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- device (torch) API -------------------------------------------------
+    def solve(self, fixed_vals, times, cost=True, free=False, status=True, out=None):
+        """Batched solveLinear + computeCost on device tensors.
+
+        fixed_vals [B, D, n_fixed], times [B, S] (float64, CUDA).  Returns a
+        dict with coeffs [B, S, D, N] and optionally cost [B], free [B, D,
+        n_free], status [B] (int32).
+        """
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        dev = times.device
+        o = out or {}
+        if "coeffs" not in o:
+            o["coeffs"] = torch.empty((B, self.S, self.D, self.N), dtype=torch.float64, device=dev)
+        if cost and "cost" not in o:
+            o["cost"] = torch.empty(B, dtype=torch.float64, device=dev)
+        if free and "free" not in o:
+            o["free"] = torch.empty((B, self.D, self.n_free), dtype=torch.float64, device=dev)
+        if status and "status" not in o:
+            o["status"] = torch.empty(B, dtype=torch.int32, device=dev)
+        check(lib().mtg_linear_solve(self._h, B, _ptr(fixed_vals), _ptr(times), _ptr(o["coeffs"]),
+                                     _ptr(o.get("cost")), _ptr(o.get("free")),
+                                     _ptr(o.get("status")), _stream(dev)), "mtg_linear_solve")
+        return o
+
+    def time_cost(self, fixed_vals, times, time_penalty=500.0, grad_mode=0, increment=0.1,
+                  w_d=0.1, w_t=1.0):
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        dev = times.device
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        grad = torch.empty((B, self.S), dtype=torch.float64, device=dev) if grad_mode else None
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        p = TimeParams(time_penalty, increment, w_d, w_t, grad_mode)
+        check(lib().mtg_time_cost(self._h, B, _ptr(fixed_vals), _ptr(times), ctypes.byref(p),
+                                  _ptr(cost), _ptr(grad), _ptr(status), _stream(dev)),
+              "mtg_time_cost")
+        return dict(cost=cost, grad=grad, status=status)
+
+    def time_optimize(self, fixed_vals, times, max_evals=50, time_penalty=500.0, increment=0.1,
+                      w_d=0.1, w_t=1.0):
+        """Optimise segment times in place on a copy; returns dict(times, cost, evals)."""
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        dev = times.device
+        t = times.clone()
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        evals = torch.empty(B, dtype=torch.int32, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        p = TimeParams(time_penalty, increment, w_d, w_t, 2)
+        check(lib().mtg_time_optimize(self._h, B, _ptr(fixed_vals), _ptr(t), ctypes.byref(p),
+                                      max_evals, _ptr(cost), _ptr(evals), _ptr(status),
+                                      _stream(dev)), "mtg_time_optimize")
+        return dict(times=t, cost=cost, evals=evals, status=status)
+
+    # -- host (numpy) API ---------------------------------------------------
+    def solve_host(self, fixed_vals, times):
+        fixed_vals = np.ascontiguousarray(fixed_vals, dtype=np.float64)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        B = times.shape[0]
+        coeffs = np.zeros((B, self.S, self.D, self.N))
+        cost = np.zeros(B)
+        free = np.zeros((B, self.D, self.n_free))
+        status = np.zeros(B, dtype=np.int32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        rc = lib().mtg_linear_solve_host(
+            self._h, B, fixed_vals.ctypes.data_as(dp), times.ctypes.data_as(dp),
+            coeffs.ctypes.data_as(dp), cost.ctypes.data_as(dp), free.ctypes.data_as(dp),
+            status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if rc not in (0, _abi_numeric()):
+            check(rc, "mtg_linear_solve_host")
+        return dict(coeffs=coeffs, cost=cost, free=free, status=status)
+
+
+def _abi_numeric():
+    return -5  # MTG_ERR_NUMERIC: per-trajectory status carries the detail
+
+
+def segment_matrices(ctx, N, r, times):
+    """Q, A, A^-1, H for each time in a CUDA float64 tensor [n] -> 4 x [n, N, N]."""
+    import torch
+    n = times.shape[0]
+    _require(times, (n,), "times")
+    outs = [torch.empty((n, N, N), dtype=torch.float64, device=times.device) for _ in range(4)]
+    check(lib().mtg_segment_matrices(ctx.handle, N, r, n, _ptr(times), *[_ptr(o) for o in outs],
+                                     _stream(times.device)), "mtg_segment_matrices")
+    return outs
+
+
+def generate_random_problems(N, D, S, B, seed0=105, pos_bound=10.0, v_max=3.0, a_max=5.0):
+    """Standard-pattern batch (host): mask [(S+1), N/2], fixed_vals [B, D, n_f],
+    times [B, S], positions [B, S+1, D] — createRandomVertices(seed0 + b) +
+    estimateSegmentTimes, bit-identical to the reference generator."""
+    M = N // 2
+    nf = 2 * M + (S - 1)
+    mask = np.zeros((S + 1, M), np.uint8)
+    fixed = np.zeros((B, D, nf))
+    times = np.zeros((B, S))
+    pos = np.zeros((B, S + 1, D))
+    dp = ctypes.POINTER(ctypes.c_double)
+    check(lib().mtg_generate_random_problems(
+        N, D, S, B, seed0, pos_bound, v_max, a_max,
+        mask.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), fixed.ctypes.data_as(dp),
+        times.ctypes.data_as(dp), pos.ctypes.data_as(dp)), "mtg_generate_random_problems")
+    return mask, fixed, times, pos
+
+
+def tube_num_constraints(N, S):
+    return lib().mtg_tube_num_constraints(N, S)
+
+
+def tube_residuals(ctx, N, r, positions, fixed_vals, times_cp, times, radii, x):
+    import torch
+    B, S = times.shape
+    m = tube_num_constraints(N, S)
+    resid = torch.empty((B, m), dtype=torch.float64, device=times.device)
+    check(lib().mtg_tube_residuals(ctx.handle, N, r, S, B, _ptr(positions), _ptr(fixed_vals),
+                                   _ptr(times_cp), _ptr(times), _ptr(radii), _ptr(x),
+                                   _ptr(resid), _stream(times.device)), "mtg_tube_residuals")
+    return resid
+
+
+def tube_solve(ctx, N, r, positions, fixed_vals, times_cp, times, radii, tol=1e-10,
+               max_iter=100):
+    import torch
+    B, S = times.shape
+    dev = times.device
+    for name, t, shp in (("positions", positions, (B, S + 1, 3)),
+                         ("fixed_vals", fixed_vals, (B, 3, N)),
+                         ("times_cp", times_cp, (B, S)), ("radii", radii, (B, S, 2))):
+        _require(t, shp, name)
+    n = 3 * (S - 1) * (N // 2)
+    x = torch.empty((B, n), dtype=torch.float64, device=dev)
+    coeffs = torch.empty((B, S, 3, N), dtype=torch.float64, device=dev)
+    cost = torch.empty(B, dtype=torch.float64, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    check(lib().mtg_tube_solve(ctx.handle, N, r, S, B, _ptr(positions), _ptr(fixed_vals),
+                               _ptr(times_cp), _ptr(times), _ptr(radii), tol, max_iter, _ptr(x),
+                               _ptr(coeffs), _ptr(cost), _ptr(iters), _ptr(status),
+                               _stream(dev)), "mtg_tube_solve")
+    return dict(x=x, coeffs=coeffs, cost=cost, iters=iters, status=status)

@@ -1,0 +1,411 @@
+// mtg_host.cpp — host side of the C ABI (include/mtg_hip.h): device
+// context, plans (constraint pattern + constant tables), argument checks and
+// the batched input generator.  Kernels live in mtg_kernels.hip / mtg_tube.hip.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "mtg_internal.h"
+#include "mav_tube_trajectory_generation_amd/vertex.h"
+
+struct mtg_ctx {
+  int device = 0;
+  std::mutex mu;
+  std::map<std::pair<int, int>, double*> tables;  // (N, r) -> H(1), A(1)^-1
+};
+
+struct mtg_plan {
+  mtg_ctx* ctx = nullptr;
+  mtg::PlanDev dev{};
+  int* d_slots = nullptr;
+  int* d_free_map = nullptr;
+};
+
+namespace {
+
+using mtg::PlanDev;
+
+int from_hip(hipError_t e) { return e == hipSuccess ? MTG_OK : MTG_ERR_HIP; }
+
+bool valid_N(int N) { return N >= 4 && N <= 12 && N % 2 == 0; }
+
+// Constant tables for (N, r), computed in long double:
+//   A(1)  = setupMappingMatrix(1)                (linear_impl:101-111)
+//   Q(1)  = computeQuadraticCostJacobian(r, 1)   (linear_impl:557-573)
+//   H(1)  = A(1)^-T Q(1) A(1)^-1                 (linear_impl:318)
+// H(T) and A(T)^-1 follow by the exact time-scaling identity (mtg_device.h).
+void build_tables(int N, int r, std::vector<double>* out) {
+  typedef long double ld;
+  const int M = N / 2;
+  auto falling = [](int n, int i) -> ld {
+    if (i < n) return 0;
+    ld p = 1;
+    for (int m = 0; m < n; ++m) p *= (i - m);
+    return p;
+  };
+  std::vector<ld> A(N * N, 0), Ai(N * N, 0), Q(N * N, 0), H(N * N, 0);
+  for (int l = 0; l < M; ++l) {
+    A[l * N + l] = falling(l, l);
+    for (int j = l; j < N; ++j) A[(M + l) * N + j] = falling(l, j);
+  }
+  // Gauss-Jordan with partial pivoting.
+  std::vector<ld> W(A), I(N * N, 0);
+  for (int i = 0; i < N; ++i) I[i * N + i] = 1;
+  for (int k = 0; k < N; ++k) {
+    int p = k;
+    for (int i = k + 1; i < N; ++i)
+      if (std::fabs(W[i * N + k]) > std::fabs(W[p * N + k])) p = i;
+    for (int j = 0; j < N; ++j) {
+      std::swap(W[k * N + j], W[p * N + j]);
+      std::swap(I[k * N + j], I[p * N + j]);
+    }
+    const ld piv = W[k * N + k];
+    for (int j = 0; j < N; ++j) {
+      W[k * N + j] /= piv;
+      I[k * N + j] /= piv;
+    }
+    for (int i = 0; i < N; ++i) {
+      if (i == k) continue;
+      const ld f = W[i * N + k];
+      if (f == 0) continue;
+      for (int j = 0; j < N; ++j) {
+        W[i * N + j] -= f * W[k * N + j];
+        I[i * N + j] -= f * I[k * N + j];
+      }
+    }
+  }
+  Ai = I;
+  for (int j = r; j < N; ++j)
+    for (int k = r; k < N; ++k)
+      Q[j * N + k] = 2 * falling(r, j) * falling(r, k) / static_cast<ld>(j + k - 2 * r + 1);
+  // H = Ai^T Q Ai.
+  std::vector<ld> QA(N * N, 0);
+  for (int i = 0; i < N; ++i)
+    for (int k = 0; k < N; ++k)
+      for (int j = 0; j < N; ++j) QA[i * N + j] += Q[i * N + k] * Ai[k * N + j];
+  for (int i = 0; i < N; ++i)
+    for (int k = 0; k < N; ++k)
+      for (int j = 0; j < N; ++j) H[i * N + j] += Ai[k * N + i] * QA[k * N + j];
+  // Symmetrise (exact in real arithmetic).
+  out->assign(2 * N * N, 0.0);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) {
+      (*out)[i * N + j] = static_cast<double>((H[i * N + j] + H[j * N + i]) / 2);
+      (*out)[N * N + i * N + j] = static_cast<double>(Ai[i * N + j]);
+    }
+}
+
+int get_tables(mtg_ctx* ctx, int N, int r, const double** out) {
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  auto key = std::make_pair(N, r);
+  auto it = ctx->tables.find(key);
+  if (it != ctx->tables.end()) {
+    *out = it->second;
+    return MTG_OK;
+  }
+  std::vector<double> host;
+  build_tables(N, r, &host);
+  double* d = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return MTG_ERR_HIP;
+  if (hipMalloc(&d, host.size() * sizeof(double)) != hipSuccess) return MTG_ERR_HIP;
+  if (hipMemcpy(d, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice) !=
+      hipSuccess) {
+    (void)hipFree(d);
+    return MTG_ERR_HIP;
+  }
+  ctx->tables[key] = d;
+  *out = d;
+  return MTG_OK;
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(size_t n) { return n ? hipMalloc(&p, n * sizeof(T)) : hipSuccess; }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* mtg_status_string(int status) {
+  switch (status) {
+    case MTG_OK: return "ok";
+    case MTG_ERR_INVALID_ARG: return "invalid argument";
+    case MTG_ERR_NO_DEVICE: return "no HIP device";
+    case MTG_ERR_HIP: return "HIP runtime error";
+    case MTG_ERR_UNSUPPORTED: return "unsupported size (LDS budget)";
+    case MTG_ERR_NUMERIC: return "numerical failure in at least one trajectory";
+    default: return "unknown status";
+  }
+}
+
+int mtg_version(void) { return 100; }
+
+int mtg_ctx_create(int device, mtg_ctx** out) {
+  if (!out) return MTG_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MTG_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return MTG_ERR_INVALID_ARG;
+  if (hipSetDevice(device) != hipSuccess) return MTG_ERR_HIP;
+  mtg_ctx* c = new mtg_ctx;
+  c->device = device;
+  *out = c;
+  return MTG_OK;
+}
+
+int mtg_ctx_destroy(mtg_ctx* ctx) {
+  if (!ctx) return MTG_ERR_INVALID_ARG;
+  (void)hipSetDevice(ctx->device);
+  for (auto& kv : ctx->tables) (void)hipFree(kv.second);
+  delete ctx;
+  return MTG_OK;
+}
+
+int mtg_ctx_device(const mtg_ctx* ctx) { return ctx ? ctx->device : MTG_ERR_INVALID_ARG; }
+
+int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fixed_mask,
+                    mtg_plan** out) {
+  if (!ctx || !out || !fixed_mask) return MTG_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (!valid_N(N) || D < 1 || D > mtg::kMaxD || r < 0 || r > N / 2 - 1 || S < 1)
+    return MTG_ERR_INVALID_ARG;
+  if (mtg::linear_lds_bytes(N, S, D) > static_cast<size_t>(mtg::kMaxLdsBytes))
+    return MTG_ERR_UNSUPPORTED;
+  const int M = N / 2;
+  // setupConstraintReorderingMatrix (linear_impl:171-252): fixed and free
+  // constraints each numbered in (vertex, derivative) order.
+  std::vector<int> slots((S + 1) * M), free_map;
+  int nf = 0, np = 0;
+  for (int v = 0; v <= S; ++v)
+    for (int k = 0; k < M; ++k) {
+      if (fixed_mask[v * M + k]) {
+        slots[v * M + k] = nf++;
+      } else {
+        slots[v * M + k] = -(np + 1);
+        free_map.push_back(v * M + k);
+        ++np;
+      }
+    }
+  const double* tab = nullptr;
+  int rc = get_tables(ctx, N, r, &tab);
+  if (rc) return rc;
+  std::unique_ptr<mtg_plan> p(new mtg_plan);
+  p->ctx = ctx;
+  if (hipMalloc(&p->d_slots, slots.size() * sizeof(int)) != hipSuccess) return MTG_ERR_HIP;
+  if (hipMalloc(&p->d_free_map, (free_map.size() + 1) * sizeof(int)) != hipSuccess) {
+    (void)hipFree(p->d_slots);
+    return MTG_ERR_HIP;
+  }
+  hipError_t e = hipMemcpy(p->d_slots, slots.data(), slots.size() * sizeof(int),
+                           hipMemcpyHostToDevice);
+  if (e == hipSuccess && np)
+    e = hipMemcpy(p->d_free_map, free_map.data(), free_map.size() * sizeof(int),
+                  hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_free_map);
+    return MTG_ERR_HIP;
+  }
+  p->dev = PlanDev{N, D, r, S, nf, np, tab, p->d_slots, p->d_free_map};
+  *out = p.release();
+  return MTG_OK;
+}
+
+int mtg_plan_destroy(mtg_plan* plan) {
+  if (!plan) return MTG_ERR_INVALID_ARG;
+  (void)hipFree(plan->d_slots);
+  (void)hipFree(plan->d_free_map);
+  delete plan;
+  return MTG_OK;
+}
+
+int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free) {
+  if (!plan) return MTG_ERR_INVALID_ARG;
+  if (n_fixed) *n_fixed = plan->dev.nf;
+  if (n_free) *n_free = plan->dev.np;
+  return MTG_OK;
+}
+
+int mtg_linear_solve(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                     const double* times, double* coeffs, double* cost, double* free_vals,
+                     int32_t* status, void* stream) {
+  if (!plan || B < 0 || B > 0x7fffffff || !times || !coeffs) return MTG_ERR_INVALID_ARG;
+  if (plan->dev.nf > 0 && !fixed_vals) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return from_hip(mtg::launch_linear_solve(plan->dev, B, fixed_vals, times, coeffs, cost,
+                                           free_vals, status,
+                                           static_cast<hipStream_t>(stream)));
+}
+
+int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                          const double* times, double* coeffs, double* cost,
+                          double* free_vals, int32_t* status) {
+  if (!plan || B < 0 || !times || !coeffs) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  const PlanDev& pl = plan->dev;
+  const size_t nfv = static_cast<size_t>(B) * pl.D * pl.nf;
+  const size_t nt = static_cast<size_t>(B) * pl.S;
+  const size_t nc = static_cast<size_t>(B) * pl.S * pl.D * pl.N;
+  const size_t npv = static_cast<size_t>(B) * pl.D * pl.np;
+  DevBuf<double> dfv, dt, dc, dcost, dfree;
+  DevBuf<int32_t> dst;
+  if (dfv.alloc(nfv) || dt.alloc(nt) || dc.alloc(nc) || dcost.alloc(B) ||
+      dfree.alloc(npv) || dst.alloc(B))
+    return MTG_ERR_HIP;
+  if (nfv && hipMemcpy(dfv.p, fixed_vals, nfv * sizeof(double), hipMemcpyHostToDevice))
+    return MTG_ERR_HIP;
+  if (hipMemcpy(dt.p, times, nt * sizeof(double), hipMemcpyHostToDevice)) return MTG_ERR_HIP;
+  int rc = mtg_linear_solve(plan, B, dfv.p, dt.p, dc.p, dcost.p, npv ? dfree.p : nullptr,
+                            dst.p, nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize()) return MTG_ERR_HIP;
+  if (hipMemcpy(coeffs, dc.p, nc * sizeof(double), hipMemcpyDeviceToHost)) return MTG_ERR_HIP;
+  if (cost && hipMemcpy(cost, dcost.p, B * sizeof(double), hipMemcpyDeviceToHost))
+    return MTG_ERR_HIP;
+  if (free_vals && npv &&
+      hipMemcpy(free_vals, dfree.p, npv * sizeof(double), hipMemcpyDeviceToHost))
+    return MTG_ERR_HIP;
+  std::vector<int32_t> st(B);
+  if (hipMemcpy(st.data(), dst.p, B * sizeof(int32_t), hipMemcpyDeviceToHost))
+    return MTG_ERR_HIP;
+  if (status) std::memcpy(status, st.data(), B * sizeof(int32_t));
+  for (int32_t s : st)
+    if (s != MTG_TRAJ_OK) return MTG_ERR_NUMERIC;
+  return MTG_OK;
+}
+
+int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* times,
+                         double* Q, double* A, double* Ainv, double* H, void* stream) {
+  if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || n < 0 || (n && !times))
+    return MTG_ERR_INVALID_ARG;
+  if (n == 0) return MTG_OK;
+  const double* tab = nullptr;
+  int rc = get_tables(ctx, N, r, &tab);
+  if (rc) return rc;
+  return from_hip(mtg::launch_segment_matrices(N, r, n, tab, times, Q, A, Ainv, H,
+                                               static_cast<hipStream_t>(stream)));
+}
+
+int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                  const double* times, const mtg_time_params* params, double* cost,
+                  double* grad, int32_t* status, void* stream) {
+  if (!plan || !params || B < 0 || B > 0x7fffffff || !times) return MTG_ERR_INVALID_ARG;
+  if (params->grad_mode < 0 || params->grad_mode > 2) return MTG_ERR_INVALID_ARG;
+  if (params->grad_mode && !(params->increment > 0)) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return from_hip(mtg::launch_time_cost(plan->dev, B, fixed_vals, times, *params, cost, grad,
+                                        status, static_cast<hipStream_t>(stream)));
+}
+
+int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                      double* times_io, const mtg_time_params* params, int max_evals,
+                      double* cost, int32_t* evals, int32_t* status, void* stream) {
+  if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
+    return MTG_ERR_INVALID_ARG;
+  if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return from_hip(mtg::launch_time_optimize(plan->dev, B, fixed_vals, times_io, *params,
+                                            max_evals, cost, evals, status,
+                                            static_cast<hipStream_t>(stream)));
+}
+
+int mtg_tube_num_constraints(int N, int S) {
+  if (!valid_N(N) || S < 1) return MTG_ERR_INVALID_ARG;
+  return (S - 1) + S * (N - 2) + 2 * S * (N - 2);
+}
+
+static int tube_args(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* positions,
+                     const double* fixed_vals, const double* times_cp, const double* times,
+                     const double* radii, mtg::TubeArgs* a) {
+  if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || S < 2 || B < 0 || B > 0x7fffffff)
+    return MTG_ERR_INVALID_ARG;
+  if (B && (!positions || !fixed_vals || !times_cp || !times || !radii))
+    return MTG_ERR_INVALID_ARG;
+  if (mtg::tube_lds_bytes(N, S) > static_cast<size_t>(mtg::kMaxLdsBytes))
+    return MTG_ERR_UNSUPPORTED;
+  const double* tab = nullptr;
+  int rc = get_tables(ctx, N, r, &tab);
+  if (rc) return rc;
+  *a = mtg::TubeArgs{N, r, S, B, tab, positions, fixed_vals, times_cp, times, radii};
+  return MTG_OK;
+}
+
+int mtg_tube_residuals(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* positions,
+                       const double* fixed_vals, const double* times_cp, const double* times,
+                       const double* radii, const double* x, double* resid, void* stream) {
+  mtg::TubeArgs a;
+  int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_cp, times, radii, &a);
+  if (rc) return rc;
+  if (B && (!x || !resid)) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return from_hip(mtg::launch_tube_residuals(a, x, resid, static_cast<hipStream_t>(stream)));
+}
+
+int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* positions,
+                   const double* fixed_vals, const double* times_cp, const double* times,
+                   const double* radii, double tol, int max_iter, double* x, double* coeffs,
+                   double* cost, int32_t* iters, int32_t* status, void* stream) {
+  mtg::TubeArgs a;
+  int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_cp, times, radii, &a);
+  if (rc) return rc;
+  if (B && !coeffs) return MTG_ERR_INVALID_ARG;
+  if (!(tol > 0) || max_iter < 1) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return from_hip(mtg::launch_tube_solve(a, tol, max_iter, x, coeffs, cost, iters, status,
+                                         static_cast<hipStream_t>(stream)));
+}
+
+int mtg_generate_random_problems(int N, int D, int S, int64_t B, uint64_t seed0,
+                                 double pos_bound, double v_max, double a_max,
+                                 uint8_t* fixed_mask, double* fixed_vals, double* times,
+                                 double* positions) {
+  using namespace mav_trajectory_generation;
+  if (!valid_N(N) || D < 1 || S < 1 || B < 0 || !(pos_bound > 0) || !(v_max > 0) ||
+      !(a_max > 0))
+    return MTG_ERR_INVALID_ARG;
+  const int M = N / 2;
+  // Standard pattern: start/end fixed to order M-1, intermediates position.
+  std::vector<uint8_t> mask((S + 1) * M, 0);
+  for (int v = 0; v <= S; ++v)
+    for (int k = 0; k < M; ++k) mask[v * M + k] = (v == 0 || v == S || k == 0) ? 1 : 0;
+  if (fixed_mask) std::memcpy(fixed_mask, mask.data(), mask.size());
+  const int nf = 2 * M + (S - 1);
+  const VectorXd lo = VectorXd::Constant(D, -pos_bound), hi = VectorXd::Constant(D, pos_bound);
+  for (int64_t b = 0; b < B; ++b) {
+    Vertex::Vector vs = createRandomVertices(M - 1, S, lo, hi, seed0 + b);
+    std::vector<double> t = estimateSegmentTimes(vs, v_max, a_max);
+    if (times)
+      for (int s = 0; s < S; ++s) times[b * S + s] = t[s];
+    if (positions)
+      for (int v = 0; v <= S; ++v) {
+        VectorXd p;
+        vs[v].getConstraint(derivative_order::POSITION, &p);
+        for (int d = 0; d < D; ++d) positions[(b * (S + 1) + v) * D + d] = p[d];
+      }
+    if (fixed_vals) {
+      int f = 0;
+      for (int v = 0; v <= S; ++v)
+        for (int k = 0; k < M; ++k) {
+          if (!mask[v * M + k]) continue;
+          VectorXd c;
+          vs[v].getConstraint(k, &c);
+          for (int d = 0; d < D; ++d) fixed_vals[(b * D + d) * nf + f] = c[d];
+          ++f;
+        }
+    }
+  }
+  return MTG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+// mtg_internal.h — shared between the host ABI (mtg_host.cpp) and the kernel
+// launchers (mtg_kernels.hip, mtg_tube.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/mtg_hip.h"
+
+namespace mtg {
+
+constexpr int kMaxD = 4;  // spatial dimensions supported by the kernels
+
+// Device view of a plan (mtg_plan_create).
+struct PlanDev {
+  int N, D, r, S;
+  int nf, np;              // fixed / free derivatives per dimension
+  const double* tab;       // H(1) then A(1)^-1, N*N each (device)
+  const int* slots;        // (S+1)*M: fixed index f >= 0, or -(p+1) for free p
+  const int* free_map;     // np: free index p -> v*M + k
+};
+
+hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
+                               const double* times, double* coeffs, double* cost,
+                               double* free_vals, int32_t* status, hipStream_t st);
+hipError_t launch_time_cost(const PlanDev& pl, int64_t B, const double* df,
+                            const double* times, const mtg_time_params& p,
+                            double* cost, double* grad, int32_t* status,
+                            hipStream_t st);
+hipError_t launch_time_optimize(const PlanDev& pl, int64_t B, const double* df,
+                                double* times, const mtg_time_params& p, int max_evals,
+                                double* cost, int32_t* evals, int32_t* status,
+                                hipStream_t st);
+hipError_t launch_segment_matrices(int N, int r, int64_t n, const double* tab,
+                                   const double* times, double* Q, double* A,
+                                   double* Ainv, double* H, hipStream_t st);
+size_t linear_lds_bytes(int N, int S, int D);
+
+// Tube QCQP (mtg_tube.hip).
+struct TubeArgs {
+  int N, r, S;
+  int64_t B;
+  const double* tab;        // H(1), A(1)^-1 for (N, r)
+  const double* positions;  // B x (S+1) x 3
+  const double* fixed_vals; // B x 3 x N
+  const double* times_cp;   // B x S
+  const double* times;      // B x S
+  const double* radii;      // B x S x 2
+};
+hipError_t launch_tube_residuals(const TubeArgs& a, const double* x, double* resid,
+                                 hipStream_t st);
+hipError_t launch_tube_solve(const TubeArgs& a, double tol, int max_iter, double* x,
+                             double* coeffs, double* cost, int32_t* iters,
+                             int32_t* status, hipStream_t st);
+size_t tube_lds_bytes(int N, int S);
+
+constexpr int kMaxLdsBytes = 160 * 1024;
+
+}  // namespace mtg

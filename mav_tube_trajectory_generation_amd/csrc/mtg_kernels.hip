@@ -1,0 +1,387 @@
+// mtg_kernels.hip — gfx950 kernels of the linear-solve and time-allocation
+// hot path.  One 64-lane workgroup per trajectory; all per-trajectory state in
+// LDS (mtg_device.h).  Launchers at the bottom are called by mtg_host.cpp.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "mtg_device.h"
+#include "mtg_internal.h"
+
+namespace mtg {
+
+// ---------------------------------------------------------------------------
+// Batched linear solve (setupFromVertices' per-trajectory part +
+// solveLinear + computeCost, linear_impl:277-379, 113-130).
+template <int N>
+__global__ __launch_bounds__(kWave) void linear_solve_kernel(
+    int S, int D, int r, int nf, int np, const double* __restrict__ tab,
+    const int* __restrict__ slots, const int* __restrict__ free_map,
+    const double* __restrict__ fixed_vals, const double* __restrict__ times,
+    double* __restrict__ coeffs, double* __restrict__ cost,
+    double* __restrict__ free_vals, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Layout lay = make_layout(N, S, D);
+  Traj<N> t{S, D, r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x)};
+  const int64_t b = blockIdx.x;
+  t.load_static(tab, slots);
+  __syncthreads();
+  for (int i = t.lane; i < S; i += kWave) t.T()[i] = times[b * S + i];
+  t.load_fixed(fixed_vals + b * D * nf, nf);
+  __syncthreads();
+  t.compute_powers();
+  __syncthreads();
+  const int bad_time = t.flag()[0] & 1;
+  if (!bad_time) t.solve();
+  const int fl = t.flag()[0];
+  const int st = (fl & 1) ? MTG_TRAJ_BAD_TIME : ((fl & 2) ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
+  const int64_t per = static_cast<int64_t>(S) * D * N;
+  if (bad_time) {
+    for (int i = t.lane; i < per; i += kWave) coeffs[b * per + i] = NAN;
+    if (cost && t.lane == 0) cost[b] = NAN;
+  } else {
+    t.write_coeffs(coeffs + b * per);
+    if (cost) {
+      const double J = t.cost();
+      if (t.lane == 0) cost[b] = J;
+    }
+    if (free_vals) {
+      for (int i = t.lane; i < np * D; i += kWave) {
+        const int d = i / np;
+        const int p = i % np;
+        const int vk = free_map[p];
+        free_vals[b * D * np + i] = t.dv()[vk * D + d];
+      }
+    }
+  }
+  if (status && t.lane == 0) status[b] = st;
+}
+
+// ---------------------------------------------------------------------------
+// Per-segment matrices Q, A, A^-1, H for a batch of times (accessor parity:
+// linear_impl:101-111, 132-169, 557-573, 318).  One thread per entry.
+__device__ inline double falling(int n, int i) {  // base(n, i) = i!/(i-n)!
+  if (i < n) return 0.0;
+  double p = 1.0;
+  for (int m = 0; m < n; ++m) p *= static_cast<double>(i - m);
+  return p;
+}
+
+__device__ inline double ipow(double t, int e) {
+  const double base = e < 0 ? 1.0 / t : t;
+  const int n = e < 0 ? -e : e;
+  double p = 1.0;
+  for (int q = 0; q < n; ++q) p *= base;
+  return p;
+}
+
+__global__ void segment_matrices_kernel(int N, int r, int64_t n,
+                                        const double* __restrict__ tab,
+                                        const double* __restrict__ times,
+                                        double* Q, double* A, double* Ainv,
+                                        double* H) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int NN = N * N;
+  if (gid >= n * NN) return;
+  const int64_t s = gid / NN;
+  const int e = static_cast<int>(gid % NN);
+  const int a = e / N, c = e % N;
+  const int M = N / 2;
+  const double T = times[s];
+  if (Q) {
+    double q = 0.0;
+    if (a >= r && c >= r) {
+      const int ex = a + c - 2 * r + 1;
+      q = falling(r, a) * falling(r, c) * ipow(T, ex) * 2.0 / ex;
+    }
+    Q[gid] = q;
+  }
+  if (A) {
+    const int l = a % M;
+    double v;
+    if (a < M)
+      v = (c == l) ? falling(l, l) : 0.0;
+    else
+      v = c >= l ? falling(l, c) * ipow(T, c - l) : 0.0;
+    A[gid] = v;
+  }
+  if (Ainv) Ainv[gid] = tab[NN + e] * ipow(T, (c % M) - a);
+  if (H) H[gid] = tab[e] * ipow(T, 1 - 2 * r + (a % M) + (c % M));
+}
+
+// ---------------------------------------------------------------------------
+// Time-allocation objective J(T) = computeCost() + time_penalty (sum T)^2
+// (objectiveFunctionTime, nonlinear_impl:877-945) with optional gradient.
+template <int N>
+__device__ double objective_at(Traj<N>& t, double time_penalty) {
+  // Assumes T() holds the times; recomputes powers and re-solves.
+  __syncthreads();
+  t.compute_powers();
+  __syncthreads();
+  t.clear_free();
+  __syncthreads();
+  t.solve();
+  const double J = t.cost();
+  double tot = 0.0;
+  for (int i = 0; i < t.S; ++i) tot += t.T()[i];  // nonlinear_impl:2768-2774
+  __syncthreads();
+  return J + tot * tot * time_penalty;
+}
+
+// Central-difference gradient of the re-solved objective (grad_mode 2) or the
+// reference's getCostAndGradientTime (grad_mode 1).  T() holds the base
+// times; on exit T() is restored and dv holds the solution at the base times
+// only for grad_mode 1.  Gradient written to g (LDS, S entries).
+template <int N>
+__device__ void gradient_at(Traj<N>& t, const mtg_time_params& p, double* g) {
+  const int S = t.S;
+  const double inc = p.increment;
+  if (p.grad_mode == 1) {
+    // J_d(T') with d fixed differs from J_d(T) only in segment n's block.
+    for (int n = 0; n < S; ++n) {
+      const double Tn = t.T()[n];
+      const double ts = Tn <= 0.1 ? 0.1 : Tn - inc;  // nonlinear_impl:2529-2530
+      const double tb = Tn <= 0.1 ? 0.1 : Tn + inc;
+      const double qs = t.seg_energy_at(n, ts);
+      const double qb = t.seg_energy_at(n, tb);
+      if (t.lane == 0) g[n] = p.w_d * (qb - qs) / (2.0 * inc) + p.w_t * 1.0;
+    }
+    __syncthreads();
+    return;
+  }
+  for (int n = 0; n < S; ++n) {
+    const double Tn = t.T()[n];
+    const double ts = Tn <= 0.1 ? 0.1 : Tn - inc;
+    const double tb = Tn <= 0.1 ? 0.1 : Tn + inc;
+    __syncthreads();
+    if (t.lane == 0) t.T()[n] = ts;
+    const double Js = objective_at(t, p.time_penalty);
+    if (t.lane == 0) t.T()[n] = tb;
+    const double Jb = objective_at(t, p.time_penalty);
+    if (t.lane == 0) {
+      t.T()[n] = Tn;
+      g[n] = (Jb - Js) / (2.0 * inc);
+    }
+  }
+  __syncthreads();
+}
+
+template <int N>
+__global__ __launch_bounds__(kWave) void time_cost_kernel(
+    int S, int D, int r, int nf, const double* __restrict__ tab,
+    const int* __restrict__ slots, const double* __restrict__ fixed_vals,
+    const double* __restrict__ times, mtg_time_params p,
+    double* __restrict__ cost, double* __restrict__ grad,
+    int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Layout lay = make_layout(N, S, D);
+  Traj<N> t{S, D, r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x)};
+  const int64_t b = blockIdx.x;
+  t.load_static(tab, slots);
+  __syncthreads();
+  for (int i = t.lane; i < S; i += kWave) t.T()[i] = times[b * S + i];
+  t.load_fixed(fixed_vals + b * D * nf, nf);
+  const double J = objective_at(t, p.time_penalty);
+  const int fl = t.flag()[0];
+  double* g = smem + lay.aux;
+  if (grad && p.grad_mode != 0 && !(fl & 1)) gradient_at(t, p, g);
+  const int fl2 = t.flag()[0];
+  if (t.lane == 0) {
+    if (cost) cost[b] = (fl & 1) ? NAN : J;
+    if (status)
+      status[b] = (fl2 & 1) ? MTG_TRAJ_BAD_TIME
+                            : ((fl2 & 2) ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
+  }
+  if (grad && p.grad_mode != 0)
+    for (int i = t.lane; i < S; i += kWave) grad[b * S + i] = (fl & 1) ? NAN : g[i];
+}
+
+// ---------------------------------------------------------------------------
+// Batched segment-time optimisation (optimizeTime, nonlinear_impl:332-397):
+// bounds [0.1, 2 T0]; projected, scaled steepest descent on the grad_mode 2
+// gradient with an expand/backtrack step rule; `max_evals` objective
+// evaluations (NLopt maxeval semantics, nonlinear_impl:101).
+template <int N>
+__global__ __launch_bounds__(kWave) void time_optimize_kernel(
+    int S, int D, int r, int nf, const double* __restrict__ tab,
+    const int* __restrict__ slots, const double* __restrict__ fixed_vals,
+    double* __restrict__ times_io, mtg_time_params p, int max_evals,
+    double* __restrict__ cost, int32_t* __restrict__ evals_out,
+    int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Layout lay = make_layout(N, S, D);
+  Traj<N> t{S, D, r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x)};
+  const int64_t b = blockIdx.x;
+  double* Tcur = smem + lay.aux;   // accepted times
+  double* T0 = Tcur + S;           // initial times (bounds)
+  double* g = T0 + S;              // gradient at Tcur
+  t.load_static(tab, slots);
+  __syncthreads();
+  for (int i = t.lane; i < S; i += kWave) {
+    const double v = times_io[b * S + i];
+    t.T()[i] = v;
+    Tcur[i] = v;
+    T0[i] = v;
+  }
+  t.load_fixed(fixed_vals + b * D * nf, nf);
+  mtg_time_params pg = p;
+  pg.grad_mode = 2;
+  double f = objective_at(t, p.time_penalty);
+  int evals = 1;
+  int fl = t.flag()[0];
+  if (!(fl & 1)) {
+    gradient_at(t, pg, g);
+    double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
+    constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
+    while (evals < max_evals && alpha > 1e-9) {
+      // Scaled direction: -g_n T0_n, normalised so the largest relative
+      // move is alpha.
+      double gmax = 0.0;
+      for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(g[i] * T0[i]));
+      if (!(gmax > 0.0)) break;
+      __syncthreads();
+      int moved = 0;
+      for (int i = 0; i < S; ++i) {
+        const double step = alpha * T0[i] * (g[i] * T0[i]) / gmax;
+        double tn = Tcur[i] - step;
+        tn = fmin(fmax(tn, kLower), 2.0 * T0[i]);
+        if (tn != Tcur[i]) moved = 1;
+        if (t.lane == 0) t.T()[i] = tn;
+      }
+      if (!moved) break;
+      const double ft = objective_at(t, p.time_penalty);
+      ++evals;
+      if (ft < f) {
+        f = ft;
+        if (t.lane == 0)
+          for (int i = 0; i < S; ++i) Tcur[i] = t.T()[i];
+        __syncthreads();
+        alpha = fmin(alpha * 1.5, 1.0);
+        gradient_at(t, pg, g);
+      } else {
+        alpha *= 0.5;
+        if (t.lane == 0)
+          for (int i = 0; i < S; ++i) t.T()[i] = Tcur[i];
+        __syncthreads();
+      }
+    }
+  }
+  fl = t.flag()[0];
+  __syncthreads();
+  for (int i = t.lane; i < S; i += kWave) times_io[b * S + i] = Tcur[i];
+  if (t.lane == 0) {
+    if (cost) cost[b] = (fl & 1) ? NAN : f;
+    if (evals_out) evals_out[b] = evals;
+    if (status)
+      status[b] = (fl & 1) ? MTG_TRAJ_BAD_TIME
+                           : ((fl & 2) ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers.
+namespace {
+template <typename K>
+hipError_t prepare_lds(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(bytes));
+  return hipSuccess;
+}
+}  // namespace
+
+template <int N>
+static hipError_t launch_linear_n(const PlanDev& pl, int64_t B, const double* df,
+                                  const double* times, double* coeffs, double* cost,
+                                  double* free_vals, int32_t* status, hipStream_t st) {
+  const size_t bytes = make_layout(N, pl.S, pl.D).bytes();
+  hipError_t e = prepare_lds(linear_solve_kernel<N>, bytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(linear_solve_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
+                     bytes, st, pl.S, pl.D, pl.r, pl.nf, pl.np, pl.tab, pl.slots,
+                     pl.free_map, df, times, coeffs, cost, free_vals, status);
+  return hipGetLastError();
+}
+
+template <int N>
+static hipError_t launch_time_cost_n(const PlanDev& pl, int64_t B, const double* df,
+                                     const double* times, const mtg_time_params& p,
+                                     double* cost, double* grad, int32_t* status,
+                                     hipStream_t st) {
+  const size_t bytes = make_layout(N, pl.S, pl.D).bytes();
+  hipError_t e = prepare_lds(time_cost_kernel<N>, bytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(time_cost_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
+                     bytes, st, pl.S, pl.D, pl.r, pl.nf, pl.tab, pl.slots, df, times, p,
+                     cost, grad, status);
+  return hipGetLastError();
+}
+
+template <int N>
+static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* df,
+                                    double* times, const mtg_time_params& p,
+                                    int max_evals, double* cost, int32_t* evals,
+                                    int32_t* status, hipStream_t st) {
+  const size_t bytes = make_layout(N, pl.S, pl.D).bytes();
+  hipError_t e = prepare_lds(time_optimize_kernel<N>, bytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(time_optimize_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
+                     bytes, st, pl.S, pl.D, pl.r, pl.nf, pl.tab, pl.slots, df, times, p,
+                     max_evals, cost, evals, status);
+  return hipGetLastError();
+}
+
+#define MTG_DISPATCH_N(N_, CALL)     \
+  switch (N_) {                      \
+    case 4: return CALL(4);          \
+    case 6: return CALL(6);          \
+    case 8: return CALL(8);          \
+    case 10: return CALL(10);        \
+    case 12: return CALL(12);        \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
+                               const double* times, double* coeffs, double* cost,
+                               double* free_vals, int32_t* status, hipStream_t st) {
+#define CALL(n) launch_linear_n<n>(pl, B, df, times, coeffs, cost, free_vals, status, st)
+  MTG_DISPATCH_N(pl.N, CALL)
+#undef CALL
+}
+
+hipError_t launch_time_cost(const PlanDev& pl, int64_t B, const double* df,
+                            const double* times, const mtg_time_params& p,
+                            double* cost, double* grad, int32_t* status,
+                            hipStream_t st) {
+#define CALL(n) launch_time_cost_n<n>(pl, B, df, times, p, cost, grad, status, st)
+  MTG_DISPATCH_N(pl.N, CALL)
+#undef CALL
+}
+
+hipError_t launch_time_optimize(const PlanDev& pl, int64_t B, const double* df,
+                                double* times, const mtg_time_params& p, int max_evals,
+                                double* cost, int32_t* evals, int32_t* status,
+                                hipStream_t st) {
+#define CALL(n) launch_time_opt_n<n>(pl, B, df, times, p, max_evals, cost, evals, status, st)
+  MTG_DISPATCH_N(pl.N, CALL)
+#undef CALL
+}
+
+hipError_t launch_segment_matrices(int N, int r, int64_t n, const double* tab,
+                                   const double* times, double* Q, double* A,
+                                   double* Ainv, double* H, hipStream_t st) {
+  const int64_t total = n * N * N;
+  const int threads = 256;
+  const int64_t blocks = (total + threads - 1) / threads;
+  hipLaunchKernelGGL(segment_matrices_kernel, dim3(static_cast<unsigned>(blocks)),
+                     dim3(threads), 0, st, N, r, n, tab, times, Q, A, Ainv, H);
+  return hipGetLastError();
+}
+
+size_t linear_lds_bytes(int N, int S, int D) { return make_layout(N, S, D).bytes(); }
+
+}  // namespace mtg

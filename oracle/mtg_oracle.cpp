@@ -1,0 +1,1318 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see mtg_oracle.h for the contract).
+//
+// Reference-faithful FP64 CPU restatement of the reference's hot path.  The
+// data structures follow the reference step by step (per-segment Q, A, A^-1
+// via the Schur complement, the 0/1 reordering matrix M built from std::set
+// ordered constraints, R = M^T blkdiag(H) M, a Householder QR solve of R_pp
+// standing in for Eigen::SparseQR<COLAMD>, per-segment coefficient recovery),
+// without the reference's unconditional stdout prints.
+#include "mtg_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <random>
+#include <set>
+#include <vector>
+
+namespace {
+
+// ----------------------------------------------------------------------------
+// Small dense matrix (row-major).
+struct Mat {
+  int r = 0, c = 0;
+  std::vector<double> a;
+  Mat() {}
+  Mat(int r_, int c_) : r(r_), c(c_), a(static_cast<size_t>(r_) * c_, 0.0) {}
+  double& operator()(int i, int j) { return a[static_cast<size_t>(i) * c + j]; }
+  double operator()(int i, int j) const {
+    return a[static_cast<size_t>(i) * c + j];
+  }
+};
+
+Mat matmul(const Mat& A, const Mat& B) {
+  Mat C(A.r, B.c);
+  for (int i = 0; i < A.r; ++i)
+    for (int k = 0; k < A.c; ++k) {
+      const double aik = A(i, k);
+      if (aik == 0.0) continue;
+      for (int j = 0; j < B.c; ++j) C(i, j) += aik * B(k, j);
+    }
+  return C;
+}
+
+Mat transpose(const Mat& A) {
+  Mat T(A.c, A.r);
+  for (int i = 0; i < A.r; ++i)
+    for (int j = 0; j < A.c; ++j) T(j, i) = A(i, j);
+  return T;
+}
+
+// Inverse by partial-pivot LU (what Eigen's fixed-size inverse() uses for
+// sizes > 4, linear_impl:160-161 / qcqp_impl:299).
+bool lu_inverse(const Mat& A, Mat* out) {
+  const int n = A.r;
+  Mat LU = A;
+  std::vector<int> piv(n);
+  for (int i = 0; i < n; ++i) piv[i] = i;
+  for (int k = 0; k < n; ++k) {
+    int p = k;
+    double best = std::fabs(LU(k, k));
+    for (int i = k + 1; i < n; ++i)
+      if (std::fabs(LU(i, k)) > best) best = std::fabs(LU(i, k)), p = i;
+    if (best == 0.0) return false;
+    if (p != k) {
+      for (int j = 0; j < n; ++j) std::swap(LU(k, j), LU(p, j));
+      std::swap(piv[k], piv[p]);
+    }
+    for (int i = k + 1; i < n; ++i) {
+      LU(i, k) /= LU(k, k);
+      const double l = LU(i, k);
+      for (int j = k + 1; j < n; ++j) LU(i, j) -= l * LU(k, j);
+    }
+  }
+  *out = Mat(n, n);
+  for (int col = 0; col < n; ++col) {
+    std::vector<double> y(n);
+    for (int i = 0; i < n; ++i) {
+      double s = (piv[i] == col) ? 1.0 : 0.0;
+      for (int j = 0; j < i; ++j) s -= LU(i, j) * y[j];
+      y[i] = s;
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double s = y[i];
+      for (int j = i + 1; j < n; ++j) s -= LU(i, j) * y[j];
+      y[i] = s / LU(i, i);
+    }
+    for (int i = 0; i < n; ++i) (*out)(i, col) = y[i];
+  }
+  return true;
+}
+
+// Householder QR of a square matrix and solve; stands in for
+// Eigen::SparseQR<SparseMatrix, COLAMDOrdering> (linear_impl:364-375).
+struct HouseholderQR {
+  Mat qr;
+  std::vector<double> beta;
+  bool ok = true;
+  explicit HouseholderQR(const Mat& A) : qr(A), beta(A.c, 0.0) {
+    const int m = qr.r, n = qr.c;
+    for (int k = 0; k < n && k < m; ++k) {
+      double norm = 0.0;
+      for (int i = k; i < m; ++i) norm += qr(i, k) * qr(i, k);
+      norm = std::sqrt(norm);
+      if (norm == 0.0) {
+        ok = false;
+        beta[k] = 0.0;
+        continue;
+      }
+      const double alpha = qr(k, k) > 0 ? -norm : norm;
+      const double v0 = qr(k, k) - alpha;
+      // v = [1, qr(k+1:,k)/v0]
+      for (int i = k + 1; i < m; ++i) qr(i, k) /= v0;
+      beta[k] = -v0 / alpha;
+      qr(k, k) = alpha;
+      for (int j = k + 1; j < n; ++j) {
+        double s = qr(k, j);
+        for (int i = k + 1; i < m; ++i) s += qr(i, k) * qr(i, j);
+        s *= beta[k];
+        qr(k, j) -= s;
+        for (int i = k + 1; i < m; ++i) qr(i, j) -= s * qr(i, k);
+      }
+    }
+  }
+  std::vector<double> solve(std::vector<double> b) const {
+    const int m = qr.r, n = qr.c;
+    for (int k = 0; k < n && k < m; ++k) {
+      double s = b[k];
+      for (int i = k + 1; i < m; ++i) s += qr(i, k) * b[i];
+      s *= beta[k];
+      b[k] -= s;
+      for (int i = k + 1; i < m; ++i) b[i] -= s * qr(i, k);
+    }
+    std::vector<double> x(n);
+    for (int i = n - 1; i >= 0; --i) {
+      double s = b[i];
+      for (int j = i + 1; j < n; ++j) s -= qr(i, j) * x[j];
+      x[i] = s / qr(i, i);
+    }
+    return x;
+  }
+};
+
+// Dense Cholesky (lower) in place; false if not positive definite.
+bool cholesky(Mat* A) {
+  const int n = A->r;
+  for (int j = 0; j < n; ++j) {
+    double d = (*A)(j, j);
+    for (int k = 0; k < j; ++k) d -= (*A)(j, k) * (*A)(j, k);
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    (*A)(j, j) = d;
+    for (int i = j + 1; i < n; ++i) {
+      double s = (*A)(i, j);
+      for (int k = 0; k < j; ++k) s -= (*A)(i, k) * (*A)(j, k);
+      (*A)(i, j) = s / d;
+    }
+    for (int k = j + 1; k < n; ++k) (*A)(j, k) = 0.0;
+  }
+  return true;
+}
+
+void cholesky_solve(const Mat& L, std::vector<double>* b) {
+  const int n = L.r;
+  std::vector<double>& x = *b;
+  for (int i = 0; i < n; ++i) {
+    double s = x[i];
+    for (int k = 0; k < i; ++k) s -= L(i, k) * x[k];
+    x[i] = s / L(i, i);
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = x[i];
+    for (int k = i + 1; k < n; ++k) s -= L(k, i) * x[k];
+    x[i] = s / L(i, i);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Polynomial base coefficients (polynomial.cpp:145-161, 200-201;
+// polynomial.h:45-51: kMaxConvolutionSize = 2*12-2 = 22).
+constexpr int kMaxConvolutionSize = 22;
+
+Mat computeBaseCoefficients(int N) {
+  Mat base(N, N);
+  for (int i = 0; i < N; ++i) base(0, i) = 1.0;
+  const int DEG = N - 1;
+  int order = DEG;
+  for (int n = 1; n < N; ++n) {
+    for (int i = DEG - order; i < N; ++i)
+      base(n, i) = (order - DEG + i) * base(n - 1, i);
+    --order;
+  }
+  return base;
+}
+
+const Mat& baseTable() {
+  static const Mat table = computeBaseCoefficients(kMaxConvolutionSize);
+  return table;
+}
+
+// polynomial.h:201-219.
+void baseCoeffsWithTime(int N, int derivative, double t, double* coeffs) {
+  const Mat& base = baseTable();
+  for (int j = 0; j < N; ++j) coeffs[j] = 0.0;
+  coeffs[derivative] = base(derivative, derivative);
+  if (std::abs(t) < std::numeric_limits<double>::epsilon()) return;
+  double t_power = t;
+  for (int j = derivative + 1; j < N; ++j) {
+    coeffs[j] = base(derivative, j) * t_power;
+    t_power = t_power * t;
+  }
+}
+
+// linear_impl:557-573.
+Mat computeQuadraticCostJacobian(int N, int derivative, double t) {
+  const Mat& base = baseTable();
+  Mat Q(N, N);
+  for (int col = 0; col < N - derivative; ++col) {
+    for (int row = 0; row < N - derivative; ++row) {
+      const double exponent = (N - 1 - derivative) * 2 + 1 - row - col;
+      Q(N - 1 - row, N - 1 - col) = base(derivative, N - 1 - row) *
+                                    base(derivative, N - 1 - col) *
+                                    std::pow(t, exponent) * 2.0 / exponent;
+    }
+  }
+  return Q;
+}
+
+// linear_impl:101-111.
+Mat setupMappingMatrix(int N, double T) {
+  Mat A(N, N);
+  std::vector<double> row(N);
+  for (int i = 0; i < N / 2; ++i) {
+    baseCoeffsWithTime(N, i, 0.0, row.data());
+    for (int j = 0; j < N; ++j) A(i, j) = row[j];
+    baseCoeffsWithTime(N, i, T, row.data());
+    for (int j = 0; j < N; ++j) A(i + N / 2, j) = row[j];
+  }
+  return A;
+}
+
+// linear_impl:132-169 (Schur complement inverse).
+Mat invertMappingMatrix(int N, const Mat& A) {
+  const int h = N / 2;
+  Mat Ainv(N, N);
+  Mat Dblk(h, h), C(h, h);
+  std::vector<double> diag_inv(h);
+  for (int i = 0; i < h; ++i) diag_inv[i] = 1.0 / A(i, i);
+  for (int i = 0; i < h; ++i)
+    for (int j = 0; j < h; ++j) {
+      C(i, j) = A(h + i, j);
+      Dblk(i, j) = A(h + i, h + j);
+    }
+  Mat Dinv;
+  lu_inverse(Dblk, &Dinv);
+  for (int i = 0; i < h; ++i) Ainv(i, i) = diag_inv[i];
+  // -D^-1 * C * A_inv
+  Mat DC = matmul(Dinv, C);
+  for (int i = 0; i < h; ++i)
+    for (int j = 0; j < h; ++j) {
+      Ainv(h + i, j) = -DC(i, j) * diag_inv[j];
+      Ainv(h + i, h + j) = Dinv(i, j);
+    }
+  return Ainv;
+}
+
+// ----------------------------------------------------------------------------
+// Vertex (vertex.h:42-112) in map form.
+struct Vertex {
+  int D;
+  std::map<int, std::vector<double>> constraints;
+  explicit Vertex(int d) : D(d) {}
+  bool get(int k, std::vector<double>* v) const {
+    auto it = constraints.find(k);
+    if (it == constraints.end()) return false;
+    *v = it->second;
+    return true;
+  }
+};
+
+std::vector<Vertex> verticesFromDense(int S, int D, int K, const uint8_t* mask,
+                                      const double* vals) {
+  std::vector<Vertex> vs;
+  for (int v = 0; v <= S; ++v) {
+    Vertex vx(D);
+    for (int k = 0; k < K; ++k) {
+      if (!mask[v * K + k]) continue;
+      std::vector<double> val(D);
+      for (int d = 0; d < D; ++d) val[d] = vals[(static_cast<size_t>(v) * K + k) * D + d];
+      vx.constraints[k] = val;
+    }
+    vs.push_back(vx);
+  }
+  return vs;
+}
+
+// Constraint record (polynomial_optimization_linear.h:288-305).
+struct Constraint {
+  size_t vertex_idx;
+  size_t constraint_idx;
+  std::vector<double> value;
+  bool operator<(const Constraint& rhs) const {
+    if (vertex_idx < rhs.vertex_idx) return true;
+    if (rhs.vertex_idx < vertex_idx) return false;
+    return constraint_idx < rhs.constraint_idx;
+  }
+  bool operator==(const Constraint& rhs) const {
+    return vertex_idx == rhs.vertex_idx && constraint_idx == rhs.constraint_idx;
+  }
+};
+
+// ----------------------------------------------------------------------------
+// PolynomialOptimization<N> restated with a runtime N
+// (polynomial_optimization_linear.h:45-285, linear_impl).
+struct LinearProblem {
+  int N = 10, D = 3, r = 4;
+  int S = 0;
+  std::vector<Vertex> vertices;
+  std::vector<double> times;
+  std::vector<Mat> Q, Ainv;
+  Mat M;                                  // constraint_reordering_
+  std::vector<std::vector<double>> df, dp;  // per dimension
+  int n_all = 0, nf = 0, np = 0;
+  std::vector<double> coeffs;  // S x D x N
+
+  // linear_impl:46-99.
+  int setupFromVertices(const std::vector<Vertex>& vs,
+                        const std::vector<double>& t, int deriv) {
+    if (N % 2 != 0 || N < 2 || N > kMaxConvolutionSize) return -1;
+    if (deriv < 0 || deriv > N / 2 - 1) return -2;
+    r = deriv;
+    vertices = vs;
+    times = t;
+    S = static_cast<int>(vs.size()) - 1;
+    if (S < 1 || static_cast<int>(t.size()) != S) return -3;
+    for (Vertex& v : vertices) {
+      Vertex tmp(D);
+      bool valid = true;
+      for (auto& kv : v.constraints) {
+        if (kv.first > N / 2 - 1)
+          valid = false;
+        else
+          tmp.constraints[kv.first] = kv.second;
+      }
+      if (!valid) v = tmp;
+    }
+    int rc = updateSegmentTimes(t);
+    if (rc) return rc;
+    setupConstraintReorderingMatrix();
+    return 0;
+  }
+
+  // linear_impl:277-304 (without the unconditional prints of :287-292).
+  int updateSegmentTimes(const std::vector<double>& t) {
+    if (static_cast<int>(t.size()) != S) return -3;
+    times = t;
+    Q.assign(S, Mat());
+    Ainv.assign(S, Mat());
+    for (int i = 0; i < S; ++i) {
+      if (!(t[i] > 0)) return -4;
+      Q[i] = computeQuadraticCostJacobian(N, r, t[i]);
+      Mat A = setupMappingMatrix(N, t[i]);
+      Ainv[i] = invertMappingMatrix(N, A);
+    }
+    return 0;
+  }
+
+  // linear_impl:171-252.
+  void setupConstraintReorderingMatrix() {
+    std::vector<Constraint> all;
+    std::set<Constraint> fixed, free_;
+    for (int v = 0; v <= S; ++v) {
+      const Vertex& vx = vertices[v];
+      const int occurrences = (v == 0 || v == S) ? 1 : 2;
+      for (int co = 0; co < occurrences; ++co) {
+        for (int k = 0; k < N / 2; ++k) {
+          Constraint c;
+          c.vertex_idx = v;
+          c.constraint_idx = k;
+          if (vx.get(k, &c.value)) {
+            all.push_back(c);
+            fixed.insert(c);
+          } else {
+            c.value.assign(D, 0.0);
+            all.push_back(c);
+            free_.insert(c);
+          }
+        }
+      }
+    }
+    n_all = static_cast<int>(all.size());
+    nf = static_cast<int>(fixed.size());
+    np = static_cast<int>(free_.size());
+    M = Mat(n_all, nf + np);
+    df.assign(D, std::vector<double>(nf, 0.0));
+    dp.assign(D, std::vector<double>(np, 0.0));
+    int row = 0;
+    for (const Constraint& ca : all) {
+      int col = 0;
+      for (const Constraint& cf : fixed) {
+        if (ca == cf) {
+          M(row, col) = 1.0;
+          for (int d = 0; d < D; ++d) df[d][col] = cf.value[d];
+        }
+        ++col;
+      }
+      for (const Constraint& cp : free_) {
+        if (ca == cp) M(row, col) = 1.0;
+        ++col;
+      }
+      ++row;
+    }
+  }
+
+  // linear_impl:306-335: R = M^T blkdiag(H_i) M, with H_i = A_i^-T Q_i A_i^-1.
+  // M has exactly one 1 per row, so the sparse product is the scatter below.
+  Mat constructR() const {
+    std::vector<int> col_of(n_all, -1);
+    for (int i = 0; i < n_all; ++i)
+      for (int j = 0; j < nf + np; ++j)
+        if (M(i, j) != 0.0) col_of[i] = j;
+    Mat R(nf + np, nf + np);
+    for (int s = 0; s < S; ++s) {
+      Mat H = matmul(matmul(transpose(Ainv[s]), Q[s]), Ainv[s]);
+      for (int a = 0; a < N; ++a)
+        for (int b = 0; b < N; ++b)
+          R(col_of[s * N + a], col_of[s * N + b]) += H(a, b);
+    }
+    return R;
+  }
+
+  // linear_impl:254-275.
+  void updateSegmentsFromCompactConstraints() {
+    coeffs.assign(static_cast<size_t>(S) * D * N, 0.0);
+    const int nall = nf + np;
+    for (int d = 0; d < D; ++d) {
+      std::vector<double> d_all(nall);
+      for (int i = 0; i < nf; ++i) d_all[i] = df[d][i];
+      for (int i = 0; i < np; ++i) d_all[nf + i] = dp[d][i];
+      for (int s = 0; s < S; ++s) {
+        std::vector<double> new_d(N, 0.0);
+        for (int a = 0; a < N; ++a)
+          for (int j = 0; j < nall; ++j) new_d[a] += M(s * N + a, j) * d_all[j];
+        for (int a = 0; a < N; ++a) {
+          double c = 0.0;
+          for (int b = 0; b < N; ++b) c += Ainv[s](a, b) * new_d[b];
+          coeffs[(static_cast<size_t>(s) * D + d) * N + a] = c;
+        }
+      }
+    }
+  }
+
+  // linear_impl:337-379 (without the print of :370).
+  int solveLinear() {
+    if (np == 0) {
+      updateSegmentsFromCompactConstraints();
+      return 0;
+    }
+    Mat R = constructR();
+    Mat Rpp(np, np), Rpf(np, nf);
+    for (int i = 0; i < np; ++i) {
+      for (int j = 0; j < nf; ++j) Rpf(i, j) = R(nf + i, j);
+      for (int j = 0; j < np; ++j) Rpp(i, j) = R(nf + i, nf + j);
+    }
+    HouseholderQR qr(Rpp);
+    for (int d = 0; d < D; ++d) {
+      std::vector<double> rhs(np, 0.0);
+      for (int i = 0; i < np; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < nf; ++j) s += Rpf(i, j) * df[d][j];
+        rhs[i] = -s;
+      }
+      dp[d] = qr.solve(rhs);
+    }
+    updateSegmentsFromCompactConstraints();
+    return qr.ok ? 0 : -5;
+  }
+
+  // linear_impl:113-130.
+  double computeCost() const {
+    double cost = 0.0;
+    for (int s = 0; s < S; ++s)
+      for (int d = 0; d < D; ++d) {
+        const double* c = &coeffs[(static_cast<size_t>(s) * D + d) * N];
+        double part = 0.0;
+        for (int a = 0; a < N; ++a) {
+          double qc = 0.0;
+          for (int b = 0; b < N; ++b) qc += Q[s](a, b) * c[b];
+          part += c[a] * qc;
+        }
+        cost += part;
+      }
+    return 0.5 * cost;
+  }
+
+  // getCostAndGradientDerivative's J_d (nonlinear_impl:1537-1606): the full
+  // d^T R d over all dimensions with the current (not re-solved) d_p.
+  double costDerivativeJd() const {
+    Mat R = constructR();
+    double J = 0.0;
+    for (int d = 0; d < D; ++d) {
+      std::vector<double> all(nf + np);
+      for (int i = 0; i < nf; ++i) all[i] = df[d][i];
+      for (int i = 0; i < np; ++i) all[nf + i] = dp[d][i];
+      for (int i = 0; i < nf + np; ++i)
+        for (int j = 0; j < nf + np; ++j) J += all[i] * R(i, j) * all[j];
+    }
+    return J;
+  }
+};
+
+int setupLinear(int N, int D, int r, int S, int K, const uint8_t* mask,
+                const double* vals, const double* times, LinearProblem* lp) {
+  if (!mask || !vals || !times || S < 1 || D < 1 || K < 1) return -1;
+  lp->N = N;
+  lp->D = D;
+  std::vector<Vertex> vs = verticesFromDense(S, D, K, mask, vals);
+  std::vector<double> t(times, times + S);
+  return lp->setupFromVertices(vs, t, r);
+}
+
+// ----------------------------------------------------------------------------
+// Tube QCQP (PolynomialOptimizationConstrained<N>, qcqp_impl).
+int factorial(int n) { return n > 1 ? n * factorial(n - 1) : 1; }  // :791-797
+int binomialCoeff(int n, int k) {  // :799-814
+  int res = 1;
+  if (k > n - k) k = n - k;
+  for (int i = 0; i < k; ++i) {
+    res *= (n - i);
+    res /= (i + 1);
+  }
+  return res;
+}
+
+// qcqp_impl:267-319.
+Mat setupInverseControlPointMappingMatrix(int N, double T) {
+  const int h = N / 2;
+  Mat Bul(h, h);
+  Bul(0, 0) = 1;
+  const int n = N - 1;
+  for (int l = 1; l < h; ++l)
+    for (int j = 0; j < h; ++j)
+      if (j <= l)
+        Bul(l, j) = factorial(n) / factorial(n - l) * std::pow(-1, l + j) /
+                    std::pow(T, l) * binomialCoeff(l, j);
+  Mat Bul_inv;
+  lu_inverse(Bul, &Bul_inv);
+  for (int k = 0; k < h; ++k)
+    for (int i = 0; i < h; ++i)
+      if (Bul_inv(k, i) > -0.00001 && Bul_inv(k, i) < 0.00001) Bul_inv(k, i) = 0;
+  Mat Binv(N, N);
+  for (int k = 0; k < h; ++k)
+    for (int i = 0; i < h; ++i) {
+      Binv(k, i) = Bul_inv(k, i);
+      // B_lr_inv = rowreverse(B_ul_inv) * diag((-1)^i)
+      Binv(h + k, h + i) = Bul_inv(h - 1 - k, i) * std::pow(-1, i);
+    }
+  return Binv;
+}
+
+// One inequality constraint 0.5 x^T quad x + lin x + cst <= 0, stored on its
+// support (the free variables it touches).
+struct QConstraint {
+  std::vector<int> supp;
+  std::vector<double> quad;  // |supp|^2
+  std::vector<double> lin;   // |supp|
+  double cst = 0.0;
+};
+
+struct TubeProblem {
+  LinearProblem lp;  // Q, A^-1, 1-D reordering (qcqp_impl:95-117)
+  int N = 10, D = 3, S = 0;
+  std::vector<std::pair<double, double>> radii;
+  std::vector<Mat> Binv;     // per segment, at setup times (qcqp_impl:152-157)
+  int nfk = 0, npk = 0, nak = 0;
+  std::vector<int> colk;     // kDim reordering: row -> column
+  std::vector<double> dfk;   // fixed_constraints_compact_kDim_
+  std::vector<int> col1;     // 1-D reordering rows -> columns
+  std::vector<QConstraint> cons;
+
+  // qcqp_impl:121-186 + :18-118.
+  int setup(const std::vector<Vertex>& vs, const std::vector<double>& times_cp,
+            const std::vector<double>& times, int deriv) {
+    N = lp.N;
+    D = lp.D;
+    if (D != 3) return -10;  // hard-coded D=3 (qcqp_impl:377-384, 777-781)
+    S = static_cast<int>(vs.size()) - 1;
+    if (static_cast<int>(radii.size()) != S) return -11;
+    Binv.clear();
+    for (int i = 0; i < S; ++i) {
+      if (!(times_cp[i] > 0)) return -4;
+      Binv.push_back(setupInverseControlPointMappingMatrix(N, times_cp[i]));
+    }
+    int rc = lp.setupFromVertices(vs, times, deriv);
+    if (rc) return rc;
+    // setupConstraintReorderingMatrixkDim (qcqp_impl:18-118).
+    const int h = N / 2;
+    lp.nf = N;
+    nfk = N * D;
+    lp.np = (S - 1) * h;
+    npk = lp.np * D;
+    lp.n_all = N * S;
+    nak = D * N * S;
+    dfk.assign(nfk, 0.0);
+    lp.df.assign(D, std::vector<double>(N, 0.0));
+    lp.dp.assign(D, std::vector<double>(lp.np, 0.0));
+    for (int ending = 0; ending < 2; ++ending) {
+      const int v = ending * S;
+      for (int k = 0; k < h; ++k) {
+        std::vector<double> val;
+        if (!lp.vertices[v].get(k, &val)) return -12;  // reference: UB
+        for (int d = 0; d < D; ++d) {
+          dfk[ending * h + d * N + k] = val[d];
+          lp.df[d][ending * h + k] = val[d];
+        }
+      }
+    }
+    colk.assign(nak, -1);
+    for (int d = 0; d < D; ++d)
+      for (int k = 0; k < 2; ++k) {
+        int row = d * (2 * h + (S - 1) * N) + k * (h + (S - 1) * N);
+        int col = d * 2 * h + k * h;
+        for (int i = 0; i < h; ++i) colk[row++] = col++;
+      }
+    for (int d = 0; d < D; ++d)
+      for (int k = 0; k < S - 1; ++k) {
+        int row = d * (2 * h + (S - 1) * N) + k * N + h;
+        int col = D * 2 * h + d * (S - 1) * h + k * h;
+        for (int i = 0; i < h; ++i) {
+          colk[row] = col;
+          colk[row + h] = col;
+          ++row;
+          ++col;
+        }
+      }
+    col1.assign(N * S, -1);
+    for (int k = 0; k < 2; ++k) {
+      int row = k * (h + (S - 1) * N);
+      int col = k * h;
+      for (int i = 0; i < h; ++i) col1[row++] = col++;
+    }
+    for (int k = 0; k < S - 1; ++k) {
+      int row = k * N + h;
+      int col = 2 * h + k * h;
+      for (int i = 0; i < h; ++i) {
+        col1[row] = col;
+        col1[row + h] = col;
+        ++row;
+        ++col;
+      }
+    }
+    lp.M = Mat(N * S, N + lp.np);
+    for (int i = 0; i < N * S; ++i) lp.M(i, col1[i]) = 1.0;
+    return 0;
+  }
+
+  // constructRkDim (qcqp_impl:188-221) restricted to the blocks used:
+  // P = 2 R_pp, q = (2 d_f^T R_fp)^T (qcqp_impl:497-502).
+  void objective(Mat* P, std::vector<double>* q) const {
+    Mat R(nfk + npk, nfk + npk);
+    for (int s = 0; s < S; ++s) {
+      Mat H = matmul(matmul(transpose(lp.Ainv[s]), lp.Q[s]), lp.Ainv[s]);
+      for (int d = 0; d < D; ++d) {
+        const int start = s * N + d * N * S;
+        for (int a = 0; a < N; ++a)
+          for (int b = 0; b < N; ++b)
+            R(colk[start + a], colk[start + b]) += H(a, b);
+      }
+    }
+    *P = Mat(npk, npk);
+    q->assign(npk, 0.0);
+    for (int i = 0; i < npk; ++i)
+      for (int j = 0; j < npk; ++j) (*P)(i, j) = 2.0 * R(nfk + i, nfk + j);
+    for (int j = 0; j < npk; ++j) {
+      double s = 0.0;
+      for (int i = 0; i < nfk; ++i) s += dfk[i] * R(i, nfk + j);
+      (*q)[j] = 2.0 * s;
+    }
+  }
+
+  // Control point j of segment i as an extraction E (D x (nfk+npk)),
+  // E = F_j * B_inv * M_kDim (qcqp_impl:337-349), kept sparse per row.
+  void extraction(int i, int j, std::vector<std::vector<double>>* E) const {
+    E->assign(D, std::vector<double>(nfk + npk, 0.0));
+    for (int k = 0; k < D; ++k)
+      for (int m = 0; m < N; ++m) {
+        const double b = Binv[i](j, m);
+        if (b == 0.0) continue;
+        (*E)[k][colk[k * N * S + i * N + m]] += b;
+      }
+  }
+
+  static QConstraint fromDense(int npk, const std::vector<double>& lin_full,
+                               const std::vector<std::vector<double>>* Ep,
+                               const double* LL, double quad_scale, double cst,
+                               int D) {
+    // quad = quad_scale * Ep^T LL Ep (Ep: D x npk), lin = lin_full.
+    QConstraint c;
+    std::vector<char> touch(npk, 0);
+    for (int j = 0; j < npk; ++j) {
+      if (lin_full[j] != 0.0) touch[j] = 1;
+      if (Ep)
+        for (int k = 0; k < D; ++k)
+          if ((*Ep)[k][j] != 0.0) touch[j] = 1;
+    }
+    for (int j = 0; j < npk; ++j)
+      if (touch[j]) c.supp.push_back(j);
+    const int m = static_cast<int>(c.supp.size());
+    c.lin.resize(m);
+    for (int a = 0; a < m; ++a) c.lin[a] = lin_full[c.supp[a]];
+    c.quad.assign(static_cast<size_t>(m) * m, 0.0);
+    if (Ep && quad_scale != 0.0) {
+      for (int a = 0; a < m; ++a)
+        for (int b = 0; b < m; ++b) {
+          double s = 0.0;
+          for (int k = 0; k < D; ++k)
+            for (int l = 0; l < D; ++l)
+              s += (*Ep)[k][c.supp[a]] * LL[k * D + l] * (*Ep)[l][c.supp[b]];
+          c.quad[static_cast<size_t>(a) * m + b] = quad_scale * s;
+        }
+    }
+    c.cst = cst;
+    return c;
+  }
+
+  // setupControlPointConstraints (qcqp_impl:321-474).
+  void buildConstraints() {
+    cons.clear();
+    const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    std::vector<std::vector<double>> E;
+    for (int i = 0; i < S; ++i) {
+      std::vector<double> p0, p1;
+      lp.vertices[i].get(0, &p0);
+      lp.vertices[i + 1].get(0, &p1);
+      // Fixed part c_f = E_f d_f and free part E_p of a control point.
+      auto split = [&](int j, std::vector<double>* cf,
+                       std::vector<std::vector<double>>* Ep) {
+        extraction(i, j, &E);
+        cf->assign(D, 0.0);
+        Ep->assign(D, std::vector<double>(npk, 0.0));
+        for (int k = 0; k < D; ++k) {
+          for (int c = 0; c < nfk; ++c) (*cf)[k] += E[k][c] * dfk[c];
+          for (int c = 0; c < npk; ++c) (*Ep)[k][c] = E[k][nfk + c];
+        }
+      };
+      std::vector<double> cf;
+      std::vector<std::vector<double>> Ep;
+      // compute_sphere_constraints (qcqp_impl:357-365): only the free columns.
+      if (i < S - 1) {
+        split(N - 1, &cf, &Ep);
+        const double r2 = radii[i].second;
+        double pp = 0.0;
+        for (int k = 0; k < D; ++k) pp += p1[k] * p1[k];
+        std::vector<double> lin(npk, 0.0);
+        for (int c = 0; c < npk; ++c)
+          for (int k = 0; k < D; ++k) lin[c] += -2.0 * p1[k] * Ep[k][c];
+        cons.push_back(fromDense(npk, lin, &Ep, I3, 2.0, pp - r2 * r2, D));
+      }
+      // compute_tube_constraints (qcqp_impl:369-429).
+      double n[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+      const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+      for (int k = 0; k < 3; ++k) n[k] /= nn;
+      const double nx = n[0], ny = n[1], nz = n[2];
+      const double px = p0[0], py = p0[1], pz = p0[2];
+      double A[9] = {1 - std::pow(nx, 2), -nx * ny,          -nx * nz,
+                     -nx * ny,            1 - std::pow(ny, 2), -ny * nz,
+                     -nx * nz,            -ny * nz,          1 - std::pow(nz, 2)};
+      for (int k = 0; k < 9; ++k)
+        if (A[k] > -0.000001 && A[k] < 0.000001) A[k] = 0;
+      double b[3] = {(std::pow(nx, 2) - 1) * px + nx * ny * py + nx * nz * pz,
+                     nx * ny * px + (std::pow(ny, 2) - 1) * py + ny * nz * pz,
+                     nx * nz * px + ny * nz * py + (std::pow(nz, 2) - 1) * pz};
+      for (int k = 0; k < 3; ++k)
+        if (b[k] > -0.000001 && b[k] < 0.000001) b[k] = 0;
+      double LL[9], L[3];
+      for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) {
+          double s = 0.0;
+          for (int k = 0; k < 3; ++k) s += A[k * 3 + a] * A[k * 3 + c];
+          LL[a * 3 + c] = s;
+        }
+      for (int c = 0; c < 3; ++c) {
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s += b[k] * A[k * 3 + c];
+        L[c] = 2.0 * s;
+      }
+      const double r1 = radii[i].first;
+      const double mu = b[0] * b[0] + b[1] * b[1] + b[2] * b[2] - std::pow(r1, 2);
+      for (int j = 1; j < N - 1; ++j) {
+        split(j, &cf, &Ep);
+        // const = cf^T LL cf + L cf + mu; lin = 2 cf^T LL Ep + L Ep;
+        // quad = 2 Ep^T LL Ep.
+        double cst = mu;
+        double LLcf[3];
+        for (int a = 0; a < 3; ++a) {
+          LLcf[a] = 0.0;
+          for (int c = 0; c < 3; ++c) LLcf[a] += LL[a * 3 + c] * cf[c];
+        }
+        for (int a = 0; a < 3; ++a) cst += cf[a] * LLcf[a] + L[a] * cf[a];
+        std::vector<double> lin(npk, 0.0);
+        for (int c = 0; c < npk; ++c)
+          for (int a = 0; a < 3; ++a)
+            lin[c] += (2.0 * LLcf[a] + L[a]) * Ep[a][c];
+        cons.push_back(fromDense(npk, lin, &Ep, LL, 2.0, cst, D));
+      }
+      // compute_tube_end_constraints (qcqp_impl:431-474).
+      const double rs = (i == 0) ? radii[0].first : radii[i - 1].second;
+      const double re = radii[i].second;
+      double ps[3], pe[3];
+      for (int k = 0; k < 3; ++k) {
+        ps[k] = p0[k] - n[k] * rs;
+        pe[k] = p1[k] + n[k] * re;
+      }
+      for (int k = 0; k < N - 2; ++k) {
+        split(k + 1, &cf, &Ep);
+        for (int side = 0; side < 2; ++side) {
+          const double sgn = side == 0 ? -1.0 : 1.0;  // n_start = -n, n_end = n
+          const double* p = side == 0 ? ps : pe;
+          double cst = 0.0;
+          for (int a = 0; a < 3; ++a) cst += -sgn * n[a] * p[a] + sgn * n[a] * cf[a];
+          std::vector<double> lin(npk, 0.0);
+          for (int c = 0; c < npk; ++c)
+            for (int a = 0; a < 3; ++a) lin[c] += sgn * n[a] * Ep[a][c];
+          cons.push_back(fromDense(npk, lin, nullptr, I3, 0.0, cst, D));
+        }
+      }
+    }
+  }
+
+  double residual(const QConstraint& c, const std::vector<double>& x) const {
+    const int m = static_cast<int>(c.supp.size());
+    double g = c.cst;
+    for (int a = 0; a < m; ++a) {
+      const double xa = x[c.supp[a]];
+      g += c.lin[a] * xa;
+      double qx = 0.0;
+      for (int b = 0; b < m; ++b) qx += c.quad[static_cast<size_t>(a) * m + b] * x[c.supp[b]];
+      g += 0.5 * xa * qx;
+    }
+    return g;
+  }
+
+  // qcqp_impl:777-785 -> linear_impl:254-275 with the 1-D reordering.
+  void recover(const std::vector<double>& x) {
+    for (int d = 0; d < D; ++d)
+      for (int i = 0; i < lp.np; ++i) lp.dp[d][i] = x[d * lp.np + i];
+    lp.updateSegmentsFromCompactConstraints();
+  }
+
+  // Primal-dual interior point (Mehrotra predictor-corrector) for
+  //   min 0.5 x^T P x + q^T x  s.t.  g_k(x) <= 0  (convex QCQP),
+  // replacing MSK_optimizetrm (qcqp_impl:700-712).
+  int solveIPM(double tol, int max_iter, std::vector<double>* xout, int* iters) {
+    Mat P;
+    std::vector<double> q;
+    objective(&P, &q);
+    const int n = npk;
+    const int m = static_cast<int>(cons.size());
+    // Start from the unconstrained minimiser P x = -q.
+    std::vector<double> x(n, 0.0);
+    {
+      Mat L = P;
+      if (!cholesky(&L)) return -20;
+      for (int i = 0; i < n; ++i) x[i] = -q[i];
+      cholesky_solve(L, &x);
+    }
+    std::vector<double> s(m), lam(m, 1.0), g(m);
+    for (int k = 0; k < m; ++k) {
+      g[k] = residual(cons[k], x);
+      s[k] = std::max(-g[k], 1.0);
+    }
+    double qnorm = 0.0;
+    for (int i = 0; i < n; ++i) qnorm = std::max(qnorm, std::fabs(q[i]));
+    int it = 0;
+    int status = 1;
+    std::vector<std::vector<double>> a(m);
+    for (it = 0; it < max_iter; ++it) {
+      // Gradients a_k = Q_k x + l_k on the support; residuals.
+      std::vector<double> rd(n, 0.0);
+      for (int i = 0; i < n; ++i) {
+        double s2 = q[i];
+        for (int j = 0; j < n; ++j) s2 += P(i, j) * x[j];
+        rd[i] = s2;
+      }
+      std::vector<double> rp(m);
+      double mu = 0.0;
+      for (int k = 0; k < m; ++k) {
+        const QConstraint& c = cons[k];
+        const int ms = static_cast<int>(c.supp.size());
+        a[k].assign(ms, 0.0);
+        for (int u = 0; u < ms; ++u) {
+          double v = c.lin[u];
+          for (int w = 0; w < ms; ++w) v += c.quad[static_cast<size_t>(u) * ms + w] * x[c.supp[w]];
+          a[k][u] = v;
+          rd[c.supp[u]] += lam[k] * v;
+        }
+        g[k] = residual(c, x);
+        rp[k] = g[k] + s[k];
+        mu += s[k] * lam[k];
+      }
+      mu /= std::max(m, 1);
+      double rdn = 0.0, rpn = 0.0;
+      for (int i = 0; i < n; ++i) rdn = std::max(rdn, std::fabs(rd[i]));
+      for (int k = 0; k < m; ++k) rpn = std::max(rpn, std::fabs(rp[k]));
+      if (rdn <= tol * (1.0 + qnorm) && rpn <= tol && mu <= tol) {
+        status = 0;
+        break;
+      }
+      // K = P + sum lam_k Q_k + sum (lam_k/s_k) a_k a_k^T.
+      Mat Kmat = P;
+      for (int k = 0; k < m; ++k) {
+        const QConstraint& c = cons[k];
+        const int ms = static_cast<int>(c.supp.size());
+        const double w = lam[k] / s[k];
+        for (int u = 0; u < ms; ++u)
+          for (int v = 0; v < ms; ++v)
+            Kmat(c.supp[u], c.supp[v]) +=
+                lam[k] * c.quad[static_cast<size_t>(u) * ms + v] + w * a[k][u] * a[k][v];
+      }
+      if (!cholesky(&Kmat)) return -21;
+      auto direction = [&](const std::vector<double>& rc, std::vector<double>* dx,
+                           std::vector<double>* dl, std::vector<double>* ds) {
+        std::vector<double> rhs(n);
+        for (int i = 0; i < n; ++i) rhs[i] = -rd[i];
+        for (int k = 0; k < m; ++k) {
+          const QConstraint& c = cons[k];
+          const double coef = (lam[k] * rp[k] - rc[k]) / s[k];
+          for (size_t u = 0; u < c.supp.size(); ++u) rhs[c.supp[u]] -= a[k][u] * coef;
+        }
+        cholesky_solve(Kmat, &rhs);
+        *dx = rhs;
+        dl->resize(m);
+        ds->resize(m);
+        for (int k = 0; k < m; ++k) {
+          const QConstraint& c = cons[k];
+          double adx = 0.0;
+          for (size_t u = 0; u < c.supp.size(); ++u) adx += a[k][u] * (*dx)[c.supp[u]];
+          (*dl)[k] = (lam[k] / s[k]) * (adx + rp[k]) - rc[k] / s[k];
+          (*ds)[k] = (-rc[k] - s[k] * (*dl)[k]) / lam[k];
+        }
+      };
+      auto max_step = [&](const std::vector<double>& dl, const std::vector<double>& ds) {
+        double alpha = 1.0;
+        for (int k = 0; k < m; ++k) {
+          if (ds[k] < 0) alpha = std::min(alpha, -s[k] / ds[k]);
+          if (dl[k] < 0) alpha = std::min(alpha, -lam[k] / dl[k]);
+        }
+        return alpha;
+      };
+      std::vector<double> rc(m), dx, dl, ds;
+      for (int k = 0; k < m; ++k) rc[k] = s[k] * lam[k];
+      direction(rc, &dx, &dl, &ds);
+      const double a_aff = max_step(dl, ds);
+      double mu_aff = 0.0;
+      for (int k = 0; k < m; ++k)
+        mu_aff += (s[k] + a_aff * ds[k]) * (lam[k] + a_aff * dl[k]);
+      mu_aff /= std::max(m, 1);
+      const double sigma = std::pow(mu_aff / mu, 3);
+      for (int k = 0; k < m; ++k) rc[k] = s[k] * lam[k] + ds[k] * dl[k] - sigma * mu;
+      direction(rc, &dx, &dl, &ds);
+      const double alpha = std::min(1.0, 0.99 * max_step(dl, ds));
+      for (int i = 0; i < n; ++i) x[i] += alpha * dx[i];
+      for (int k = 0; k < m; ++k) {
+        s[k] += alpha * ds[k];
+        lam[k] += alpha * dl[k];
+      }
+    }
+    *xout = x;
+    *iters = it;
+    return status;
+  }
+};
+
+int setupTube(int N, int D, int r, int S, int K, const uint8_t* mask,
+              const double* vals, const double* times_cp, const double* times,
+              const double* radii, TubeProblem* tp) {
+  if (!mask || !vals || !times || !times_cp || !radii || S < 1) return -1;
+  tp->lp.N = N;
+  tp->lp.D = D;
+  tp->radii.clear();
+  for (int i = 0; i < S; ++i) tp->radii.push_back({radii[2 * i], radii[2 * i + 1]});
+  std::vector<Vertex> vs = verticesFromDense(S, D, K, mask, vals);
+  for (int v = 0; v <= S; ++v)
+    if (!vs[v].constraints.count(0)) return -13;  // tube geometry needs positions
+  std::vector<double> tcp(times_cp, times_cp + S), t(times, times + S);
+  int rc = tp->setup(vs, tcp, t, r);
+  if (rc) return rc;
+  tp->buildConstraints();
+  return 0;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+extern "C" {
+
+int orc_base_coefficients(int n, double* out) {
+  if (n < 1 || n > kMaxConvolutionSize || !out) return -1;
+  const Mat& b = baseTable();
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) out[i * n + j] = b(i, j);
+  return 0;
+}
+
+int orc_base_coeffs_with_time(int N, int deriv, double t, double* out) {
+  if (N < 1 || N > kMaxConvolutionSize || deriv < 0 || deriv >= N || !out) return -1;
+  baseCoeffsWithTime(N, deriv, t, out);
+  return 0;
+}
+
+int orc_segment_matrices(int N, int r, double T, double* Q, double* A,
+                         double* Ainv, double* H) {
+  if (N < 2 || N % 2 || N > kMaxConvolutionSize || r < 0 || r >= N) return -1;
+  Mat q = computeQuadraticCostJacobian(N, r, T);
+  Mat a = setupMappingMatrix(N, T);
+  Mat ai = invertMappingMatrix(N, a);
+  Mat h = matmul(matmul(transpose(ai), q), ai);
+  if (Q) std::memcpy(Q, q.a.data(), sizeof(double) * N * N);
+  if (A) std::memcpy(A, a.a.data(), sizeof(double) * N * N);
+  if (Ainv) std::memcpy(Ainv, ai.a.data(), sizeof(double) * N * N);
+  if (H) std::memcpy(H, h.a.data(), sizeof(double) * N * N);
+  return 0;
+}
+
+// vertex.cpp:27-82.
+int orc_random_vertices(int max_deriv, int S, int D, const double* pos_min,
+                        const double* pos_max, uint64_t seed, int K,
+                        uint8_t* mask, double* vals) {
+  if (S < 1 || D < 1 || max_deriv < 1 || K < max_deriv + 1) return -1;
+  double span = 0.0;
+  for (int d = 0; d < D; ++d) span += (pos_max[d] - pos_min[d]) * (pos_max[d] - pos_min[d]);
+  if (std::sqrt(span) < 0.2) return -2;
+  std::mt19937 generator(static_cast<std::mt19937::result_type>(seed));
+  std::vector<std::uniform_real_distribution<double>> dist(D);
+  for (int d = 0; d < D; ++d)
+    dist[d] = std::uniform_real_distribution<double>(pos_min[d], pos_max[d]);
+  const double min_distance = 0.2;
+  std::memset(mask, 0, static_cast<size_t>(S + 1) * K);
+  std::memset(vals, 0, sizeof(double) * static_cast<size_t>(S + 1) * K * D);
+  std::vector<double> last(D), pos(D);
+  for (int d = 0; d < D; ++d) last[d] = dist[d](generator);
+  auto setc = [&](int v, int k, const std::vector<double>& val) {
+    mask[v * K + k] = 1;
+    for (int d = 0; d < D; ++d) vals[(static_cast<size_t>(v) * K + k) * D + d] = val[d];
+  };
+  // makeStartOrEnd (vertex.cpp:147-153).
+  auto start_or_end = [&](int v, const std::vector<double>& p) {
+    setc(v, 0, p);
+    std::vector<double> zero(D, 0.0);
+    for (int i = 1; i <= max_deriv; ++i) setc(v, i, zero);
+  };
+  start_or_end(0, last);
+  for (int v = 1; v <= S; ++v) {
+    while (true) {
+      for (int d = 0; d < D; ++d) pos[d] = dist[d](generator);
+      double dist2 = 0.0;
+      for (int d = 0; d < D; ++d) dist2 += (pos[d] - last[d]) * (pos[d] - last[d]);
+      if (std::sqrt(dist2) > min_distance) break;
+    }
+    setc(v, 0, pos);
+    last = pos;
+  }
+  start_or_end(S, last);
+  return 0;
+}
+
+int orc_estimate_segment_times(int S, int D, const double* positions,
+                               double v_max, double a_max, int method,
+                               double magic_or_factor, double* times) {
+  if (S < 1 || D < 1 || !positions || !times) return -1;
+  for (int i = 0; i < S; ++i) {
+    double dist2 = 0.0;
+    for (int d = 0; d < D; ++d) {
+      const double e = positions[(i + 1) * D + d] - positions[i * D + d];
+      dist2 += e * e;
+    }
+    const double distance = std::sqrt(dist2);
+    if (method == 0) {  // vertex.cpp:252-269
+      times[i] = distance / v_max * 2 *
+                 (1.0 + magic_or_factor * v_max / a_max * std::exp(-distance / v_max * 2));
+    } else {  // vertex.cpp:271-287 (+ time_factor, :233-250)
+      const double acc_time = v_max / a_max;
+      const double acc_distance = 0.5 * v_max * acc_time;
+      double t;
+      if (distance < 2.0 * acc_distance)
+        t = 2.0 * std::sqrt(distance / a_max);
+      else
+        t = 2.0 * acc_time + (distance - 2.0 * acc_distance) / v_max;
+      times[i] = t * magic_or_factor;
+    }
+  }
+  return 0;
+}
+
+int orc_linear_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
+                     const double* vals, const double* times, double* coeffs,
+                     double* cost, double* df, double* dp, int* nf, int* np) {
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
+  if (rc) return rc;
+  rc = lp.solveLinear();
+  if (coeffs) std::memcpy(coeffs, lp.coeffs.data(), sizeof(double) * lp.coeffs.size());
+  if (cost) *cost = lp.computeCost();
+  if (nf) *nf = lp.nf;
+  if (np) *np = lp.np;
+  for (int d = 0; d < D; ++d) {
+    if (df) std::memcpy(df + static_cast<size_t>(d) * lp.nf, lp.df[d].data(), sizeof(double) * lp.nf);
+    if (dp) std::memcpy(dp + static_cast<size_t>(d) * lp.np, lp.dp[d].data(), sizeof(double) * lp.np);
+  }
+  return rc;
+}
+
+int orc_linear_matrices(int N, int D, int r, int S, int K, const uint8_t* mask,
+                        const double* vals, const double* times, double* R,
+                        double* M, double* A, double* Ainv, double* Mpinv) {
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
+  if (rc) return rc;
+  const int nc = lp.nf + lp.np;
+  if (R) {
+    Mat Rm = lp.constructR();
+    std::memcpy(R, Rm.a.data(), sizeof(double) * nc * nc);
+  }
+  if (M) std::memcpy(M, lp.M.a.data(), sizeof(double) * lp.n_all * nc);
+  const int NS = N * S;
+  if (A || Ainv) {
+    if (A) std::memset(A, 0, sizeof(double) * NS * NS);
+    if (Ainv) std::memset(Ainv, 0, sizeof(double) * NS * NS);
+    for (int s = 0; s < S; ++s) {
+      Mat a = setupMappingMatrix(N, lp.times[s]);
+      for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) {
+          if (A) A[(s * N + i) * NS + s * N + j] = a(i, j);
+          if (Ainv) Ainv[(s * N + i) * NS + s * N + j] = lp.Ainv[s](i, j);
+        }
+    }
+  }
+  if (Mpinv) {  // linear_impl:546-555
+    Mat Mt = transpose(lp.M);
+    for (int i = 0; i < Mt.r; ++i) {
+      double sum = 0.0;
+      for (int j = 0; j < Mt.c; ++j) sum += Mt(i, j);
+      for (int j = 0; j < Mt.c; ++j) Mt(i, j) /= sum;
+    }
+    std::memcpy(Mpinv, Mt.a.data(), sizeof(double) * nc * lp.n_all);
+  }
+  return 0;
+}
+
+int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                  const double* vals, const double* times, double time_penalty,
+                  int grad_mode, double increment, double w_d, double w_t,
+                  double* cost, double* grad) {
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
+  if (rc) return rc;
+  auto objective = [&](LinearProblem& p, const std::vector<double>& t) {
+    p.updateSegmentTimes(t);
+    p.solveLinear();
+    double total = 0.0;
+    for (double v : t) total += v;  // nonlinear_impl:2768-2774
+    return p.computeCost() + total * total * time_penalty;
+  };
+  std::vector<double> t(times, times + S);
+  const double J = objective(lp, t);
+  if (cost) *cost = J;
+  if (grad_mode == 0 || !grad) return 0;
+  if (grad_mode == 1) {
+    // nonlinear_impl:2515-2574: d_p held at the solution for t.
+    for (int n = 0; n < S; ++n) {
+      std::vector<double> ts = t, tb = t;
+      ts[n] = ts[n] <= 0.1 ? 0.1 : ts[n] - increment;
+      tb[n] = tb[n] <= 0.1 ? 0.1 : tb[n] + increment;
+      lp.updateSegmentTimes(ts);
+      const double Js = lp.costDerivativeJd();
+      lp.updateSegmentTimes(tb);
+      const double Jb = lp.costDerivativeJd();
+      grad[n] = w_d * (Jb - Js) / (2.0 * increment) + w_t * 1.0;
+    }
+    lp.updateSegmentTimes(t);
+    return 0;
+  }
+  // grad_mode 2: central differences of the re-solved objective.
+  for (int n = 0; n < S; ++n) {
+    std::vector<double> ts = t, tb = t;
+    ts[n] = ts[n] <= 0.1 ? 0.1 : ts[n] - increment;
+    tb[n] = tb[n] <= 0.1 ? 0.1 : tb[n] + increment;
+    LinearProblem p2 = lp;
+    const double Js = objective(p2, ts);
+    const double Jb = objective(p2, tb);
+    grad[n] = (Jb - Js) / (2.0 * increment);
+  }
+  return 0;
+}
+
+int orc_control_point_map(int N, double T, double* Binv) {
+  if (N < 2 || N % 2 || N > 12 || !(T > 0) || !Binv) return -1;
+  Mat b = setupInverseControlPointMappingMatrix(N, T);
+  std::memcpy(Binv, b.a.data(), sizeof(double) * N * N);
+  return 0;
+}
+
+int orc_tube_num_constraints(int N, int S) {
+  return (S - 1) + S * (N - 2) + 2 * S * (N - 2);
+}
+
+int orc_tube_qcqp_assemble(int N, int D, int r, int S, int K,
+                           const uint8_t* mask, const double* vals,
+                           const double* times_cp, const double* times,
+                           const double* radii, double* P, double* q,
+                           double* quad, double* lin, double* cst, int* n_free) {
+  TubeProblem tp;
+  int rc = setupTube(N, D, r, S, K, mask, vals, times_cp, times, radii, &tp);
+  if (rc) return rc;
+  const int n = tp.npk;
+  if (n_free) *n_free = n;
+  Mat Pm;
+  std::vector<double> qv;
+  tp.objective(&Pm, &qv);
+  if (P) std::memcpy(P, Pm.a.data(), sizeof(double) * n * n);
+  if (q) std::memcpy(q, qv.data(), sizeof(double) * n);
+  const int m = static_cast<int>(tp.cons.size());
+  for (int k = 0; k < m; ++k) {
+    const QConstraint& c = tp.cons[k];
+    const int ms = static_cast<int>(c.supp.size());
+    if (quad) {
+      double* Qk = quad + static_cast<size_t>(k) * n * n;
+      std::memset(Qk, 0, sizeof(double) * n * n);
+      for (int a = 0; a < ms; ++a)
+        for (int b = 0; b < ms; ++b)
+          Qk[c.supp[a] * n + c.supp[b]] = c.quad[static_cast<size_t>(a) * ms + b];
+    }
+    if (lin) {
+      double* lk = lin + static_cast<size_t>(k) * n;
+      std::memset(lk, 0, sizeof(double) * n);
+      for (int a = 0; a < ms; ++a) lk[c.supp[a]] = c.lin[a];
+    }
+    if (cst) cst[k] = c.cst;
+  }
+  return 0;
+}
+
+int orc_tube_residuals(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times_cp,
+                       const double* times, const double* radii,
+                       const double* x, double* resid) {
+  TubeProblem tp;
+  int rc = setupTube(N, D, r, S, K, mask, vals, times_cp, times, radii, &tp);
+  if (rc) return rc;
+  std::vector<double> xv(x, x + tp.npk);
+  for (size_t k = 0; k < tp.cons.size(); ++k) resid[k] = tp.residual(tp.cons[k], xv);
+  return 0;
+}
+
+int orc_tube_qcqp_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
+                        const double* vals, const double* times_cp,
+                        const double* times, const double* radii, double tol,
+                        int max_iter, double* x_out, double* coeffs,
+                        double* cost, int* iters) {
+  TubeProblem tp;
+  int rc = setupTube(N, D, r, S, K, mask, vals, times_cp, times, radii, &tp);
+  if (rc) return rc;
+  std::vector<double> x;
+  int it = 0;
+  int status = tp.solveIPM(tol, max_iter, &x, &it);
+  if (status < 0) return status;
+  tp.recover(x);
+  if (x_out) std::memcpy(x_out, x.data(), sizeof(double) * x.size());
+  if (coeffs) std::memcpy(coeffs, tp.lp.coeffs.data(), sizeof(double) * tp.lp.coeffs.size());
+  if (cost) *cost = tp.lp.computeCost();
+  if (iters) *iters = it;
+  return status;
+}
+
+int orc_bench_linear(int N, int D, int r, int S, int K, int B, const uint8_t* masks,
+                     const double* vals, const double* times, int threads,
+                     double min_seconds, int64_t* solves, double* seconds) {
+  if (B < 1 || threads < 1 || !masks || !vals || !times) return -1;
+  std::atomic<int64_t> total(0);
+  std::atomic<int> failed(0);
+  volatile double sink = 0.0;
+  const size_t mstride = static_cast<size_t>(S + 1) * K;
+  auto t0 = std::chrono::steady_clock::now();
+  auto worker = [&](int tid) {
+    int64_t n = 0;
+    double acc = 0.0;
+    for (int64_t it = tid;; it += threads) {
+      const int b = static_cast<int>(it % B);
+      LinearProblem lp;
+      int rc = setupLinear(N, D, r, S, K, masks + b * mstride, vals + b * mstride * D,
+                           times + static_cast<size_t>(b) * S, &lp);
+      if (!rc) rc = lp.solveLinear();
+      if (rc) failed = 1;
+      acc += lp.computeCost();
+      ++n;
+      if ((n & 15) == 0) {
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el >= min_seconds) break;
+      }
+    }
+    total += n;
+    sink = sink + acc;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t) pool.emplace_back(worker, t);
+  for (auto& th : pool) th.join();
+  const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (solves) *solves = total.load();
+  if (seconds) *seconds = el;
+  return failed.load() ? -2 : 0;
+}
+
+}  // extern "C"

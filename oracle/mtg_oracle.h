@@ -1,0 +1,148 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY.
+//
+// CPU (FP64) restatement of the reference algorithm of
+// NilsFunk/mav_tube_trajectory_generation for the hot path named in
+// BASELINE.json `north_star` (linear minimum-derivative solve, tube QCQP
+// constraint assembly, time-allocation cost callback).  Every function cites
+// the reference file:line it follows (paths relative to the reference root;
+// "linear_impl" = include/mav_tube_trajectory_generation/impl/
+// polynomial_optimization_linear_impl.h, "qcqp_impl" / "nonlinear_impl"
+// likewise).
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+// load this library, and only as the checker / CPU baseline: the product path
+// (mav_tube_trajectory_generation_amd/, libmtg_hip.so) never links it.
+//
+// Parity pinning: the reference itself cannot be built here (Eigen, glog,
+// NLopt, MOSEK and supereight are absent).  The linear
+// restatement is pinned by the reference's own known-answer test
+// (TwoVerticesSetup, test/test_polynomial_optimization.cpp:707-751) and its
+// property tests (AMatrixInversion :695-705, ConstraintPacking :510-570,
+// checkPath :113-172, checkCost :174-195) — see tests/test_oracle.py.  The
+// QCQP solve (MOSEK in the reference) and the NLopt driver are "parity
+// unpinned": MOSEK is replaced by the oracle's own primal-dual interior-point
+// method, cross-checked against SciPy in tests.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// Falling-factorial table base(n, i) = i!/(i-n)! (polynomial.cpp:145-161),
+// n x n row-major.
+int orc_base_coefficients(int n, double* out);
+
+// Row `deriv` of the derivative basis at time t (polynomial.h:201-219).
+int orc_base_coeffs_with_time(int N, int deriv, double t, double* out);
+
+// Per-segment matrices for time T: Q (linear_impl:557-573), A
+// (linear_impl:101-111), A^-1 by the Schur complement (linear_impl:132-169),
+// H = A^-T Q A^-1 (linear_impl:318).  All N x N row-major; any may be NULL.
+int orc_segment_matrices(int N, int r, double T, double* Q, double* A,
+                         double* Ainv, double* H);
+
+// createRandomVertices (vertex.cpp:27-82) with std::mt19937(seed) and
+// std::uniform_real_distribution<double>.  Dense vertex form: mask[(v*K+k)]
+// = 1 when vertex v carries a constraint on derivative k, values at
+// vals[(v*K+k)*D + d].  K >= max_deriv+1.
+int orc_random_vertices(int max_deriv, int S, int D, const double* pos_min,
+                        const double* pos_max, uint64_t seed, int K,
+                        uint8_t* mask, double* vals);
+
+// estimateSegmentTimesNfabian (vertex.cpp:252-269; method 0) and
+// estimateSegmentTimesVelocityRamp (vertex.cpp:233-250, 271-287; method 1).
+// positions: (S+1) x D.
+int orc_estimate_segment_times(int S, int D, const double* positions,
+                               double v_max, double a_max, int method,
+                               double magic_or_factor, double* times);
+
+// Full linear path: setupFromVertices (linear_impl:46-99) + solveLinear
+// (:337-379) + computeCost (:113-130).  Vertex constraints given in the dense
+// form above with stride K (constraints of order > N/2-1 are dropped as in
+// linear_impl:72-95).  Outputs (any may be NULL):
+//   coeffs  S x D x N (segment, dimension, coefficient)
+//   cost    scalar
+//   df, dp  D x n_f, D x n_p compact fixed / free constraints
+//   nf, np  counts
+// Returns 0 on success, <0 on contract violation (the reference CHECK-aborts).
+int orc_linear_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
+                     const double* vals, const double* times, double* coeffs,
+                     double* cost, double* df, double* dp, int* nf, int* np);
+
+// Accessors of the linear problem (linear_impl:489-555): dense R
+// ((nf+np)^2), M (n_all x (nf+np)), A and A^-1 (NS x NS), M_pinv
+// ((nf+np) x n_all).  Sizes via orc_linear_solve's nf/np (n_all = N*S).
+int orc_linear_matrices(int N, int D, int r, int S, int K, const uint8_t* mask,
+                        const double* vals, const double* times, double* R,
+                        double* M, double* A, double* Ainv, double* Mpinv);
+
+// Time-allocation objective of objectiveFunctionTime (nonlinear_impl:877-945)
+// with w_c = 0 and no soft constraints, linear inner solve (upstream
+// semantics): J = computeCost() + time_penalty * (sum T)^2.
+// grad_mode 0: none; 1: getCostAndGradientTime (nonlinear_impl:2495-2584)
+//   = w_d * dJd/dT_n + w_t, J_d = d^T R d with d held fixed (:1537-1606);
+// 2: central differences of J itself (re-solved), increment and clamp rule of
+//   nonlinear_impl:2525-2530.
+int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                  const double* vals, const double* times, double time_penalty,
+                  int grad_mode, double increment, double w_d, double w_t,
+                  double* cost, double* grad);
+
+// ---------------- tube QCQP (qcqp_impl) ----------------
+// Inverse Bezier control-point map B^-1(T) with the 1e-5 zero-snap
+// (qcqp_impl:267-319), N x N row-major.
+int orc_control_point_map(int N, double T, double* Binv);
+
+// Number of inequality constraints the tube problem builds
+// (qcqp_impl:321-474): (S-1) spheres + S*(N-2) tubes + 2*S*(N-2) half-spaces.
+int orc_tube_num_constraints(int N, int S);
+
+// Assemble the tube QCQP exactly as setupFromVertices(radii) +
+// setupControlPointConstraints (qcqp_impl:121-186, 321-474) and return it in
+// dense form over the n_free_kDim = (S-1)*N/2*D free variables
+// (dim-major, qcqp_impl:95-117):
+//   P = 2 R_pp (n x n), q = 2 R_pf d_f (n), and per constraint k
+//   quad_k (n x n), lin_k (n), cst_k: 0.5 x^T quad_k x + lin_k x + cst_k <= 0.
+// times_cp = segment times used for the control-point maps (the reference
+// builds them once at setup, qcqp_impl:152-157); times = current segment
+// times (Q, A^-1).  Pass the same array twice for a fresh setup.
+// radii: S x 2 (tube radius r1 = .first, sphere radius r2 = .second).
+// Any output may be NULL; quad is large (ncon*n*n doubles).
+int orc_tube_qcqp_assemble(int N, int D, int r, int S, int K,
+                           const uint8_t* mask, const double* vals,
+                           const double* times_cp, const double* times,
+                           const double* radii, double* P, double* q,
+                           double* quad, double* lin, double* cst, int* n_free);
+
+// Residuals g_k(x) of the assembled constraints at free vector x
+// (length n_free_kDim).  resid: ncon.
+int orc_tube_residuals(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times_cp,
+                       const double* times, const double* radii,
+                       const double* x, double* resid);
+
+// Solve the tube QCQP (replaces MSK_optimizetrm, qcqp_impl:476-788) with the
+// oracle's primal-dual interior-point method, then recover coefficients
+// (qcqp_impl:777-785 -> linear_impl:254-275) and the cost.
+//   x_out: n_free_kDim; coeffs: S x D x N; cost: computeCost();
+//   iters: IPM iterations; returns 0 converged, 1 max-iterations, <0 error.
+int orc_tube_qcqp_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
+                        const double* vals, const double* times_cp,
+                        const double* times, const double* radii, double tol,
+                        int max_iter, double* x_out, double* coeffs,
+                        double* cost, int* iters);
+
+// CPU baseline timing (bench.py cpu_baseline leg): repeat setupFromVertices +
+// solveLinear + computeCost (the region polynomial_timing_evaluation.cpp:
+// 93-110 times) over B trajectories given in dense vertex form
+// (masks: B x (S+1) x K, vals: B x (S+1) x K x D, times: B x S), cycling
+// until at least min_seconds have elapsed, on `threads` std::threads.
+// Returns the number of solves and the wall seconds (steady_clock).
+int orc_bench_linear(int N, int D, int r, int S, int K, int B, const uint8_t* masks,
+                     const double* vals, const double* times, int threads,
+                     double min_seconds, int64_t* solves, double* seconds);
+
+#ifdef __cplusplus
+}
+#endif

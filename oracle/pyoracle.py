@@ -1,0 +1,231 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes view of oracle/liboracle.so, the FP64 CPU restatement of the
+reference's hot path (see oracle/mtg_oracle.h for the per-function reference
+citations).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg import this module; the product package never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+def build():
+    """Compile liboracle.so from oracle/mtg_oracle.cpp (g++ only)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        L = _lib
+        L.orc_base_coefficients.argtypes = [ctypes.c_int, _dp]
+        L.orc_base_coeffs_with_time.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _dp]
+        L.orc_segment_matrices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _dp, _dp, _dp, _dp]
+        L.orc_random_vertices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp,
+                                          ctypes.c_uint64, ctypes.c_int, _u8p, _dp]
+        L.orc_estimate_segment_times.argtypes = [ctypes.c_int, ctypes.c_int, _dp, ctypes.c_double,
+                                                 ctypes.c_double, ctypes.c_int, ctypes.c_double, _dp]
+        L.orc_linear_solve.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _ip]
+        L.orc_linear_matrices.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.orc_time_cost.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, ctypes.c_double, ctypes.c_int,
+                                                         ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                                         _dp, _dp]
+        L.orc_control_point_map.argtypes = [ctypes.c_int, ctypes.c_double, _dp]
+        L.orc_tube_num_constraints.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_tube_qcqp_assemble.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, _dp, _dp, _dp, _dp, _dp,
+                                                                  _dp, _dp, _ip]
+        L.orc_tube_residuals.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.orc_tube_qcqp_solve.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, _dp, _dp, ctypes.c_double,
+                                                               ctypes.c_int, _dp, _dp, _dp, _ip]
+    return _lib
+
+
+def _d(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise RuntimeError(f"oracle {what} failed with status {rc}")
+    return rc
+
+
+def base_coefficients(n=22):
+    out = np.zeros((n, n))
+    _check(lib().orc_base_coefficients(n, _d(out)), "base_coefficients")
+    return out
+
+
+def base_coeffs_with_time(N, deriv, t):
+    out = np.zeros(N)
+    _check(lib().orc_base_coeffs_with_time(N, deriv, t, _d(out)), "base_coeffs_with_time")
+    return out
+
+
+def segment_matrices(N, r, T):
+    Q, A, Ai, H = (np.zeros((N, N)) for _ in range(4))
+    _check(lib().orc_segment_matrices(N, r, T, _d(Q), _d(A), _d(Ai), _d(H)), "segment_matrices")
+    return Q, A, Ai, H
+
+
+class Vertices:
+    """Dense vertex constraints: mask[(S+1), K], vals[(S+1), K, D]."""
+
+    def __init__(self, mask, vals):
+        self.mask = np.ascontiguousarray(mask, dtype=np.uint8)
+        self.vals = np.ascontiguousarray(vals, dtype=np.float64)
+
+    @property
+    def S(self):
+        return self.mask.shape[0] - 1
+
+    @property
+    def K(self):
+        return self.mask.shape[1]
+
+    @property
+    def D(self):
+        return self.vals.shape[2]
+
+    def positions(self):
+        return np.ascontiguousarray(self.vals[:, 0, :])
+
+
+def random_vertices(max_deriv, S, D, pos_min, pos_max, seed, K=None):
+    K = K or (max_deriv + 1)
+    mask = np.zeros((S + 1, K), np.uint8)
+    vals = np.zeros((S + 1, K, D))
+    pmin = np.ascontiguousarray(np.broadcast_to(np.asarray(pos_min, float), (D,)))
+    pmax = np.ascontiguousarray(np.broadcast_to(np.asarray(pos_max, float), (D,)))
+    _check(lib().orc_random_vertices(max_deriv, S, D, _d(pmin), _d(pmax), seed, K,
+                                     mask.ctypes.data_as(_u8p), _d(vals)), "random_vertices")
+    return Vertices(mask, vals)
+
+
+def estimate_segment_times(vertices, v_max, a_max, method=0, magic=6.5):
+    pos = vertices.positions()
+    t = np.zeros(vertices.S)
+    _check(lib().orc_estimate_segment_times(vertices.S, vertices.D, _d(pos), v_max, a_max,
+                                            method, magic, _d(t)), "estimate_segment_times")
+    return t
+
+
+def linear_solve(N, r, vertices, times):
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    coeffs = np.zeros((S, D, N))
+    cost = np.zeros(1)
+    nf, np_ = ctypes.c_int(), ctypes.c_int()
+    n_all = (S + 1) * (N // 2)
+    df = np.zeros(D * n_all)
+    dp = np.zeros(D * n_all)
+    rc = lib().orc_linear_solve(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p), _d(vertices.vals),
+                                _d(times), _d(coeffs), _d(cost), _d(df), _d(dp),
+                                ctypes.byref(nf), ctypes.byref(np_))
+    _check(rc, "linear_solve")
+    nf, np_ = nf.value, np_.value
+    return dict(coeffs=coeffs, cost=float(cost[0]), df=df[:D * nf].reshape(D, nf),
+                dp=dp[:D * np_].reshape(D, np_), nf=nf, np=np_, status=rc)
+
+
+def linear_matrices(N, r, vertices, times):
+    S, D, K = vertices.S, vertices.D, vertices.K
+    sol = linear_solve(N, r, vertices, times)
+    nc = sol["nf"] + sol["np"]
+    NS = N * S
+    R = np.zeros((nc, nc))
+    M = np.zeros((NS, nc))
+    A = np.zeros((NS, NS))
+    Ai = np.zeros((NS, NS))
+    Mp = np.zeros((nc, NS))
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    _check(lib().orc_linear_matrices(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                     _d(vertices.vals), _d(times), _d(R), _d(M), _d(A), _d(Ai),
+                                     _d(Mp)), "linear_matrices")
+    return dict(R=R, M=M, A=A, Ainv=Ai, Mpinv=Mp, **sol)
+
+
+def time_cost(N, r, vertices, times, time_penalty=500.0, grad_mode=0, increment=0.1,
+              w_d=0.1, w_t=1.0):
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    cost = np.zeros(1)
+    grad = np.zeros(S)
+    _check(lib().orc_time_cost(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p), _d(vertices.vals),
+                               _d(times), time_penalty, grad_mode, increment, w_d, w_t, _d(cost),
+                               _d(grad)), "time_cost")
+    return float(cost[0]), (grad if grad_mode else None)
+
+
+def control_point_map(N, T):
+    B = np.zeros((N, N))
+    _check(lib().orc_control_point_map(N, T, _d(B)), "control_point_map")
+    return B
+
+
+def tube_num_constraints(N, S):
+    return lib().orc_tube_num_constraints(N, S)
+
+
+def tube_assemble(N, r, vertices, times, radii, times_cp=None, with_quad=True):
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    times_cp = times if times_cp is None else np.ascontiguousarray(times_cp, dtype=np.float64)
+    radii = np.ascontiguousarray(radii, dtype=np.float64).reshape(S, 2)
+    n = (S - 1) * (N // 2) * D
+    m = tube_num_constraints(N, S)
+    P = np.zeros((n, n))
+    q = np.zeros(n)
+    quad = np.zeros((m, n, n)) if with_quad else None
+    lin = np.zeros((m, n))
+    cst = np.zeros(m)
+    nfree = ctypes.c_int()
+    _check(lib().orc_tube_qcqp_assemble(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                        _d(vertices.vals), _d(times_cp), _d(times), _d(radii),
+                                        _d(P), _d(q), _d(quad), _d(lin), _d(cst),
+                                        ctypes.byref(nfree)), "tube_assemble")
+    return dict(P=P, q=q, quad=quad, lin=lin, cst=cst, n=nfree.value)
+
+
+def tube_residuals(N, r, vertices, times, radii, x, times_cp=None):
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    times_cp = times if times_cp is None else np.ascontiguousarray(times_cp, dtype=np.float64)
+    radii = np.ascontiguousarray(radii, dtype=np.float64).reshape(S, 2)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    res = np.zeros(tube_num_constraints(N, S))
+    _check(lib().orc_tube_residuals(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                    _d(vertices.vals), _d(times_cp), _d(times), _d(radii), _d(x),
+                                    _d(res)), "tube_residuals")
+    return res
+
+
+def tube_solve(N, r, vertices, times, radii, times_cp=None, tol=1e-10, max_iter=100):
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    times_cp = times if times_cp is None else np.ascontiguousarray(times_cp, dtype=np.float64)
+    radii = np.ascontiguousarray(radii, dtype=np.float64).reshape(S, 2)
+    n = (S - 1) * (N // 2) * D
+    x = np.zeros(n)
+    coeffs = np.zeros((S, D, N))
+    cost = np.zeros(1)
+    iters = ctypes.c_int()
+    rc = lib().orc_tube_qcqp_solve(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                   _d(vertices.vals), _d(times_cp), _d(times), _d(radii), tol,
+                                   max_iter, _d(x), _d(coeffs), _d(cost), ctypes.byref(iters))
+    _check(rc, "tube_solve")
+    return dict(x=x, coeffs=coeffs, cost=float(cost[0]), iters=iters.value, status=rc)

@@ -1,0 +1,158 @@
+"""CPU tests that pin the oracle (oracle/liboracle.so) to the reference.
+
+The reference cannot be built here, so the oracle is pinned by
+the reference's own known answers and property tests
+(test/test_polynomial_optimization.cpp) and by an independent NumPy
+restatement (tests/numpy_ref.py) plus the committed golden fixtures.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import numpy_ref
+from helpers import check_path, cost_numeric, rel_err, rel_err_coeffs, standard_vertices
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_two_vertices_known_answer(oracle):
+    """TwoVerticesSetup (test_polynomial_optimization.cpp:707-751): the Matlab
+    coefficients of the 1-D rest-to-rest 0 -> 5 m, T = 5 s snap solution."""
+    mask = np.ones((2, 5), np.uint8)
+    vals = np.zeros((2, 5, 1))
+    vals[1, 0, 0] = 5.0
+    sol = oracle.linear_solve(10, 4, oracle.Vertices(mask, vals), [5.0])
+    matlab = np.array([-0.000000000000004, 0.000000000000004, -0.000000000000006,
+                       0.000000000000003, -0.000000000000001, 0.201600000000015,
+                       -0.134400000000012, 0.034560000000004, -0.004032000000000,
+                       0.000179200000000])
+    assert sol["np"] == 0 and sol["nf"] == 10
+    assert np.max(np.abs(sol["coeffs"][0, 0] - matlab)) < 1e-13
+
+
+def test_base_coefficients(oracle):
+    """computeBaseCoefficients: base(n, i) = i!/(i-n)! (polynomial.cpp:145-161)."""
+    B = oracle.base_coefficients(22)
+    for n in range(22):
+        for i in range(22):
+            assert B[n, i] == numpy_ref.falling(n, i)
+
+
+@pytest.mark.parametrize("N", [4, 6, 8, 10])
+def test_a_matrix_inversion(oracle, N):
+    """AMatrixInversion (test_polynomial_optimization.cpp:695-705), 1e-10
+    (the reference runs it for its N = 10; at N = 12 numpy's dense inverse
+    itself is only ~1e-8 accurate at T = 1)."""
+    for t in np.arange(1.0, 61.0):
+        _, A, Ai, _ = oracle.segment_matrices(N, N // 2 - 1, t)
+        assert np.array_equal(A, numpy_ref.mapping_matrix(N, t))
+        assert np.max(np.abs(Ai - np.linalg.inv(A))) < 1e-10, t
+
+
+def test_constraint_packing(oracle):
+    """ConstraintPacking (test_polynomial_optimization.cpp:510-570): [d_f; d_p]
+    -> p = A^-1 M d -> M_pinv A p round trip, p equals segment coefficients."""
+    for D, S in ((1, 10), (3, 10), (3, 5)):
+        for i in range(4):
+            v = oracle.random_vertices(4, S, D, -50.0, 50.0, 12345 + i)
+            t = oracle.estimate_segment_times(v, 3.0, 5.0)
+            m = oracle.linear_matrices(10, 4, v, t)
+            for d in range(D):
+                d_all = np.concatenate([m["df"][d], m["dp"][d]])
+                p = m["Ainv"] @ m["M"] @ d_all
+                back = m["Mpinv"] @ (m["A"] @ p)
+                assert np.max(np.abs(back - d_all)) < 1e-6
+                for s in range(S):
+                    assert np.max(np.abs(p[s * 10:(s + 1) * 10] - m["coeffs"][s, d])) < 1e-6
+
+
+REF_PARAMS = [
+    (1, 4, 1, 100, 3.0, 5.0), (1, 4, 10, 102, 3.0, 5.0), (1, 4, 50, 103, 3.0, 5.0),
+    (3, 4, 1, 104, 3.0, 5.0), (3, 4, 10, 105, 3.0, 5.0), (3, 4, 50, 106, 3.0, 5.0),
+    (3, 4, 75, 106, 3.0, 5.0), (1, 2, 5, 107, 1.0, 2.0), (3, 2, 1, 108, 1.0, 2.0),
+    (3, 2, 5, 109, 1.0, 2.0), (3, 3, 5, 110, 1.0, 2.0),
+]
+
+
+@pytest.mark.parametrize("D,r,S,seed,vmax,amax", REF_PARAMS)
+def test_reference_fixture_properties(oracle, D, r, S, seed, vmax, amax):
+    """checkPath + checkCost (test_polynomial_optimization.cpp:113-195) and
+    VertexGeneration (:249-268) on the reference's parameter sets."""
+    v = standard_vertices(10, S, D, seed)
+    assert v.mask[0].sum() == 5 and v.mask[-1].sum() == 5
+    assert np.all(np.abs(v.vals[:, 0, :]) <= 10.0)
+    t = oracle.estimate_segment_times(v, vmax, amax)
+    sol = oracle.linear_solve(10, r, v, t)
+    check_path(v, sol["coeffs"], t, 10)
+    if S <= 10:
+        num = cost_numeric(sol["coeffs"], t, r)
+        assert abs(num - sol["cost"]) <= 0.1 * num
+
+
+@pytest.mark.parametrize("D,r,S,seed,vmax,amax", REF_PARAMS[:9])
+def test_numpy_cross_check(oracle, D, r, S, seed, vmax, amax):
+    """Oracle vs the independent NumPy restatement (dense KKT)."""
+    v = standard_vertices(10, S, D, seed)
+    t = oracle.estimate_segment_times(v, vmax, amax)
+    sol = oracle.linear_solve(10, r, v, t)
+    c, cost = numpy_ref.solve_linear(10, r, v.mask[:, :5], v.vals[:, :5, :], t)
+    assert rel_err_coeffs(sol["coeffs"], c) <= 1e-7
+    assert rel_err(sol["cost"], cost) <= 1e-7
+
+
+@pytest.mark.parametrize("seed", [0, 1, 105, 4242, 2**31 + 5])
+def test_generator_matches_libstdcxx_semantics(oracle, seed):
+    """createRandomVertices positions vs a pure-Python std::mt19937 +
+    generate_canonical<double, 53> emulation (bit-exact)."""
+    v = oracle.random_vertices(4, 10, 3, -10.0, 10.0, seed & 0xFFFFFFFF)
+    ref = numpy_ref.random_positions(10, 3, -10.0, 10.0, seed & 0xFFFFFFFF)
+    assert np.array_equal(v.positions(), ref)
+
+
+def test_time_estimates(oracle):
+    """estimateSegmentTimesNfabian / VelocityRamp formulas (vertex.cpp:252-287)."""
+    v = standard_vertices(10, 6, 3, 7)
+    p = v.positions()
+    d = np.linalg.norm(np.diff(p, axis=0), axis=1)
+    t0 = oracle.estimate_segment_times(v, 3.0, 5.0)
+    assert np.allclose(t0, d / 3.0 * 2 * (1.0 + 6.5 * 3.0 / 5.0 * np.exp(-d / 3.0 * 2)),
+                       rtol=1e-15)
+    t1 = oracle.estimate_segment_times(v, 3.0, 5.0, method=1, magic=1.0)
+    acc_t, acc_d = 3.0 / 5.0, 0.5 * 3.0 * 3.0 / 5.0
+    exp = np.where(d < 2 * acc_d, 2 * np.sqrt(d / 5.0), 2 * acc_t + (d - 2 * acc_d) / 3.0)
+    assert np.allclose(t1, exp, rtol=1e-15)
+
+
+def test_time_cost_modes(oracle):
+    """objectiveFunctionTime value and the two gradient forms are consistent:
+    mode 2 (re-solved central differences) ~ analytic envelope derivative,
+    mode 1 = w_d dJ_d/dT + w_t with fixed d (getCostAndGradientTime)."""
+    v = standard_vertices(10, 5, 3, 105)
+    t = oracle.estimate_segment_times(v, 3.0, 5.0)
+    J0, _ = oracle.time_cost(10, 4, v, t)
+    sol = oracle.linear_solve(10, 4, v, t)
+    assert abs(J0 - (sol["cost"] + 500.0 * t.sum() ** 2)) <= 1e-12 * J0
+    _, g2 = oracle.time_cost(10, 4, v, t, grad_mode=2, increment=1e-4)
+    # Envelope theorem: d(min_x J)/dT = dJ/dT at fixed x, so mode 1 with
+    # w_d = 0.5 (J_d = 2 computeCost) and w_t = 0 plus the penalty
+    # derivative equals mode 2 up to O(increment^2).
+    _, g1 = oracle.time_cost(10, 4, v, t, grad_mode=1, increment=1e-4, w_d=0.5, w_t=0.0)
+    pen = 2 * 500.0 * t.sum()
+    assert np.allclose(g1 + pen, g2, rtol=1e-5, atol=1e-6 * np.abs(g2).max())
+
+
+def test_golden_fixtures(oracle):
+    """Committed fixtures (tests/golden/make_golden.py) reproduce."""
+    path = os.path.join(GOLDEN, "linear_golden.json")
+    with open(path) as f:
+        cases = json.load(f)["cases"]
+    assert cases
+    for c in cases:
+        mask = np.array(c["mask"], np.uint8)
+        vals = np.array(c["vals"])
+        t = np.array(c["times"])
+        sol = oracle.linear_solve(c["N"], c["r"], oracle.Vertices(mask, vals), t)
+        assert rel_err_coeffs(sol["coeffs"], np.array(c["coeffs"])) <= 1e-12, c["name"]
+        assert rel_err(sol["cost"], c["cost"]) <= 1e-12, c["name"]

@@ -1,0 +1,114 @@
+"""GPU parity of the time-allocation cost callback and the batched segment
+time optimiser (mtg_time_cost / mtg_time_optimize) against the oracle."""
+import numpy as np
+import pytest
+
+from helpers import rel_err, standard_vertices
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+N, D, R = 10, 3, 4
+
+
+def _batch(S, B, seed0):
+    import mav_tube_trajectory_generation_amd as mtg
+    return mtg.generate_random_problems(N, D, S, B, seed0=seed0)
+
+
+@pytest.mark.parametrize("grad_mode", [0, 1, 2])
+def test_time_cost_vs_oracle(ctx, dev, oracle, grad_mode):
+    """objectiveFunctionTime (nonlinear_impl:877-945) with the gradient forms
+    of getCostAndGradientTime (:2495-2584)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    S, B = 8, 16
+    mask, fixed, times, _ = _batch(S, B, 500)
+    times[3, 2] = 0.1   # exercise the clamp rule (nonlinear_impl:2529-2530)
+    times[5, 0] = 0.07
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    out = plan.time_cost(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev),
+                         grad_mode=grad_mode, increment=0.1, w_d=0.1, w_t=1.0)
+    cost = out["cost"].cpu().numpy()
+    assert (out["status"].cpu().numpy() == 0).all()
+    for b in range(B):
+        v = standard_vertices(N, S, D, 500 + b)
+        J, g = oracle.time_cost(N, R, v, times[b], grad_mode=grad_mode, increment=0.1,
+                                w_d=0.1, w_t=1.0)
+        # A segment time of 0.1 s makes A(T) ill-conditioned (cond ~1e10):
+        # the reference-faithful oracle then carries ~1e-7 relative error in
+        # J, which central differences amplify by J / (2 increment).
+        well = times[b].min() > 0.5
+        assert rel_err(cost[b], J) <= (1e-9 if well else 1e-6), b
+        if grad_mode:
+            gg = out["grad"].cpu().numpy()[b]
+            tol = 1e-6 if (well or grad_mode == 1) else 1e-4
+            assert np.max(np.abs(gg - g)) <= tol * np.max(np.abs(g)) + 1e-9, (b, gg, g)
+
+
+def _optimize_reference(oracle, v, t0, max_evals, time_penalty=500.0, inc=0.1):
+    """The optimiser of time_optimize_kernel restated on the oracle objective:
+    projected scaled steepest descent, expand x1.5 / backtrack x0.5."""
+    T0 = np.array(t0, float)
+    T = T0.copy()
+    f, _ = oracle.time_cost(N, R, v, T, time_penalty=time_penalty)
+    _, g = oracle.time_cost(N, R, v, T, time_penalty=time_penalty, grad_mode=2, increment=inc)
+    evals, alpha = 1, 0.1
+    while evals < max_evals and alpha > 1e-9:
+        gmax = np.max(np.abs(g * T0))
+        if not gmax > 0:
+            break
+        trial = np.clip(T - alpha * T0 * (g * T0) / gmax, 0.1, 2.0 * T0)
+        if np.array_equal(trial, T):
+            break
+        ft, _ = oracle.time_cost(N, R, v, trial, time_penalty=time_penalty)
+        evals += 1
+        if ft < f:
+            T, f = trial, ft
+            alpha = min(alpha * 1.5, 1.0)
+            _, g = oracle.time_cost(N, R, v, T, time_penalty=time_penalty, grad_mode=2,
+                                    increment=inc)
+        else:
+            alpha *= 0.5
+    return T, f, evals
+
+
+def test_time_optimize_vs_reference_driver(ctx, dev, oracle):
+    import mav_tube_trajectory_generation_amd as mtg
+    S, B, E = 6, 8, 20
+    mask, fixed, times, _ = _batch(S, B, 900)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    out = plan.time_optimize(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev),
+                             max_evals=E)
+    T = out["times"].cpu().numpy()
+    cost = out["cost"].cpu().numpy()
+    evals = out["evals"].cpu().numpy()
+    for b in range(B):
+        v = standard_vertices(N, S, D, 900 + b)
+        Tr, fr, er = _optimize_reference(oracle, v, times[b], E)
+        assert evals[b] == er, b
+        assert np.max(np.abs(T[b] - Tr) / Tr) <= 1e-6, (b, T[b], Tr)
+        assert rel_err(cost[b], fr) <= 1e-6, b
+
+
+def test_time_optimize_properties(ctx, dev, oracle):
+    """BASELINE config 5 shape (reduced batch): 50 evaluations, bounds
+    [0.1, 2 T0] (nonlinear_impl:350-378), monotone objective."""
+    import mav_tube_trajectory_generation_amd as mtg
+    S, B = 10, 256
+    mask, fixed, times, _ = _batch(S, B, 105)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    fd = torch.from_numpy(fixed).to(dev)
+    td = torch.from_numpy(times).to(dev)
+    c0 = plan.time_cost(fd, td)["cost"].cpu().numpy()
+    out = plan.time_optimize(fd, td, max_evals=50)
+    T = out["times"].cpu().numpy()
+    c1 = out["cost"].cpu().numpy()
+    assert (out["status"].cpu().numpy() == 0).all()
+    assert np.all(out["evals"].cpu().numpy() <= 50)
+    assert np.all(T >= 0.1 - 1e-15) and np.all(T <= 2 * times + 1e-12)
+    assert np.all(c1 <= c0)
+    assert np.mean(c1 / c0) < 0.9
+    # The reported cost is the objective at the returned times.
+    chk = plan.time_cost(fd, out["times"])["cost"].cpu().numpy()
+    assert np.allclose(chk, c1, rtol=1e-12)
