@@ -41,11 +41,11 @@ struct Layout {
   int pw;          // S * (2N-1): T_s^e for e in [-(N-1), N-1]
   int T;           // S segment times
   int dv;          // (S+1)*M*D vertex derivatives (fixed values, then x)
-  int L;           // (S+1)*M*M Cholesky factors
-  int W;           // S*M*M     L_v^-1 * O_v
-  int Y;           // (S+1)*M*D forward solutions
-  int Sv, Ov, Rv;  // per-step workspace
-  int red;         // 64 reduction scratch
+  int Dt;          // (S+1)*M*M pinned diagonal blocks -> Schur complements
+  int Ot;          // S*M*M     pinned coupling blocks -> W_v = L_v^-1 O_v
+  int Bt;          // (S+1)*M*D right-hand sides -> y_v = L_v^-1 r_v
+  int Lu;          // (S+1)*M*M unit-lower LDL^T factors
+  int dinv;        // (S+1)*M   inverse pivots
   int aux;         // 4*S extra (optimiser state)
   int ndouble;
   int slot;        // (S+1)*M int slots (after the doubles)
@@ -62,18 +62,26 @@ __host__ __device__ inline Layout make_layout(int N, int S, int D) {
   l.pw = o;   o += S * (2 * N - 1);
   l.T = o;    o += S;
   l.dv = o;   o += (S + 1) * M * D;
-  l.L = o;    o += (S + 1) * M * M;
-  l.W = o;    o += S * M * M;
-  l.Y = o;    o += (S + 1) * M * D;
-  l.Sv = o;   o += M * M;
-  l.Ov = o;   o += M * M;
-  l.Rv = o;   o += M * kMaxD;
-  l.red = o;  o += kWave;
+  l.Dt = o;   o += (S + 1) * M * M;
+  l.Ot = o;   o += S * M * M;
+  l.Bt = o;   o += (S + 1) * M * D;
+  l.Lu = o;   o += (S + 1) * M * M;
+  l.dinv = o; o += (S + 1) * M;
   l.aux = o;  o += 4 * S + 8;
   l.ndouble = o;
   l.slot = 0;
   l.nint = (S + 1) * M + 4;
   return l;
+}
+
+// 1/d to full FP64 accuracy: v_rcp_f64 seed + two Newton steps (no IEEE
+// division sequence on the serial chain).
+__device__ inline double rcp64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
 }
 
 // Per-trajectory solver state living in LDS.  Every method is called by all
@@ -93,9 +101,6 @@ struct Traj {
   __device__ double* pw() const { return sm + lay->pw; }
   __device__ double* T() const { return sm + lay->T; }
   __device__ double* dv() const { return sm + lay->dv; }
-  __device__ double* Lf() const { return sm + lay->L; }
-  __device__ double* W() const { return sm + lay->W; }
-  __device__ double* Y() const { return sm + lay->Y; }
   __device__ int* slot() const { return si + lay->slot; }
   __device__ int* flag() const { return si + (S + 1) * M; }
 
@@ -118,7 +123,7 @@ struct Traj {
   }
 
   // Powers T_s^e by repeated multiplication (exact integer exponents).
-  // Returns via flag()[0] |= 1 if any time is not > 0.
+  // Sets flag()[0] |= 1 if any time is not > 0.
   __device__ void compute_powers() {
     for (int i = lane; i < S * PWN; i += kWave) {
       const int s = i / PWN;
@@ -158,137 +163,166 @@ struct Traj {
     return dv()[(v * M + k) * D + d];
   }
 
-  // Block-tridiagonal Cholesky forward sweep + back substitution.  On exit
-  // dv holds every vertex derivative (fixed values untouched bit-for-bit).
+  // Phase C (parallel over all vertices): pinned diagonal blocks, pinned
+  // coupling blocks and right-hand sides b = -R_pf d_f, so the serial sweep
+  // below only does Schur updates and factorisations.
+  __device__ void assemble() {
+    double* Dt = sm + lay->Dt;
+    double* Ot = sm + lay->Ot;
+    double* Bt = sm + lay->Bt;
+    for (int i = lane; i < (S + 1) * M * M; i += kWave) {
+      const int v = i / (M * M);
+      const int j = (i / M) % M, k = i % M;
+      double val;
+      if (fixed_at(v, j) || fixed_at(v, k)) {
+        val = (j == k) ? 1.0 : 0.0;
+      } else {
+        val = 0.0;
+        if (v > 0) val += H(v - 1, 1, 1, j, k);
+        if (v < S) val += H(v, 0, 0, j, k);
+      }
+      Dt[i] = val;
+    }
+    for (int i = lane; i < S * M * M; i += kWave) {
+      const int v = i / (M * M);
+      const int j = (i / M) % M, k = i % M;
+      Ot[i] = (fixed_at(v, j) || fixed_at(v + 1, k)) ? 0.0 : H(v, 0, 1, j, k);
+    }
+    for (int i = lane; i < (S + 1) * M * D; i += kWave) {
+      const int v = i / (M * D);
+      const int j = (i / D) % M, d = i % D;
+      double val;
+      if (fixed_at(v, j)) {
+        val = dval(v, j, d);
+      } else {
+        // dv is zero at free entries, so these sums run over fixed columns.
+        double b = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          double dkk = 0.0;
+          if (v > 0) dkk += H(v - 1, 1, 1, j, k);
+          if (v < S) dkk += H(v, 0, 0, j, k);
+          b += dkk * dval(v, k, d);
+          if (v < S) b += H(v, 0, 1, j, k) * dval(v + 1, k, d);
+          if (v > 0) b += H(v - 1, 1, 0, j, k) * dval(v - 1, k, d);
+        }
+        val = -b;
+      }
+      Bt[i] = val;
+    }
+  }
+
+  // Block LDL^T forward sweep over the S+1 vertices, then back substitution.
+  // On exit dv holds every vertex derivative (fixed values untouched).
   // Sets flag()[0] |= 2 on a non-positive pivot.
   __device__ void solve() {
-    double* Sv = sm + lay->Sv;
-    double* Ov = sm + lay->Ov;
-    double* Rv = sm + lay->Rv;
+    double* Dt = sm + lay->Dt;
+    double* Ot = sm + lay->Ot;
+    double* Bt = sm + lay->Bt;
+    double* Lu = sm + lay->Lu;
+    double* dinv = sm + lay->dinv;
+    assemble();
+    __syncthreads();
     for (int v = 0; v <= S; ++v) {
-      const double* Wp = W() + (v - 1) * M * M;  // valid for v > 0
-      const double* Yp = Y() + (v - 1) * M * D;
-      if (lane < M * M) {
-        const int j = lane / M, k = lane % M;
-        const bool fj = fixed_at(v, j), fk = fixed_at(v, k);
-        double sval;
-        if (fj || fk) {
-          sval = (j == k) ? 1.0 : 0.0;
-        } else {
-          sval = 0.0;
-          if (v > 0) sval += H(v - 1, 1, 1, j, k);
-          if (v < S) sval += H(v, 0, 0, j, k);
-          if (v > 0) {
+      double* Sv = Dt + v * M * M;
+      double* Rv = Bt + v * M * D;
+      if (v > 0) {
+        // Schur update with the previous vertex:
+        //   S_v = Dt_v - W^T diag(dinv) W,  r_v = b_v - W^T diag(dinv) y.
+        const double* Wp = Ot + (v - 1) * M * M;
+        const double* Yp = Bt + (v - 1) * M * D;
+        const double* dp = dinv + (v - 1) * M;
+        if (lane < M * M) {
+          const int j = lane / M, k = lane % M;
+          double s = Sv[lane];
 #pragma unroll
-            for (int m = 0; m < M; ++m) sval -= Wp[m * M + j] * Wp[m * M + k];
-          }
-        }
-        Sv[j * M + k] = sval;
-        if (v < S) {
-          const bool pin = fj || fixed_at(v + 1, k);
-          Ov[j * M + k] = pin ? 0.0 : H(v, 0, 1, j, k);
-        }
-      } else if (lane < M * M + M * D) {
-        const int idx = lane - M * M;
-        const int j = idx / D, d = idx % D;
-        double rv;
-        if (fixed_at(v, j)) {
-          rv = dval(v, j, d);
-        } else {
-          double b = 0.0;
+          for (int m = 0; m < M; ++m) s -= Wp[m * M + j] * dp[m] * Wp[m * M + k];
+          Sv[lane] = s;
+        } else if (lane < M * M + M * D) {
+          const int idx = lane - M * M;
+          const int j = idx / D, d = idx % D;
+          double s = Rv[idx];
 #pragma unroll
-          for (int k = 0; k < M; ++k) {
-            double dkk = 0.0;
-            if (v > 0) dkk += H(v - 1, 1, 1, j, k);
-            if (v < S) dkk += H(v, 0, 0, j, k);
-            b += dkk * dval(v, k, d);
-            if (v < S) b += H(v, 0, 1, j, k) * dval(v + 1, k, d);
-            if (v > 0) b += H(v - 1, 1, 0, j, k) * dval(v - 1, k, d);
-          }
-          rv = -b;
-          if (v > 0) {
-#pragma unroll
-            for (int m = 0; m < M; ++m) rv -= Wp[m * M + j] * Yp[m * D + d];
-          }
+          for (int m = 0; m < M; ++m) s -= Wp[m * M + j] * dp[m] * Yp[m * D + d];
+          Rv[idx] = s;
         }
-        Rv[j * D + d] = rv;
+        __syncthreads();
       }
-      __syncthreads();
-      // Lane -> column: 0..M-1 the coupling block W_v (absent at v = S),
-      // then the D right-hand sides.
+      // Lane -> column: 0..M-1 the coupling block (absent at v = S), then
+      // the D right-hand sides.  Each active lane factors S_v = L Delta L^T
+      // in registers (redundantly) and forward-substitutes its column.
       int col;
       if (v < S)
         col = lane < M + D ? lane : -1;
       else
         col = lane < D ? M + lane : -1;
       if (col >= 0) {
-        // Cholesky of Sv in registers (lower triangle).
         double Lr[M][M];
+        double inv[M];
 #pragma unroll
         for (int i = 0; i < M; ++i)
 #pragma unroll
-          for (int j = 0; j < M; ++j) Lr[i][j] = (j <= i) ? Sv[i * M + j] : 0.0;
+          for (int j = 0; j <= i; ++j) Lr[i][j] = Sv[i * M + j];
         bool ok = true;
 #pragma unroll
         for (int j = 0; j < M; ++j) {
+          // Lr[i][k] for k < j holds L[i][k] * delta_k (scaled column).
           double dj = Lr[j][j];
 #pragma unroll
-          for (int k = 0; k < j; ++k) dj -= Lr[j][k] * Lr[j][k];
+          for (int k = 0; k < j; ++k) dj -= Lr[j][k] * (Lr[j][k] * inv[k]);
           ok = ok && (dj > 0.0);
-          dj = sqrt(dj > 0.0 ? dj : 1.0);
-          Lr[j][j] = dj;
-          const double inv = 1.0 / dj;
+          inv[j] = rcp64(dj > 0.0 ? dj : 1.0);
 #pragma unroll
           for (int i = j + 1; i < M; ++i) {
             double s = Lr[i][j];
 #pragma unroll
-            for (int k = 0; k < j; ++k) s -= Lr[i][k] * Lr[j][k];
-            Lr[i][j] = s * inv;
+            for (int k = 0; k < j; ++k) s -= Lr[i][k] * (Lr[j][k] * inv[k]);
+            Lr[i][j] = s;  // = L[i][j] * delta_j
           }
         }
         if (!ok) atomicOr(&flag()[0], 2);
-        if (lane == 0) {
-          double* Lv = Lf() + v * M * M;
-#pragma unroll
-          for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = 0; j < M; ++j) Lv[i * M + j] = Lr[i][j];
-        }
-        // Forward substitution on one column.
+        // Unit-lower L[i][j] = Lr[i][j] * inv[j].
         double x[M];
         const bool isW = col < M;
 #pragma unroll
-        for (int i = 0; i < M; ++i)
-          x[i] = isW ? Ov[i * M + col] : Rv[i * D + (col - M)];
+        for (int i = 0; i < M; ++i) x[i] = isW ? Ot[v * M * M + i * M + col] : Rv[i * D + (col - M)];
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           double s = x[i];
 #pragma unroll
-          for (int k = 0; k < i; ++k) s -= Lr[i][k] * x[k];
-          x[i] = s / Lr[i][i];
+          for (int k = 0; k < i; ++k) s -= (Lr[i][k] * inv[k]) * x[k];
+          x[i] = s;
         }
         if (isW) {
-          double* Wv = W() + v * M * M;
 #pragma unroll
-          for (int i = 0; i < M; ++i) Wv[i * M + col] = x[i];
+          for (int i = 0; i < M; ++i) Ot[v * M * M + i * M + col] = x[i];
         } else {
-          double* Yv = Y() + v * M * D;
 #pragma unroll
-          for (int i = 0; i < M; ++i) Yv[i * D + (col - M)] = x[i];
+          for (int i = 0; i < M; ++i) Rv[i * D + (col - M)] = x[i];
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            dinv[v * M + i] = inv[i];
+#pragma unroll
+            for (int j = 0; j < i; ++j) Lu[v * M * M + i * M + j] = Lr[i][j] * inv[j];
+          }
         }
       }
       __syncthreads();
     }
-    // Back substitution: x_v = L_v^-T (y_v - W_v x_{v+1}), one lane per dim.
+    // Back substitution x_v = L_v^-T diag(dinv_v) (y_v - W_v x_{v+1}), one
+    // lane per dimension.
     if (lane < D) {
       const int d = lane;
       double xn[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) xn[i] = 0.0;
       for (int v = S; v >= 0; --v) {
-        const double* Lv = Lf() + v * M * M;
-        const double* Wv = W() + v * M * M;
-        const double* Yv = Y() + v * M * D;
+        const double* L = Lu + v * M * M;
+        const double* Wv = Ot + v * M * M;
+        const double* Yv = Bt + v * M * D;
+        const double* di = dinv + v * M;
         double t[M];
 #pragma unroll
         for (int i = 0; i < M; ++i) {
@@ -297,49 +331,24 @@ struct Traj {
 #pragma unroll
             for (int k = 0; k < M; ++k) s -= Wv[i * M + k] * xn[k];
           }
-          t[i] = s;
+          t[i] = s * di[i];
         }
 #pragma unroll
         for (int i = M - 1; i >= 0; --i) {
           double s = t[i];
 #pragma unroll
-          for (int k = i + 1; k < M; ++k) s -= Lv[k * M + i] * t[k];
-          t[i] = s / Lv[i * M + i];
+          for (int k = i + 1; k < M; ++k) s -= L[k * M + i] * t[k];
+          t[i] = s;
         }
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           xn[i] = t[i];
-          // Fixed entries come back as their pinned value exactly; keep the
-          // original bits anyway (no-op in exact arithmetic).
+          // Pinned entries come back as their value; keep the input bits.
           if (!fixed_at(v, i)) dv()[(v * M + i) * D + d] = t[i];
         }
       }
     }
     __syncthreads();
-  }
-
-  // c_s[d][k] = sum_j A(1)^-1[k][j] T_s^(j mod M - k) e_j, e = [x_s; x_{s+1}].
-  __device__ double coeff(int s, int d, int k) const {
-    double c = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const int l = j % M;
-      const int v = s + j / M;
-      c += tabA()[k * N + j] * pwr(s, l - k) * dval(v, l, d);
-    }
-    return c;
-  }
-
-  // Write B x S x D x N coefficients for this trajectory (coalesced).
-  __device__ void write_coeffs(double* __restrict__ out) const {
-    const int n = S * D * N;
-    for (int i = lane; i < n; i += kWave) {
-      const int s = i / (D * N);
-      const int rem = i % (D * N);
-      const int d = rem / N;
-      const int k = rem % N;
-      out[i] = coeff(s, d, k);
-    }
   }
 
   // Wave-wide sum (all 64 lanes receive it).
@@ -349,30 +358,36 @@ struct Traj {
     return x;
   }
 
-  // Quadratic form of segment s for dimension d: e^T H_s e.
-  __device__ double seg_quad(int s, int d, int a) const {
-    // Row a of H_s times e, times e_a.
-    const int la = a % M, va = s + a / M;
-    double h = 0.0;
-#pragma unroll
-    for (int b = 0; b < N; ++b) {
-      const int lb = b % M, vb = s + b / M;
-      h += tabH()[a * N + b] * pwr(s, 1 - 2 * r + la + lb) * dval(vb, lb, d);
-    }
-    return h * dval(va, la, d);
-  }
-
-  // computeCost() = 0.5 * sum_s sum_d e^T H_s e  (== 0.5 sum c^T Q c).
-  __device__ double cost() const {
+  // One pass over (segment, dimension, coefficient k) with e = [x_s; x_{s+1}]:
+  //   c_s[d][k] = sum_j A(1)^-1[k][j] T_s^(j mod M - k) e_j   (coefficients,
+  //               linear_impl:254-275; written to `out` when non-null)
+  //   cost     += e_k (H_s e)_k                               (computeCost,
+  //               linear_impl:113-130: 0.5 c^T Q c == 0.5 e^T H e)
+  // Returns computeCost() on every lane.
+  __device__ double coeffs_and_cost(double* __restrict__ out) const {
     double acc = 0.0;
     const int n = S * D * N;
     for (int i = lane; i < n; i += kWave) {
       const int s = i / (D * N);
       const int rem = i % (D * N);
-      acc += seg_quad(s, rem / N, rem % N);
+      const int d = rem / N;
+      const int k = rem % N;
+      const int lk = k % M;
+      double c = 0.0, h = 0.0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const int l = j % M;
+        const double e = dval(s + j / M, l, d);
+        c += tabA()[k * N + j] * pwr(s, l - k) * e;
+        h += tabH()[k * N + j] * pwr(s, 1 - 2 * r + lk + l) * e;
+      }
+      if (out) out[i] = c;
+      acc += h * dval(s + k / M, lk, d);
     }
     return 0.5 * wave_sum(acc);
   }
+
+  __device__ double cost() const { return coeffs_and_cost(nullptr); }
 
   // sum_d e_s^T H_s(tau) e_s for segment s at time tau (fixed e): the part of
   // getCostAndGradientDerivative's J_d that depends on T_s.

@@ -35,7 +35,8 @@ int from_hip(hipError_t e) { return e == hipSuccess ? MTG_OK : MTG_ERR_HIP; }
 
 bool valid_N(int N) { return N >= 4 && N <= 12 && N % 2 == 0; }
 
-// Constant tables for (N, r), computed in long double:
+// Constant tables for (N, r), computed in long double (layout: H(1) N*N,
+// A(1)^-1 N*N, C^-1 M*M):
 //   A(1)  = setupMappingMatrix(1)                (linear_impl:101-111)
 //   Q(1)  = computeQuadraticCostJacobian(r, 1)   (linear_impl:557-573)
 //   H(1)  = A(1)^-T Q(1) A(1)^-1                 (linear_impl:318)
@@ -92,8 +93,25 @@ void build_tables(int N, int r, std::vector<double>* out) {
   for (int i = 0; i < N; ++i)
     for (int k = 0; k < N; ++k)
       for (int j = 0; j < N; ++j) H[i * N + j] += Ai[k * N + i] * QA[k * N + j];
+  // Bezier control-point map (qcqp_impl:280-297): B_ul(T) = diag(T^-l) C
+  // with C[l][j] = n!/(n-l)! (-1)^(l+j) binom(l, j), n = N-1, so
+  // B_ul^-1(T) = C^-1 diag(T^l); C^-1 by forward substitution.
+  std::vector<ld> C(M * M, 0), Ci(M * M, 0);
+  for (int l = 0; l < M; ++l)
+    for (int j = 0; j <= l; ++j) {
+      ld binom = 1;
+      for (int t = 0; t < j; ++t) binom = binom * (l - t) / (t + 1);
+      C[l * M + j] = falling(l, N - 1) * (((l + j) & 1) ? -1 : 1) * binom;
+    }
+  for (int c = 0; c < M; ++c)
+    for (int i = 0; i < M; ++i) {
+      ld s = (i == c) ? 1 : 0;
+      for (int k = 0; k < i; ++k) s -= C[i * M + k] * Ci[k * M + c];
+      Ci[i * M + c] = s / C[i * M + i];
+    }
   // Symmetrise (exact in real arithmetic).
-  out->assign(2 * N * N, 0.0);
+  out->assign(2 * N * N + M * M, 0.0);
+  for (int i = 0; i < M * M; ++i) (*out)[2 * N * N + i] = static_cast<double>(Ci[i]);
   for (int i = 0; i < N; ++i)
     for (int j = 0; j < N; ++j) {
       (*out)[i * N + j] = static_cast<double>((H[i * N + j] + H[j * N + i]) / 2);

@@ -41,11 +41,8 @@ __global__ __launch_bounds__(kWave) void linear_solve_kernel(
     for (int i = t.lane; i < per; i += kWave) coeffs[b * per + i] = NAN;
     if (cost && t.lane == 0) cost[b] = NAN;
   } else {
-    t.write_coeffs(coeffs + b * per);
-    if (cost) {
-      const double J = t.cost();
-      if (t.lane == 0) cost[b] = J;
-    }
+    const double J = t.coeffs_and_cost(coeffs + b * per);
+    if (cost && t.lane == 0) cost[b] = J;
     if (free_vals) {
       for (int i = t.lane; i < np * D; i += kWave) {
         const int d = i / np;

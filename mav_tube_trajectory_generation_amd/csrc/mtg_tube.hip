@@ -1,19 +1,166 @@
-// mtg_tube.hip — tube QCQP kernels (placeholder until the batched IPM lands).
+// mtg_tube.hip — tube QCQP kernels (solveQCQP replacement and constraint
+// residuals), one 64-lane workgroup per trajectory (mtg_tube_device.h).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "mtg_internal.h"
+#include "mtg_tube_device.h"
 
 namespace mtg {
 
-size_t tube_lds_bytes(int N, int S) { return 0; }
-
-hipError_t launch_tube_residuals(const TubeArgs&, const double*, double*, hipStream_t) {
-  return hipErrorNotSupported;
+template <int N>
+__device__ inline Tube<N> make_tube(const TubeLayout* L, double* smem, int S, int r) {
+  return Tube<N>{S, r, S - 1, tube_ncon(N, S), L, smem, static_cast<int>(threadIdx.x)};
 }
 
-hipError_t launch_tube_solve(const TubeArgs&, double, int, double*, double*, double*,
-                             int32_t*, int32_t*, hipStream_t) {
-  return hipErrorNotSupported;
+// Constraint residuals g_k(x) (compute_sphere/tube/tube_end_constraints,
+// qcqp_impl:357-474) at x given in the reference's dimension-major order.
+template <int N>
+__global__ __launch_bounds__(kWave) void tube_residuals_kernel(
+    int S, int r, const double* __restrict__ tab, const double* __restrict__ positions,
+    const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
+    const double* __restrict__ times, const double* __restrict__ radii,
+    const double* __restrict__ x, double* __restrict__ resid) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const TubeLayout L = make_tube_layout(N, S);
+  Tube<N> t = make_tube<N>(&L, smem, S, r);
+  int* bad = reinterpret_cast<int*>(smem + L.ndouble);
+  const int64_t b = blockIdx.x;
+  constexpr int M = N / 2;
+  t.setup(tab, b, positions, fixed_vals, times_cp, times, radii, bad);
+  const int n = t.nv * 3 * M;
+  for (int idx = t.lane; idx < n; idx += kWave) {
+    // reference order d*(S-1)*M + (u-1)*M + m  ->  internal ((u-1)*3+d)*M + m
+    const int d = idx / ((S - 1) * M), a = (idx / M) % (S - 1), m = idx % M;
+    smem[L.x + (a * 3 + d) * M + m] = x[b * n + idx];
+  }
+  __syncthreads();
+  t.control_points(smem + L.x, L.cp);
+  __syncthreads();
+  for (int k = t.lane; k < t.nc; k += kWave) {
+    double w[3];
+    resid[b * t.nc + k] = t.con_eval(k, L.cp, w);
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(kWave) void tube_solve_kernel(
+    int S, int r, const double* __restrict__ tab, const double* __restrict__ positions,
+    const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
+    const double* __restrict__ times, const double* __restrict__ radii, double tol,
+    int max_iter, double* __restrict__ x_out, double* __restrict__ coeffs,
+    double* __restrict__ cost, int32_t* __restrict__ iters, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const TubeLayout L = make_tube_layout(N, S);
+  Tube<N> t = make_tube<N>(&L, smem, S, r);
+  int* bad = reinterpret_cast<int*>(smem + L.ndouble);
+  const int64_t b = blockIdx.x;
+  constexpr int M = N / 2;
+  t.setup(tab, b, positions, fixed_vals, times_cp, times, radii, bad);
+  int st = 1;
+  int it = 0;
+  if (!(*bad & 1)) it = t.ipm(tol, max_iter, &st, bad);
+  __syncthreads();
+  const int fl = *bad;
+  // Outputs: x (reference order), coefficients (qcqp_impl:777-785 ->
+  // linear_impl:254-275) and computeCost (linear_impl:113-130).
+  const int n = t.nv * 3 * M;
+  if (x_out)
+    for (int idx = t.lane; idx < n; idx += kWave) {
+      const int d = idx / ((S - 1) * M), a = (idx / M) % (S - 1), m = idx % M;
+      x_out[b * n + idx] = smem[L.x + (a * 3 + d) * M + m];
+    }
+  const double* xv = smem + L.x;
+  double acc = 0.0;
+  const int per = S * 3 * N;
+  for (int i = t.lane; i < per; i += kWave) {
+    const int s = i / (3 * N), d = (i / N) % 3, k = i % N;
+    const int lk = k % M;
+    double c = 0.0, h = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const int l = j % M;
+      const double e = t.xval(xv, s + j / M, d, l);
+      c += smem[L.tabA + k * N + j] * t.pwr(s, l - k) * e;
+      h += smem[L.tabH + k * N + j] * t.pwr(s, 1 - 2 * r + lk + l) * e;
+    }
+    coeffs[b * per + i] = (fl & 1) ? NAN : c;
+    acc += h * t.xval(xv, s + k / M, d, lk);
+  }
+  const double J = 0.5 * Tube<N>::wave_sum(acc);
+  if (t.lane == 0) {
+    if (cost) cost[b] = (fl & 1) ? NAN : J;
+    if (iters) iters[b] = it;
+    if (status)
+      status[b] = (fl & 1) ? MTG_TRAJ_BAD_TIME
+                           : ((fl & 2) || st == 2) ? MTG_TRAJ_NOT_SPD
+                           : (st == 0 ? MTG_TRAJ_OK : MTG_TRAJ_NOT_CONVERGED);
+  }
+}
+
+size_t tube_lds_bytes(int N, int S) {
+  if (S < 2) return 0;
+  return make_tube_layout(N, S).bytes() + 16;  // + 2 ints (bad, fail)
+}
+
+namespace {
+template <typename K>
+hipError_t prepare_lds(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(bytes));
+  return hipSuccess;
+}
+
+template <int N>
+hipError_t residuals_n(const TubeArgs& a, const double* x, double* resid, hipStream_t st) {
+  const size_t bytes = tube_lds_bytes(N, a.S);
+  hipError_t e = prepare_lds(tube_residuals_kernel<N>, bytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tube_residuals_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(kWave),
+                     bytes, st, a.S, a.r, a.tab, a.positions, a.fixed_vals, a.times_cp,
+                     a.times, a.radii, x, resid);
+  return hipGetLastError();
+}
+
+template <int N>
+hipError_t solve_n(const TubeArgs& a, double tol, int max_iter, double* x, double* coeffs,
+                   double* cost, int32_t* iters, int32_t* status, hipStream_t st) {
+  const size_t bytes = tube_lds_bytes(N, a.S);
+  hipError_t e = prepare_lds(tube_solve_kernel<N>, bytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tube_solve_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(kWave),
+                     bytes, st, a.S, a.r, a.tab, a.positions, a.fixed_vals, a.times_cp,
+                     a.times, a.radii, tol, max_iter, x, coeffs, cost, iters, status);
+  return hipGetLastError();
+}
+}  // namespace
+
+#define MTG_TUBE_DISPATCH(CALL)              \
+  switch (a.N) {                             \
+    case 4: return CALL(4);                  \
+    case 6: return CALL(6);                  \
+    case 8: return CALL(8);                  \
+    case 10: return CALL(10);                \
+    case 12: return CALL(12);                \
+    default: return hipErrorInvalidValue;    \
+  }
+
+hipError_t launch_tube_residuals(const TubeArgs& a, const double* x, double* resid,
+                                 hipStream_t st) {
+#define CALL(n) residuals_n<n>(a, x, resid, st)
+  MTG_TUBE_DISPATCH(CALL)
+#undef CALL
+}
+
+hipError_t launch_tube_solve(const TubeArgs& a, double tol, int max_iter, double* x,
+                             double* coeffs, double* cost, int32_t* iters, int32_t* status,
+                             hipStream_t st) {
+#define CALL(n) solve_n<n>(a, tol, max_iter, x, coeffs, cost, iters, status, st)
+  MTG_TUBE_DISPATCH(CALL)
+#undef CALL
 }
 
 }  // namespace mtg

@@ -1,0 +1,746 @@
+// mtg_tube_device.h — per-trajectory tube QCQP (PolynomialOptimizationConstrained,
+// qcqp_impl) on one 64-lane workgroup, all state in LDS.
+//
+// Problem (qcqp_impl:476-788): free variables are every
+// derivative 0..M-1 of every intermediate vertex in all 3 dimensions,
+// objective x^T R_pp x + 2 d_f^T R_fp x, and per segment i the constraints
+//   sphere  (i < S-1)     ||c_{i,N-1} - p_{i+1}||^2 - r2_i^2        <= 0
+//   tube    j = 1..N-2    ||A_i c_ij + b_i||^2 - r1_i^2             <= 0
+//   ends    j = 1..N-2    n_i.(p_s - c_ij) <= 0,  n_i.(c_ij - p_e) <= 0
+// with c_ij the Bezier control points of the segment (qcqp_impl:267-474).
+//
+// MI355X formulation.  Control point j < M of segment i depends only on the
+// start vertex i (row j of B_ul^-1), j >= M only on the end vertex i+1 (row
+// j-M of B_lr^-1): every constraint touches ONE vertex's 3M variables, so its
+// gradient is w (3-vector) (x) beta (M-vector) and its Hessian G (x) beta
+// beta^T.  The Newton/KKT matrix is therefore block tridiagonal with 3M x 3M
+// blocks (vertex coupling only through R_pp, which is the same M x M block in
+// each dimension).  A primal-dual Mehrotra interior-point method (the
+// oracle's algorithm, oracle/mtg_oracle.cpp TubeProblem::solveIPM) runs per
+// trajectory: per iteration one block LDL^T factorisation (explicit unit
+// L^-1 per block so the two solves are mat-vecs) and two solves.
+#pragma once
+#include "mtg_device.h"
+
+namespace mtg {
+
+constexpr int kTubeD = 3;
+
+struct TubeLayout {
+  int tabH, tabA, cinv;   // N*N, N*N, M*M
+  int bul;                // S*M*M  B_ul^-1 per segment (zero-snapped)
+  int bet;                // S*N*M  beta rows per control point
+  int pw;                 // S*(2N-1) powers of the current times
+  int T;                  // S
+  int geo;                // S*kGeo tube geometry per segment
+  int fixv;               // 2*3*M start/end derivatives [end][d][m]
+  int pos;                // (S+1)*3
+  int Pd, Po, q;          // nv*M*M, (nv-1)*M*M, nv*3M
+  int x, dx, rd, rhs;     // nv*3M each
+  int cp, dcp, acc;       // S*N*3 each
+  int s, lam, g, ds, dl, prod;  // ncon each
+  int Lk;                 // nv*BS*BS  (K blocks -> L^-1)
+  int W;                  // max(nv-1,1)*BS*BS (also G per control point: S*N*9)
+  int dinv;               // nv*BS
+  int tmp;                // BS*BS
+  int red;                // 64
+  int ndouble;
+  size_t bytes() const { return sizeof(double) * ndouble; }
+};
+
+constexpr int kGeo = 20;  // n[3] LL[9] L[3] mu n.ps n.pe r2^2 pad
+
+__host__ __device__ inline int tube_ncon(int N, int S) { return (S - 1) + 3 * S * (N - 2); }
+
+__host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
+  const int M = N / 2, BS = 3 * M, nv = S - 1, nc = tube_ncon(N, S);
+  TubeLayout l;
+  int o = 0;
+  l.tabH = o; o += N * N;
+  l.tabA = o; o += N * N;
+  l.cinv = o; o += M * M;
+  l.bul = o;  o += S * M * M;
+  l.bet = o;  o += S * N * M;
+  l.pw = o;   o += S * (2 * N - 1);
+  l.T = o;    o += S;
+  l.geo = o;  o += S * kGeo;
+  l.fixv = o; o += 2 * 3 * M;
+  l.pos = o;  o += (S + 1) * 3;
+  l.Pd = o;   o += nv * M * M;
+  l.Po = o;   o += (nv > 1 ? nv - 1 : 1) * M * M;
+  l.q = o;    o += nv * BS;
+  l.x = o;    o += nv * BS;
+  l.dx = o;   o += nv * BS;
+  l.rd = o;   o += nv * BS;
+  l.rhs = o;  o += nv * BS;
+  l.cp = o;   o += S * N * 3;
+  l.dcp = o;  o += S * N * 3;
+  l.acc = o;  o += S * N * 3;
+  l.s = o;    o += nc;
+  l.lam = o;  o += nc;
+  l.g = o;    o += nc;
+  l.ds = o;   o += nc;
+  l.dl = o;   o += nc;
+  l.prod = o; o += nc;
+  l.Lk = o;   o += nv * BS * BS;
+  const int wsz = (nv > 1 ? nv - 1 : 1) * BS * BS;
+  const int gsz = S * N * 9;
+  l.W = o;    o += wsz > gsz ? wsz : gsz;
+  l.dinv = o; o += nv * BS;
+  l.tmp = o;  o += BS * BS;
+  l.red = o;  o += kWave;
+  l.ndouble = o;
+  return l;
+}
+
+template <int N>
+struct Tube {
+  static constexpr int M = N / 2;
+  static constexpr int BS = 3 * M;
+  static constexpr int PWN = 2 * N - 1;
+  int S, r, nv, nc;
+  const TubeLayout* L;
+  double* sm;
+  int lane;
+
+  __device__ double* at(int off) const { return sm + off; }
+  __device__ double pwr(int s, int e) const { return sm[L->pw + s * PWN + e + (N - 1)]; }
+
+  // Control point (i, j) -> vertex it depends on.
+  __device__ static int cp_vertex(int i, int j) { return j < M ? i : i + 1; }
+  // beta_ij[m]: row j of B_ul^-1 (j < M) or row j-M of
+  // B_lr^-1 = rowreverse(B_ul^-1) diag((-1)^m) (qcqp_impl:309-317).
+  __device__ double beta_raw(int i, int j, int m) const {
+    const double* b = sm + L->bul + i * M * M;
+    if (j < M) return b[j * M + m];
+    const double v = b[(M - 1 - (j - M)) * M + m];
+    return (m & 1) ? -v : v;
+  }
+  __device__ double beta(int i, int j, int m) const { return sm[L->bet + (i * N + j) * M + m]; }
+  // Derivative m of vertex u in dimension d (fixed at the ends).
+  __device__ double xval(const double* xv, int u, int d, int m) const {
+    if (u == 0) return sm[L->fixv + (0 * 3 + d) * M + m];
+    if (u == S) return sm[L->fixv + (1 * 3 + d) * M + m];
+    return xv[((u - 1) * 3 + d) * M + m];
+  }
+
+  // Constraint index layout per segment (qcqp_impl:321-355):
+  // [sphere if i < S-1] [tube j=1..N-2] [end j=1..N-2: side 0, side 1].
+  __device__ int seg_base(int i) const { return i * (3 * N - 5); }
+  __device__ int sphere_idx(int i) const { return seg_base(i); }
+  __device__ int tube_idx(int i, int j) const {
+    return seg_base(i) + (i < S - 1 ? 1 : 0) + (j - 1);
+  }
+  __device__ int end_idx(int i, int j, int side) const {
+    return seg_base(i) + (i < S - 1 ? 1 : 0) + (N - 2) + 2 * (j - 1) + side;
+  }
+  // Inverse: constraint k -> (segment, control point, type 0 sphere / 1 tube
+  // / 2 end side 0 / 3 end side 1).
+  __device__ void con_of(int k, int* i, int* j, int* type) const {
+    int seg = k / (3 * N - 5);
+    if (seg > S - 1) seg = S - 1;
+    int o = k - seg_base(seg);
+    const int sp = seg < S - 1 ? 1 : 0;
+    *i = seg;
+    if (sp && o == 0) {
+      *j = N - 1;
+      *type = 0;
+      return;
+    }
+    o -= sp;
+    if (o < N - 2) {
+      *j = o + 1;
+      *type = 1;
+      return;
+    }
+    o -= N - 2;
+    *j = o / 2 + 1;
+    *type = 2 + (o & 1);
+  }
+
+  // ------------------------------------------------------------------ setup
+  // Loads inputs, builds B_ul^-1 (zero-snapped), tube geometry, P and q.
+  __device__ void setup(const double* __restrict__ tab, int64_t b,
+                        const double* __restrict__ positions,
+                        const double* __restrict__ fixed_vals,
+                        const double* __restrict__ times_cp,
+                        const double* __restrict__ times,
+                        const double* __restrict__ radii, int* bad) {
+    const int NN = N * N;
+    for (int i = lane; i < 2 * NN + M * M; i += kWave) sm[L->tabH + i] = tab[i];
+    for (int i = lane; i < S; i += kWave) sm[L->T + i] = times[b * S + i];
+    for (int i = lane; i < (S + 1) * 3; i += kWave) sm[L->pos + i] = positions[b * (S + 1) * 3 + i];
+    for (int i = lane; i < 3 * N; i += kWave) {
+      // fixed_vals[d][end*M + m] -> fixv[end][d][m]
+      const int d = i / N, e = (i % N) / M, m = i % M;
+      sm[L->fixv + (e * 3 + d) * M + m] = fixed_vals[b * 3 * N + i];
+    }
+    if (lane == 0) *bad = 0;
+    __syncthreads();
+    // B_ul^-1(T_cp) = C^-1 diag(T^l), snapped |x| < 1e-5 (qcqp_impl:299-307).
+    for (int idx = lane; idx < S * M * M; idx += kWave) {
+      const int i = idx / (M * M), k = (idx / M) % M, l = idx % M;
+      const double tc = times_cp[b * S + i];
+      if (!(tc > 0.0)) atomicOr(bad, 1);
+      double p = 1.0;
+      for (int q = 0; q < l; ++q) p *= tc;
+      double v = sm[L->cinv + k * M + l] * p;
+      if (v > -0.00001 && v < 0.00001) v = 0.0;
+      sm[L->bul + idx] = v;
+    }
+    __syncthreads();
+    for (int idx = lane; idx < S * N * M; idx += kWave) {
+      const int i = idx / (N * M), j = (idx / M) % N, m = idx % M;
+      sm[L->bet + idx] = beta_raw(i, j, m);
+    }
+    // Powers of the current times (H, A^-1, cost).
+    for (int idx = lane; idx < S * PWN; idx += kWave) {
+      const int s = idx / PWN;
+      const int e = idx % PWN - (N - 1);
+      const double t = sm[L->T + s];
+      if (!(t > 0.0) || !(t < 1e300)) atomicOr(bad, 1);
+      const double base = e < 0 ? 1.0 / t : t;
+      const int n = e < 0 ? -e : e;
+      double p = 1.0;
+      for (int q = 0; q < n; ++q) p *= base;
+      sm[L->pw + idx] = p;
+    }
+    // Tube geometry per segment (qcqp_impl:369-474).
+    for (int i = lane; i < S; i += kWave) {
+      const double* p0 = sm + L->pos + i * 3;
+      const double* p1 = p0 + 3;
+      double n[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+      const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+      for (int k = 0; k < 3; ++k) n[k] /= nn;
+      double A[9] = {1 - n[0] * n[0], -n[0] * n[1], -n[0] * n[2],
+                     -n[0] * n[1], 1 - n[1] * n[1], -n[1] * n[2],
+                     -n[0] * n[2], -n[1] * n[2], 1 - n[2] * n[2]};
+      for (int k = 0; k < 9; ++k)
+        if (A[k] > -0.000001 && A[k] < 0.000001) A[k] = 0.0;
+      double bb[3] = {(n[0] * n[0] - 1) * p0[0] + n[0] * n[1] * p0[1] + n[0] * n[2] * p0[2],
+                      n[0] * n[1] * p0[0] + (n[1] * n[1] - 1) * p0[1] + n[1] * n[2] * p0[2],
+                      n[0] * n[2] * p0[0] + n[1] * n[2] * p0[1] + (n[2] * n[2] - 1) * p0[2]};
+      for (int k = 0; k < 3; ++k)
+        if (bb[k] > -0.000001 && bb[k] < 0.000001) bb[k] = 0.0;
+      double* G = sm + L->geo + i * kGeo;
+      for (int k = 0; k < 3; ++k) G[k] = n[k];
+      for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) {
+          double s = 0.0;
+          for (int k = 0; k < 3; ++k) s += A[k * 3 + a] * A[k * 3 + c];
+          G[3 + a * 3 + c] = s;  // LL = A^T A
+        }
+      for (int c = 0; c < 3; ++c) {
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s += bb[k] * A[k * 3 + c];
+        G[12 + c] = 2.0 * s;  // L = 2 b^T A
+      }
+      const double r1 = radii[(b * S + i) * 2 + 0];
+      const double r2 = radii[(b * S + i) * 2 + 1];
+      G[15] = bb[0] * bb[0] + bb[1] * bb[1] + bb[2] * bb[2] - r1 * r1;  // mu
+      const double rs = (i == 0) ? radii[(b * S + 0) * 2 + 0] : radii[(b * S + i - 1) * 2 + 1];
+      double nps = 0.0, npe = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        nps += n[k] * (p0[k] - n[k] * rs);
+        npe += n[k] * (p1[k] + n[k] * r2);
+      }
+      G[16] = nps;
+      G[17] = npe;
+      G[18] = r2 * r2;
+    }
+    __syncthreads();
+    // P = 2 R_pp (identical M x M blocks per dimension) and q = 2 R_pf d_f.
+    for (int idx = lane; idx < nv * M * M; idx += kWave) {
+      const int a = idx / (M * M), j = (idx / M) % M, k = idx % M;
+      const int u = a + 1;  // vertex
+      sm[L->Pd + idx] = 2.0 * (Hb(u - 1, 1, 1, j, k) + Hb(u, 0, 0, j, k));
+    }
+    for (int idx = lane; idx < (nv - 1) * M * M; idx += kWave) {
+      const int a = idx / (M * M), j = (idx / M) % M, k = idx % M;
+      sm[L->Po + idx] = 2.0 * Hb(a + 1, 0, 1, j, k);  // vertex a+1 -> a+2
+    }
+    for (int idx = lane; idx < nv * BS; idx += kWave) {
+      const int a = idx / BS, d = (idx / M) % 3, j = idx % M;
+      const int u = a + 1;
+      double v = 0.0;
+      if (u == 1)
+        for (int k = 0; k < M; ++k) v += Hb(0, 1, 0, j, k) * sm[L->fixv + (0 * 3 + d) * M + k];
+      if (u == S - 1)
+        for (int k = 0; k < M; ++k) v += Hb(S - 1, 0, 1, j, k) * sm[L->fixv + (1 * 3 + d) * M + k];
+      sm[L->q + idx] = 2.0 * v;
+    }
+    __syncthreads();
+  }
+
+  __device__ double Hb(int s, int ab, int bb, int j, int k) const {
+    return sm[L->tabH + (ab * M + j) * N + bb * M + k] * pwr(s, 1 - 2 * r + j + k);
+  }
+
+  // --------------------------------------------------------- control points
+  __device__ void control_points(const double* xv, int out) {
+    for (int idx = lane; idx < S * N * 3; idx += kWave) {
+      const int i = idx / (N * 3), j = (idx / 3) % N, d = idx % 3;
+      const int u = cp_vertex(i, j);
+      double c = 0.0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) c += beta(i, j, m) * xval(xv, u, d, m);
+      sm[out + idx] = c;
+    }
+  }
+  // Same, for a step direction (fixed vertices contribute zero).
+  __device__ void control_point_steps(const double* dxv, int out) {
+    for (int idx = lane; idx < S * N * 3; idx += kWave) {
+      const int i = idx / (N * 3), j = (idx / 3) % N, d = idx % 3;
+      const int u = cp_vertex(i, j);
+      double c = 0.0;
+      if (u > 0 && u < S) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) c += beta(i, j, m) * dxv[((u - 1) * 3 + d) * M + m];
+      }
+      sm[out + idx] = c;
+    }
+  }
+
+  // Residual g_k and gradient w_k (w.r.t. the control point) of constraint k
+  // at control points `cpo`.
+  __device__ double con_eval(int k, int cpo, double w[3]) const {
+    int i, j, type;
+    con_of(k, &i, &j, &type);
+    const double* c = sm + cpo + (i * N + j) * 3;
+    const double* G = sm + L->geo + i * kGeo;
+    if (type == 0) {  // sphere around vertex i+1 (qcqp_impl:357-365)
+      const double* p = sm + L->pos + (i + 1) * 3;
+      double g = -G[18];
+      for (int d = 0; d < 3; ++d) {
+        const double e = c[d] - p[d];
+        g += e * e;
+        w[d] = 2.0 * e;
+      }
+      return g;
+    }
+    if (type == 1) {  // tube (qcqp_impl:369-429): c^T LL c + L c + mu
+      double g = G[15];
+      for (int a = 0; a < 3; ++a) {
+        double llc = 0.0;
+        for (int e = 0; e < 3; ++e) llc += G[3 + a * 3 + e] * c[e];
+        g += c[a] * llc + G[12 + a] * c[a];
+        w[a] = 2.0 * llc + G[12 + a];
+      }
+      return g;
+    }
+    // end caps (qcqp_impl:431-474)
+    const double sgn = type == 2 ? -1.0 : 1.0;
+    double nc = 0.0;
+    for (int d = 0; d < 3; ++d) {
+      nc += G[d] * c[d];
+      w[d] = sgn * G[d];
+    }
+    return type == 2 ? (G[16] - nc) : (nc - G[17]);
+  }
+
+  // Hessian factor of constraint type (w.r.t. the control point): 2 I, 2 LL, 0.
+  __device__ double con_hess(int type, int i, int a, int e) const {
+    if (type == 0) return a == e ? 2.0 : 0.0;
+    if (type == 1) return 2.0 * sm[L->geo + i * kGeo + 3 + a * 3 + e];
+    return 0.0;
+  }
+
+  // Constraint slot t (0..2) acting on control point (i, j): returns its
+  // index or -1.  Slots: sphere on j = N-1 (i < S-1); tube / end side 0 /
+  // end side 1 on j = 1..N-2.  (Fixed-slot form: no runtime-indexed arrays,
+  // which hipcc would place in scratch.)
+  __device__ int con_at(int i, int j, int t) const {
+    if (j == N - 1) return (t == 0 && i < S - 1) ? sphere_idx(i) : -1;
+    if (j < 1 || j > N - 2) return -1;
+    return t == 0 ? tube_idx(i, j) : end_idx(i, j, t - 1);
+  }
+
+  // P x + q for vertex block entry idx (a, d, m).
+  __device__ double Pxq(const double* xv, int idx) const {
+    const int a = idx / BS, d = (idx / M) % 3, m = idx % M;
+    double v = sm[L->q + idx];
+    for (int k = 0; k < M; ++k) {
+      v += sm[L->Pd + a * M * M + m * M + k] * xv[(a * 3 + d) * M + k];
+      if (a > 0) v += sm[L->Po + (a - 1) * M * M + k * M + m] * xv[((a - 1) * 3 + d) * M + k];
+      if (a < nv - 1) v += sm[L->Po + a * M * M + m * M + k] * xv[((a + 1) * 3 + d) * M + k];
+    }
+    return v;
+  }
+
+  // Sum over the control points of vertex u=a+1 of beta[m] * acc[cp][d]
+  // (the a_k-weighted sums of the dual residual / right-hand side).
+  __device__ double gather_cp(int acc_off, int a, int d, int m) const {
+    const int u = a + 1;
+    double v = 0.0;
+    for (int j = M; j < N; ++j) v += beta(u - 1, j, m) * sm[acc_off + ((u - 1) * N + j) * 3 + d];
+    for (int j = 0; j < M; ++j) v += beta(u, j, m) * sm[acc_off + (u * N + j) * 3 + d];
+    return v;
+  }
+
+  // --------------------------------------------------------- KKT assembly
+  // G per control point -> W region; K_a = P_a (x) I + sum G (x) beta beta^T.
+  __device__ void assemble_kkt(bool with_constraints) {
+    double* Gcp = sm + L->W;
+    if (with_constraints) {
+      for (int cpi = lane; cpi < S * N; cpi += kWave) {
+        const int i = cpi / N, j = cpi % N;
+        double G[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) G[e] = 0.0;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int k = con_at(i, j, t);
+          if (k < 0) continue;
+          double w[3];
+          con_eval(k, L->cp, w);
+          int ii, jj, type;
+          con_of(k, &ii, &jj, &type);
+          const double lam = sm[L->lam + k], s = sm[L->s + k];
+          const double ws = lam / s;
+          for (int a = 0; a < 3; ++a)
+            for (int e = 0; e < 3; ++e)
+              G[a * 3 + e] += lam * con_hess(type, i, a, e) + ws * w[a] * w[e];
+        }
+        for (int e = 0; e < 9; ++e) Gcp[cpi * 9 + e] = G[e];
+      }
+      __syncthreads();
+    }
+    for (int idx = lane; idx < nv * BS * BS; idx += kWave) {
+      const int a = idx / (BS * BS);
+      const int row = (idx / BS) % BS, col = idx % BS;
+      if (col > row) continue;  // the factorisation reads the lower triangle
+      const int d = row / M, m = row % M, d2 = col / M, m2 = col % M;
+      double v = (d == d2) ? sm[L->Pd + a * M * M + m * M + m2] : 0.0;
+      if (with_constraints) {
+        const int u = a + 1;
+        for (int j = M; j < N; ++j)
+          v += Gcp[((u - 1) * N + j) * 9 + d * 3 + d2] * beta(u - 1, j, m) * beta(u - 1, j, m2);
+        for (int j = 0; j < M; ++j)
+          v += Gcp[(u * N + j) * 9 + d * 3 + d2] * beta(u, j, m) * beta(u, j, m2);
+      }
+      sm[L->Lk + idx] = v;
+    }
+    __syncthreads();
+  }
+
+  // --------------------------------------------------------- factorisation
+  // Block LDL^T: Lk_a <- unit L_a^-1 (lower), dinv_a, W_a = L_a^-1 K_{a,a+1}.
+  // Sets *fail = 1 on a non-positive pivot.
+  __device__ void factor(int* fail) {
+    double* tmp = sm + L->tmp;
+    for (int a = 0; a < nv; ++a) {
+      double* A = sm + L->Lk + a * BS * BS;
+      if (a > 0) {
+        const double* Wp = sm + L->W + (a - 1) * BS * BS;
+        const double* dp = sm + L->dinv + (a - 1) * BS;
+        for (int idx = lane; idx < BS * BS; idx += kWave) {
+          const int i = idx / BS, k = idx % BS;
+          if (k > i) continue;
+          double v = A[idx];
+          for (int t = 0; t < BS; ++t) v -= Wp[t * BS + i] * dp[t] * Wp[t * BS + k];
+          A[idx] = v;
+        }
+        __syncthreads();
+      }
+      // Right-looking LDL^T on the lower triangle.
+      for (int j = 0; j < BS; ++j) {
+        const double dj = A[j * BS + j];
+        if (lane == 0 && !(dj > 0.0)) *fail = 1;
+        const double inv = rcp64(dj > 0.0 ? dj : 1.0);
+        const int rem = BS - 1 - j;
+        for (int t = lane; t < rem * rem; t += kWave) {
+          const int i = j + 1 + t / rem, k = j + 1 + t % rem;
+          if (k > i) continue;
+          A[i * BS + k] -= A[i * BS + j] * inv * A[k * BS + j];
+        }
+        __syncthreads();
+      }
+      if (lane < BS) sm[L->dinv + a * BS + lane] = rcp64(A[lane * BS + lane] > 0.0 ? A[lane * BS + lane] : 1.0);
+      __syncthreads();
+      // Unit L in place (lower, strictly): L[i][j] = A[i][j] * dinv[j].
+      for (int idx = lane; idx < BS * BS; idx += kWave) {
+        const int i = idx / BS, j = idx % BS;
+        if (j < i) A[idx] *= sm[L->dinv + a * BS + j];
+      }
+      __syncthreads();
+      // Column c of L^-1 (unit lower): x = e_c, x_i = -sum_{k<i} L[i][k] x_k,
+      // built in LDS (tmp) by lane c (no private arrays -> no scratch).
+      if (lane < BS) {
+        const int c = lane;
+        for (int i = 0; i < BS; ++i) {
+          double v;
+          if (i < c) {
+            v = 0.0;
+          } else if (i == c) {
+            v = 1.0;
+          } else {
+            v = 0.0;
+            for (int k = c; k < i; ++k) v -= A[i * BS + k] * tmp[k * BS + c];
+          }
+          tmp[i * BS + c] = v;
+        }
+      }
+      __syncthreads();
+      for (int idx = lane; idx < BS * BS; idx += kWave) A[idx] = tmp[idx];
+      __syncthreads();
+      // W_a = L_a^-1 (I_3 (x) Po_a)
+      if (a < nv - 1) {
+        double* Wa = sm + L->W + a * BS * BS;
+        const double* P = sm + L->Po + a * M * M;
+        for (int idx = lane; idx < BS * BS; idx += kWave) {
+          const int i = idx / BS, col = idx % BS;
+          const int d2 = col / M, m2 = col % M;
+          double v = 0.0;
+          for (int t = 0; t < M; ++t) v += A[i * BS + d2 * M + t] * P[t * M + m2];
+          Wa[idx] = v;
+        }
+        __syncthreads();
+      }
+    }
+  }
+
+  // Solve K dx = rhs with the factors (rhs overwritten by y).
+  __device__ void solve(int rhs_off, int out_off) {
+    double* tmp = sm + L->tmp;
+    double* y = sm + rhs_off;
+    double* xo = sm + out_off;
+    for (int a = 0; a < nv; ++a) {
+      if (lane < BS) {
+        double t = y[a * BS + lane];
+        if (a > 0) {
+          const double* Wp = sm + L->W + (a - 1) * BS * BS;
+          const double* dp = sm + L->dinv + (a - 1) * BS;
+          for (int k = 0; k < BS; ++k) t -= Wp[k * BS + lane] * dp[k] * y[(a - 1) * BS + k];
+        }
+        tmp[lane] = t;
+      }
+      __syncthreads();
+      if (lane < BS) {
+        const double* Li = sm + L->Lk + a * BS * BS;
+        double v = 0.0;
+        for (int k = 0; k <= lane; ++k) v += Li[lane * BS + k] * tmp[k];
+        y[a * BS + lane] = v;
+      }
+      __syncthreads();
+    }
+    for (int a = nv - 1; a >= 0; --a) {
+      if (lane < BS) {
+        double t = y[a * BS + lane];
+        if (a < nv - 1) {
+          const double* Wa = sm + L->W + a * BS * BS;
+          for (int k = 0; k < BS; ++k) t -= Wa[lane * BS + k] * xo[(a + 1) * BS + k];
+        }
+        tmp[lane] = t * sm[L->dinv + a * BS + lane];
+      }
+      __syncthreads();
+      if (lane < BS) {
+        const double* Li = sm + L->Lk + a * BS * BS;
+        double v = 0.0;
+        for (int k = lane; k < BS; ++k) v += Li[k * BS + lane] * tmp[k];
+        xo[a * BS + lane] = v;
+      }
+      __syncthreads();
+    }
+  }
+
+  __device__ static double wave_max(double x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = fmax(x, __shfl_xor(x, off, kWave));
+    return x;
+  }
+  __device__ static double wave_min(double x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = fmin(x, __shfl_xor(x, off, kWave));
+    return x;
+  }
+  __device__ static double wave_sum(double x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+    return x;
+  }
+
+  // Newton direction for a complementarity target rc (stored in `prod`
+  // beforehand as rc_k): rhs = -rd - sum a_k (lam rp - rc)/s, solve, then
+  // dl, ds.  Expects cp, g, rd valid and the factorisation done.
+  __device__ void direction() {
+    // Per control point: Psi[d] = sum_k w_k[d] (lam_k rp_k - rc_k) / s_k.
+    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+      const int i = cpi / N, j = cpi % N;
+      double P3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int k = con_at(i, j, t);
+        if (k < 0) continue;
+        double w[3];
+        con_eval(k, L->cp, w);
+        const double lam = sm[L->lam + k], s = sm[L->s + k];
+        const double rp = sm[L->g + k] + s;
+        const double coef = (lam * rp - sm[L->prod + k]) / s;
+        for (int d = 0; d < 3; ++d) P3[d] += w[d] * coef;
+      }
+      for (int d = 0; d < 3; ++d) sm[L->acc + cpi * 3 + d] = P3[d];
+    }
+    __syncthreads();
+    for (int idx = lane; idx < nv * BS; idx += kWave) {
+      const int a = idx / BS, d = (idx / M) % 3, m = idx % M;
+      sm[L->rhs + idx] = -sm[L->rd + idx] - gather_cp(L->acc, a, d, m);
+    }
+    __syncthreads();
+    solve(L->rhs, L->dx);
+    control_point_steps(sm + L->dx, L->dcp);
+    __syncthreads();
+    for (int k = lane; k < nc; k += kWave) {
+      double w[3];
+      con_eval(k, L->cp, w);
+      int i, j, type;
+      con_of(k, &i, &j, &type);
+      const double* dc = sm + L->dcp + (i * N + j) * 3;
+      const double adx = w[0] * dc[0] + w[1] * dc[1] + w[2] * dc[2];
+      const double lam = sm[L->lam + k], s = sm[L->s + k];
+      const double rp = sm[L->g + k] + s;
+      const double rc = sm[L->prod + k];
+      const double dl = (lam / s) * (adx + rp) - rc / s;
+      sm[L->dl + k] = dl;
+      sm[L->ds + k] = (-rc - s * dl) / lam;
+    }
+    __syncthreads();
+  }
+
+  __device__ double max_step() const {
+    double alpha = 1.0;
+    for (int k = lane; k < nc; k += kWave) {
+      const double ds = sm[L->ds + k], dl = sm[L->dl + k];
+      if (ds < 0) alpha = fmin(alpha, -sm[L->s + k] / ds);
+      if (dl < 0) alpha = fmin(alpha, -sm[L->lam + k] / dl);
+    }
+    return wave_min(alpha);
+  }
+
+  // Full IPM (oracle TubeProblem::solveIPM).  Returns iterations; *status
+  // 0 converged, 1 iteration cap, 2 numerical breakdown away from the
+  // optimum; *bad bit 2 set for a non-positive pivot of the start system.
+  // Safeguard (same in the oracle): when the KKT factorisation or the step
+  // breaks down, stop at the current iterate and accept it if every
+  // residual is within 1e3 * tol.
+  __device__ int ipm(double tol, int max_iter, int* status, int* bad) {
+    int* fail = bad + 1;
+    if (lane == 0) *fail = 0;
+    __syncthreads();
+    // Unconstrained start: P x = -q.
+    assemble_kkt(false);
+    factor(fail);
+    __syncthreads();
+    if (*fail) {
+      if (lane == 0) *bad |= 2;
+      *status = 2;
+      return 0;
+    }
+    for (int idx = lane; idx < nv * BS; idx += kWave) sm[L->rhs + idx] = -sm[L->q + idx];
+    __syncthreads();
+    solve(L->rhs, L->x);
+    control_points(sm + L->x, L->cp);
+    __syncthreads();
+    for (int k = lane; k < nc; k += kWave) {
+      double w[3];
+      const double g = con_eval(k, L->cp, w);
+      sm[L->g + k] = g;
+      sm[L->s + k] = fmax(-g, 1.0);
+      sm[L->lam + k] = 1.0;
+    }
+    double qn = 0.0;
+    for (int idx = lane; idx < nv * BS; idx += kWave) qn = fmax(qn, fabs(sm[L->q + idx]));
+    qn = wave_max(qn);
+    __syncthreads();
+    int it = 0;
+    *status = 1;
+    for (it = 0; it < max_iter; ++it) {
+      // Residuals at the current point.
+      control_points(sm + L->x, L->cp);
+      __syncthreads();
+      double rpn = 0.0, mu = 0.0;
+      for (int k = lane; k < nc; k += kWave) {
+        double w[3];
+        const double g = con_eval(k, L->cp, w);
+        sm[L->g + k] = g;
+        const double s = sm[L->s + k];
+        rpn = fmax(rpn, fabs(g + s));
+        mu += s * sm[L->lam + k];
+      }
+      rpn = wave_max(rpn);
+      mu = wave_sum(mu) / nc;
+      // Omega[cp][d] = sum_k lam_k w_k[d]  (dual residual weights).
+      for (int cpi = lane; cpi < S * N; cpi += kWave) {
+        const int i = cpi / N, j = cpi % N;
+        double O3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int k = con_at(i, j, t);
+          if (k < 0) continue;
+          double w[3];
+          con_eval(k, L->cp, w);
+          const double lam = sm[L->lam + k];
+          for (int d = 0; d < 3; ++d) O3[d] += lam * w[d];
+        }
+        for (int d = 0; d < 3; ++d) sm[L->acc + cpi * 3 + d] = O3[d];
+      }
+      __syncthreads();
+      double rdn = 0.0;
+      for (int idx = lane; idx < nv * BS; idx += kWave) {
+        const int a = idx / BS, d = (idx / M) % 3, m = idx % M;
+        const double v = Pxq(sm + L->x, idx) + gather_cp(L->acc, a, d, m);
+        sm[L->rd + idx] = v;
+        rdn = fmax(rdn, fabs(v));
+      }
+      rdn = wave_max(rdn);
+      __syncthreads();
+      if (rdn <= tol * (1.0 + qn) && rpn <= tol && mu <= tol) {
+        *status = 0;
+        break;
+      }
+      const bool near = rdn <= 1e3 * tol * (1.0 + qn) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
+      assemble_kkt(true);
+      if (lane == 0) *fail = 0;
+      __syncthreads();
+      factor(fail);
+      __syncthreads();
+      if (*fail) {
+        *status = near ? 0 : 2;
+        break;
+      }
+      // Affine (predictor) direction: rc = s * lam.
+      for (int k = lane; k < nc; k += kWave) sm[L->prod + k] = sm[L->s + k] * sm[L->lam + k];
+      __syncthreads();
+      direction();
+      const double a_aff = max_step();
+      double mua = 0.0;
+      for (int k = lane; k < nc; k += kWave)
+        mua += (sm[L->s + k] + a_aff * sm[L->ds + k]) * (sm[L->lam + k] + a_aff * sm[L->dl + k]);
+      mua = wave_sum(mua) / nc;
+      const double ratio = mua / mu;
+      const double sigma = ratio * ratio * ratio;
+      __syncthreads();
+      // Corrector: rc = s lam + ds_aff dl_aff - sigma mu.
+      for (int k = lane; k < nc; k += kWave)
+        sm[L->prod + k] = sm[L->s + k] * sm[L->lam + k] + sm[L->ds + k] * sm[L->dl + k] - sigma * mu;
+      __syncthreads();
+      direction();
+      const double alpha = fmin(1.0, 0.99 * max_step());
+      double dxn = 0.0;
+      for (int idx = lane; idx < nv * BS; idx += kWave) dxn = fmax(dxn, fabs(sm[L->dx + idx]));
+      dxn = wave_max(dxn);
+      if (!(alpha > 0.0) || !(dxn < 1e300) || !(sigma < 1e300)) {
+        *status = near ? 0 : 2;
+        break;
+      }
+      for (int idx = lane; idx < nv * BS; idx += kWave) sm[L->x + idx] += alpha * sm[L->dx + idx];
+      for (int k = lane; k < nc; k += kWave) {
+        sm[L->s + k] += alpha * sm[L->ds + k];
+        sm[L->lam + k] += alpha * sm[L->dl + k];
+      }
+      __syncthreads();
+    }
+    return it;
+  }
+};
+
+}  // namespace mtg

@@ -910,6 +910,9 @@ struct TubeProblem {
         status = 0;
         break;
       }
+      // Safeguard: on a breakdown of the KKT factorisation or step, stop at
+      // the current iterate and accept it if within 1e3 * tol.
+      const bool near = rdn <= 1e3 * tol * (1.0 + qnorm) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
       // K = P + sum lam_k Q_k + sum (lam_k/s_k) a_k a_k^T.
       Mat Kmat = P;
       for (int k = 0; k < m; ++k) {
@@ -921,7 +924,10 @@ struct TubeProblem {
             Kmat(c.supp[u], c.supp[v]) +=
                 lam[k] * c.quad[static_cast<size_t>(u) * ms + v] + w * a[k][u] * a[k][v];
       }
-      if (!cholesky(&Kmat)) return -21;
+      if (!cholesky(&Kmat)) {
+        status = near ? 0 : 2;
+        break;
+      }
       auto direction = [&](const std::vector<double>& rc, std::vector<double>* dx,
                            std::vector<double>* dl, std::vector<double>* ds) {
         std::vector<double> rhs(n);
@@ -963,6 +969,12 @@ struct TubeProblem {
       for (int k = 0; k < m; ++k) rc[k] = s[k] * lam[k] + ds[k] * dl[k] - sigma * mu;
       direction(rc, &dx, &dl, &ds);
       const double alpha = std::min(1.0, 0.99 * max_step(dl, ds));
+      double dxn = 0.0;
+      for (int i = 0; i < n; ++i) dxn = std::max(dxn, std::fabs(dx[i]));
+      if (!(alpha > 0.0) || !(dxn < 1e300) || !(sigma < 1e300)) {
+        status = near ? 0 : 2;
+        break;
+      }
       for (int i = 0; i < n; ++i) x[i] += alpha * dx[i];
       for (int k = 0; k < m; ++k) {
         s[k] += alpha * ds[k];
@@ -1269,6 +1281,7 @@ int orc_tube_qcqp_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
   int it = 0;
   int status = tp.solveIPM(tol, max_iter, &x, &it);
   if (status < 0) return status;
+  if (status == 2) status = -22;  // numerical breakdown away from the optimum
   tp.recover(x);
   if (x_out) std::memcpy(x_out, x.data(), sizeof(double) * x.size());
   if (coeffs) std::memcpy(coeffs, tp.lp.coeffs.data(), sizeof(double) * tp.lp.coeffs.size());

@@ -1,0 +1,77 @@
+"""Multi-process (gloo, world_size 2 and 3) tests of the sharded selection
+path: each rank solves its contiguous shard (here with the oracle on CPU,
+standing in for the per-GPU kernel), costs are all-gathered, the global
+argmin and the winner's coefficients agree with a single-process solve."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _solve_shard(seeds, N=10, S=6, D=3):
+    sys.path[:0] = [os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")]
+    import pyoracle
+    costs, coeffs = [], []
+    for sd in seeds:
+        v = pyoracle.random_vertices(N // 2 - 1, S, D, -10.0, 10.0, int(sd))
+        t = pyoracle.estimate_segment_times(v, 3.0, 5.0)
+        sol = pyoracle.linear_solve(N, 4, v, t)
+        costs.append(sol["cost"])
+        coeffs.append(sol["coeffs"])
+    return np.array(costs), np.array(coeffs)
+
+
+def _worker(rank, world, port, global_batch, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, REPO)
+    import torch.distributed as dist
+    from mav_tube_trajectory_generation_amd.shard import (broadcast_best, select_best,
+                                                          shard_range)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    start, count = shard_range(global_batch, world, rank)
+    costs, coeffs = _solve_shard(range(105 + start, 105 + start + count))
+    idx, cost, owner = select_best(torch.from_numpy(costs), global_batch)
+    best = broadcast_best(torch.from_numpy(coeffs), idx, owner, global_batch)
+    result_q.put((rank, idx, cost, owner, best.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,global_batch", [(2, 10), (3, 11)])
+def test_sharded_selection_matches_single_process(world, global_batch):
+    from mav_tube_trajectory_generation_amd.shard import shard_range
+    # Shards cover the batch exactly once.
+    covered = []
+    for r in range(world):
+        s, c = shard_range(global_batch, world, r)
+        covered += list(range(s, s + c))
+    assert covered == list(range(global_batch))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, global_batch, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    costs, coeffs = _solve_shard(range(105, 105 + global_batch))
+    want = int(np.argmin(costs))
+    for rank, idx, cost, owner, best in results:
+        assert idx == want
+        assert cost == costs[want]
+        assert np.array_equal(best, coeffs[want])

@@ -42,8 +42,49 @@ def test_time_cost_vs_oracle(ctx, dev, oracle, grad_mode):
         assert rel_err(cost[b], J) <= (1e-9 if well else 1e-6), b
         if grad_mode:
             gg = out["grad"].cpu().numpy()[b]
-            tol = 1e-6 if (well or grad_mode == 1) else 1e-4
-            assert np.max(np.abs(gg - g)) <= tol * np.max(np.abs(g)) + 1e-9, (b, gg, g)
+            if well:
+                assert np.max(np.abs(gg - g)) <= 1e-6 * np.max(np.abs(g)) + 1e-9, (b, gg, g)
+            elif grad_mode == 1:
+                # The reference differences two full J_d sums
+                # (nonlinear_impl:2549-2566); with one 0.1 s segment J_d is
+                # ~1e14 and that cancels ~1e-3 of the gradient away.  Check
+                # against the same derivative formed segment-wise from the
+                # oracle's solution and H matrices instead; that solution is
+                # itself only ~1e-5 accurate here (cond(A(0.1)) ~ 1e10).
+                ref = _grad_mode1_segmentwise(oracle, v, times[b], 0.1, 0.1, 1.0)
+                assert np.max(np.abs(gg - ref)) <= 1e-4 * np.max(np.abs(ref)), (b, gg, ref)
+            else:
+                assert np.max(np.abs(gg - g)) <= 1e-4 * np.max(np.abs(g)), (b, gg, g)
+
+
+def _vertex_derivs(v, sol, N):
+    """All vertex derivatives x[(S+1), M, D] from the oracle's d_f / d_p."""
+    M = N // 2
+    x = np.zeros((v.S + 1, M, v.D))
+    f = p = 0
+    for vi in range(v.S + 1):
+        for k in range(M):
+            if k < v.K and v.mask[vi, k]:
+                x[vi, k] = sol["df"][:, f]
+                f += 1
+            else:
+                x[vi, k] = sol["dp"][:, p]
+                p += 1
+    return x
+
+
+def _grad_mode1_segmentwise(oracle, v, t, inc, w_d, w_t):
+    sol = oracle.linear_solve(N, R, v, t)
+    x = _vertex_derivs(v, sol, N)
+    g = np.zeros(len(t))
+    for n, Tn in enumerate(t):
+        ts = 0.1 if Tn <= 0.1 else Tn - inc
+        tb = 0.1 if Tn <= 0.1 else Tn + inc
+        e = np.concatenate([x[n], x[n + 1]], axis=0)  # [N, D]
+        Hs = oracle.segment_matrices(N, R, ts)[3]
+        Hb = oracle.segment_matrices(N, R, tb)[3]
+        g[n] = w_d * np.einsum("ad,ab,bd->", e, Hb - Hs, e) / (2 * inc) + w_t
+    return g
 
 
 def _optimize_reference(oracle, v, t0, max_evals, time_penalty=500.0, inc=0.1):

@@ -1,0 +1,135 @@
+"""GPU tube QCQP (mtg_tube_residuals / mtg_tube_solve) against the oracle.
+
+The reference solves this problem with MOSEK (qcqp_impl:476-788), which is
+absent: parity of the solve is against the oracle's own interior-point method
+("parity unpinned" vs MOSEK; the oracle IPM is cross-checked with SciPy in
+tests/test_tube_oracle.py).  Constraint residuals are pinned to the oracle's
+reference-faithful assembly of qcqp_impl:321-474.
+"""
+import numpy as np
+import pytest
+
+from helpers import rel_err, rel_err_coeffs
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+N, R = 10, 4
+M = N // 2
+
+
+def main_cpp_vertices(oracle):
+    """The 4-segment geometry of src/main.cpp:26-53 (radii 0.15, :55-67)."""
+    S, D = 4, 3
+    mask = np.zeros((S + 1, M), np.uint8)
+    vals = np.zeros((S + 1, M, D))
+    pts = [(2.7, 9.5, 4.8), (3.50796, 4.34802, 4.56653), (3.95552, 3.23008, 4.75131),
+           (5.06673, 2.31032, 4.79433), (7.0, 2.2, 4.8)]
+    for v, p in enumerate(pts):
+        mask[v, 0] = 1
+        vals[v, 0] = p
+    mask[0, :] = 1
+    mask[S, :] = 1
+    return oracle.Vertices(mask, vals)
+
+
+def tube_inputs(v):
+    """positions [(S+1), 3] and tube fixed values [3, N] (start derivatives
+    then end derivatives, qcqp_impl:48-65)."""
+    S = v.S
+    pos = v.vals[:, 0, :].copy()
+    fv = np.zeros((3, N))
+    fv[:, :M] = v.vals[0, :M, :].T
+    fv[:, M:] = v.vals[S, :M, :].T
+    return pos, fv
+
+
+def _gpu(ctx, dev, items, radius=0.15, times_cp=None, tol=1e-10):
+    import mav_tube_trajectory_generation_amd as mtg
+    B = len(items)
+    S = items[0][0].S
+    pos = np.stack([tube_inputs(v)[0] for v, _ in items])
+    fv = np.stack([tube_inputs(v)[1] for v, _ in items])
+    times = np.stack([t for _, t in items])
+    tcp = times if times_cp is None else times_cp
+    radii = np.full((B, S, 2), radius)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    out = mtg.tube_solve(ctx, N, R, T(pos), T(fv), T(tcp), T(times), T(radii), tol=tol,
+                         max_iter=100)
+    torch.cuda.synchronize()
+    res = mtg.tube_residuals(ctx, N, R, T(pos), T(fv), T(tcp), T(times), T(radii), out["x"])
+    o = {k: v.cpu().numpy() for k, v in out.items()}
+    o["resid"] = res.cpu().numpy()
+    return o
+
+
+def test_main_cpp_fixture(ctx, dev, oracle):
+    v = main_cpp_vertices(oracle)
+    t = oracle.estimate_segment_times(v, 2.0, 2.0)  # main.cpp:73-74
+    radii = np.full((4, 2), 0.15)
+    ref = oracle.tube_solve(N, R, v, t, radii, tol=1e-10, max_iter=100)
+    assert ref["status"] == 0
+    out = _gpu(ctx, dev, [(v, t)])
+    assert out["status"][0] == 0, out["status"]
+    assert abs(int(out["iters"][0]) - ref["iters"]) <= 2
+    assert rel_err_coeffs(out["x"][0], ref["x"]) <= 1e-6
+    assert rel_err_coeffs(out["coeffs"][0], ref["coeffs"]) <= 1e-6
+    assert rel_err(out["cost"][0], ref["cost"]) <= 1e-6
+    # Feasible: every residual <= 0 up to the IPM tolerance.
+    assert out["resid"][0].max() <= 1e-8
+
+
+def test_residuals_match_oracle_assembly(ctx, dev, oracle):
+    """g_k(x) of the GPU (control-point form) vs the oracle's reference-
+    faithful quadratic forms (qcqp_impl:357-474) at arbitrary x."""
+    import mav_tube_trajectory_generation_amd as mtg
+    rng = np.random.default_rng(3)
+    for S, seed in ((4, 11), (10, 105)):
+        v = oracle.random_vertices(M - 1, S, 3, -10.0, 10.0, seed)
+        t = oracle.estimate_segment_times(v, 3.0, 5.0)
+        tcp = t * rng.uniform(0.8, 1.2, size=S)  # stale control-point map quirk
+        radii = np.column_stack([rng.uniform(0.1, 0.5, S), rng.uniform(0.1, 0.5, S)])
+        n = (S - 1) * M * 3
+        x = rng.normal(size=n)
+        ref = oracle.tube_residuals(N, R, v, t, radii, x, times_cp=tcp)
+        pos, fv = tube_inputs(v)
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        got = mtg.tube_residuals(ctx, N, R, T(pos[None]), T(fv[None]), T(tcp[None]), T(t[None]),
+                                 T(radii[None]), T(x[None])).cpu().numpy()[0]
+        assert got.shape == ref.shape == (mtg.tube_num_constraints(N, S),)
+        scale = np.maximum(1.0, np.abs(ref))
+        assert np.max(np.abs(got - ref) / scale) <= 1e-10
+
+
+def test_random_batch_vs_oracle(ctx, dev, oracle):
+    """BASELINE config 3 shape (reduced batch for the oracle comparison)."""
+    S, B = 10, 12
+    items = []
+    for b in range(B):
+        v = oracle.random_vertices(M - 1, S, 3, -10.0, 10.0, 105 + b)
+        items.append((v, oracle.estimate_segment_times(v, 3.0, 5.0)))
+    out = _gpu(ctx, dev, items)
+    radii = np.full((S, 2), 0.15)
+    for b, (v, t) in enumerate(items):
+        ref = oracle.tube_solve(N, R, v, t, radii, tol=1e-10, max_iter=100)
+        assert out["status"][b] == ref["status"] == 0, b
+        assert rel_err_coeffs(out["x"][b], ref["x"]) <= 1e-6, b
+        assert rel_err_coeffs(out["coeffs"][b], ref["coeffs"]) <= 1e-6, b
+        assert rel_err(out["cost"][b], ref["cost"]) <= 1e-6, b
+        assert out["resid"][b].max() <= 1e-8, b
+
+
+def test_stale_control_point_times(ctx, dev, oracle):
+    """Inside objectiveFunctionTime the control-point maps keep the setup
+    times (qcqp_impl:152-157 vs :183): times_cp != times."""
+    S = 6
+    v = oracle.random_vertices(M - 1, S, 3, -10.0, 10.0, 77)
+    t0 = oracle.estimate_segment_times(v, 3.0, 5.0)
+    t = t0 * 0.9
+    radii = np.full((S, 2), 0.15)
+    ref = oracle.tube_solve(N, R, v, t, radii, times_cp=t0, tol=1e-10, max_iter=100)
+    out = _gpu(ctx, dev, [(v, t)], times_cp=t0[None])
+    assert out["status"][0] == ref["status"] == 0
+    assert rel_err_coeffs(out["coeffs"][0], ref["coeffs"]) <= 1e-6
+    assert rel_err(out["cost"][0], ref["cost"]) <= 1e-6
