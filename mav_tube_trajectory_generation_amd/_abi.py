@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmtg_hip.so")
+# MTG_LIB_PATH selects a diagnostic build (tools/stamps.py); default in-tree.
+LIB_PATH = os.environ.get("MTG_LIB_PATH", os.path.join(_HERE, "libmtg_hip.so"))
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _u8p = ctypes.POINTER(ctypes.c_uint8)

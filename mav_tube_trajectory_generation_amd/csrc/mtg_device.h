@@ -18,18 +18,42 @@
 //     (M = N/2 derivatives per vertex).  Fixed derivatives are "pinned"
 //     (identity row/column, value on the right-hand side), which leaves the
 //     free-free system R_pp d_p = -R_pf d_f unchanged while giving every
-//     trajectory the same uniform block structure.  It is solved by a block
-//     Cholesky sweep over the S+1 vertices: lanes build the Schur complement
-//     and right-hand side in parallel, then lane c factors the M x M block in
-//     registers and triangular-solves column c (M columns of the coupling
-//     block + D right-hand sides), so one barrier pair per vertex.
-// LDS holds everything a trajectory touches (about 9 KB at S=10, N=10, D=3);
-// HBM sees only the compact inputs (times, d_f) and the outputs.
+//     trajectory the same uniform block structure.
+//   * Block LDL^T sweep over the S+1 vertices.  Per vertex one parallel Schur
+//     step (lanes over block entries) and one factor step in which lane c
+//     factors the M x M block in registers and turns column c of the coupling
+//     block / right-hand side into Z_v = S_v^-1 O_v, z_v = S_v^-1 r_v.  The
+//     back substitution is then the affine recurrence x_v = z_v - Z_v x_{v+1}
+//     (M*D lanes, one step per vertex).  Fully fixed vertices (start/end of
+//     the standard pattern) skip the factorisation.
+// LDS holds everything a trajectory touches (about 11 KB at S=10, N=10,
+// D=3); HBM sees only the compact inputs (times, d_f) and the outputs.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "mtg_internal.h"
+
+// Diagnostic build only (make STAMPS=1): s_memtime stamps of workgroup 0 at
+// phase boundaries into g_mtg_stamps (read by mtg_debug_stamps).  The
+// shipped library never defines MTG_STAMPS.
+#ifdef MTG_STAMPS
+__device__ unsigned long long g_mtg_stamps[512];
+#define MTG_STAMP(slot)                                                     \
+  do {                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                              \
+      unsigned long long t_;                                                \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      g_mtg_stamps[(slot)] = t_;                                            \
+    }                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+  } while (0)
+#else
+#define MTG_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
 
 namespace mtg {
 
@@ -41,11 +65,10 @@ struct Layout {
   int pw;          // S * (2N-1): T_s^e for e in [-(N-1), N-1]
   int T;           // S segment times
   int dv;          // (S+1)*M*D vertex derivatives (fixed values, then x)
-  int Dt;          // (S+1)*M*M pinned diagonal blocks -> Schur complements
-  int Ot;          // S*M*M     pinned coupling blocks -> W_v = L_v^-1 O_v
-  int Bt;          // (S+1)*M*D right-hand sides -> y_v = L_v^-1 r_v
-  int Lu;          // (S+1)*M*M unit-lower LDL^T factors
-  int dinv;        // (S+1)*M   inverse pivots
+  int Dt;          // (S+1)*M*M diagonal blocks -> pinned -> Schur complements
+  int Ot;          // S*M*M     coupling blocks -> pinned
+  int Zt;          // S*M*M     Z_v = S_v^-1 O_v
+  int Bt;          // (S+1)*M*D right-hand sides -> z_v = S_v^-1 r_v
   int aux;         // 4*S extra (optimiser state)
   int ndouble;
   int slot;        // (S+1)*M int slots (after the doubles)
@@ -64,9 +87,8 @@ __host__ __device__ inline Layout make_layout(int N, int S, int D) {
   l.dv = o;   o += (S + 1) * M * D;
   l.Dt = o;   o += (S + 1) * M * M;
   l.Ot = o;   o += S * M * M;
+  l.Zt = o;   o += S * M * M;
   l.Bt = o;   o += (S + 1) * M * D;
-  l.Lu = o;   o += (S + 1) * M * M;
-  l.dinv = o; o += (S + 1) * M;
   l.aux = o;  o += 4 * S + 8;
   l.ndouble = o;
   l.slot = 0;
@@ -92,9 +114,11 @@ struct Traj {
   static constexpr int PWN = 2 * N - 1;
   int S, D, r;
   const Layout* lay;
-  double* sm;   // double region
-  int* si;      // int region
+  double* sm;         // double region
+  int* si;            // int region
   int lane;
+  uint64_t fmask;     // fixed-pattern bits (v*M+k) when (S+1)*M <= 64
+  bool use_mask;
 
   __device__ double* tabH() const { return sm + lay->tabH; }
   __device__ double* tabA() const { return sm + lay->tabA; }
@@ -106,7 +130,17 @@ struct Traj {
 
   // T_s^e, e in [-(N-1), N-1].
   __device__ double pwr(int s, int e) const { return pw()[s * PWN + e + (N - 1)]; }
-  __device__ bool fixed_at(int v, int k) const { return slot()[v * M + k] >= 0; }
+  // Pattern test: SGPR bitmask when it fits (wave-uniform, no LDS load).
+  __device__ bool fixed_at(int v, int k) const {
+    const int idx = v * M + k;
+    return use_mask ? ((fmask >> idx) & 1ull) != 0 : slot()[idx] >= 0;
+  }
+  __device__ bool vertex_fixed(int v) const {
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < M; ++k) all = all && fixed_at(v, k);
+    return all;
+  }
 
   // H_s block entry: row (a_blk, j), column (b_blk, k); a_blk 0 = start
   // vertex s, 1 = end vertex s+1.
@@ -114,48 +148,53 @@ struct Traj {
     return tabH()[(ab * M + j) * N + bb * M + k] * pwr(s, 1 - 2 * r + j + k);
   }
 
-  // Load the constant tables and the slot map (global -> LDS).
-  __device__ void load_static(const double* __restrict__ tab,
-                              const int* __restrict__ slots) {
+  // All global inputs of one trajectory in a single round of independent
+  // loads: tables, slots, times, and d_f scattered into dv (fixed_map gives
+  // the (vertex, derivative) slot of fixed index f).
+  __device__ void load_inputs(const double* __restrict__ tab, const int* __restrict__ slots,
+                              const int* __restrict__ fixed_map,
+                              const double* __restrict__ times_b,
+                              const double* __restrict__ df, int nf) {
     for (int i = lane; i < 2 * N * N; i += kWave) sm[lay->tabH + i] = tab[i];
     for (int i = lane; i < (S + 1) * M; i += kWave) slot()[i] = slots[i];
+    for (int i = lane; i < S; i += kWave) T()[i] = times_b[i];
+    // Free entries are zero; fixed ones take d_f (disjoint writes).
+    for (int i = lane; i < (S + 1) * M * D; i += kWave) {
+      const int vk = i / D;
+      if (slots[vk] < 0) dv()[i] = 0.0;
+    }
+    for (int i = lane; i < D * nf; i += kWave) {
+      const int d = i / nf, f = i % nf;
+      dv()[fixed_map[f] * D + d] = df[i];
+    }
     if (lane == 0) flag()[0] = 0;
   }
 
-  // Powers T_s^e by repeated multiplication (exact integer exponents).
-  // Sets flag()[0] |= 1 if any time is not > 0.
+  // Powers T_s^e by two multiplication chains per segment (exact integer
+  // exponents; 1/T by rcp64).  Sets flag()[0] |= 1 if any time is not > 0.
   __device__ void compute_powers() {
-    for (int i = lane; i < S * PWN; i += kWave) {
-      const int s = i / PWN;
-      const int e = i % PWN - (N - 1);
+    for (int s = lane; s < S; s += kWave) {
       const double t = T()[s];
       if (!(t > 0.0) || !(t < 1e300)) atomicOr(&flag()[0], 1);
-      const double base = e < 0 ? 1.0 / t : t;
-      const int n = e < 0 ? -e : e;
-      double p = 1.0;
-      for (int q = 0; q < n; ++q) p *= base;
-      pw()[i] = p;
-    }
-  }
-
-  // Scatter compact fixed values d_f (D x nf, global) into dv; free entries 0.
-  __device__ void load_fixed(const double* __restrict__ df, int nf) {
-    for (int i = lane; i < (S + 1) * M * D; i += kWave) {
-      const int v = i / (M * D);
-      const int rem = i % (M * D);
-      const int k = rem / D;
-      const int d = rem % D;
-      const int sl = slot()[v * M + k];
-      dv()[i] = sl >= 0 ? df[d * nf + sl] : 0.0;
+      const double inv = rcp64(t);
+      double* p = pw() + s * PWN + (N - 1);
+      double up = 1.0, dn = 1.0;
+      p[0] = 1.0;
+#pragma unroll
+      for (int e = 1; e < N; ++e) {
+        up *= t;
+        dn *= inv;
+        p[e] = up;
+        p[-e] = dn;
+      }
     }
   }
 
   // Re-zero the free entries of dv (before a re-solve that reuses dv).
   __device__ void clear_free() {
     for (int i = lane; i < (S + 1) * M * D; i += kWave) {
-      const int v = i / (M * D);
-      const int k = (i % (M * D)) / D;
-      if (slot()[v * M + k] < 0) dv()[i] = 0.0;
+      const int vk = i / D;
+      if (!fixed_at(vk / M, vk % M)) dv()[i] = 0.0;
     }
   }
 
@@ -163,9 +202,7 @@ struct Traj {
     return dv()[(v * M + k) * D + d];
   }
 
-  // Phase C (parallel over all vertices): pinned diagonal blocks, pinned
-  // coupling blocks and right-hand sides b = -R_pf d_f, so the serial sweep
-  // below only does Schur updates and factorisations.
+  // Blocks of R in vertex order, b = -R_pf d_f, then pinning.
   __device__ void assemble() {
     double* Dt = sm + lay->Dt;
     double* Ot = sm + lay->Ot;
@@ -173,21 +210,16 @@ struct Traj {
     for (int i = lane; i < (S + 1) * M * M; i += kWave) {
       const int v = i / (M * M);
       const int j = (i / M) % M, k = i % M;
-      double val;
-      if (fixed_at(v, j) || fixed_at(v, k)) {
-        val = (j == k) ? 1.0 : 0.0;
-      } else {
-        val = 0.0;
-        if (v > 0) val += H(v - 1, 1, 1, j, k);
-        if (v < S) val += H(v, 0, 0, j, k);
+      double val = 0.0;
+      if (v > 0) val += H(v - 1, 1, 1, j, k);
+      if (v < S) {
+        val += H(v, 0, 0, j, k);
+        Ot[i] = H(v, 0, 1, j, k);
       }
       Dt[i] = val;
     }
-    for (int i = lane; i < S * M * M; i += kWave) {
-      const int v = i / (M * M);
-      const int j = (i / M) % M, k = i % M;
-      Ot[i] = (fixed_at(v, j) || fixed_at(v + 1, k)) ? 0.0 : H(v, 0, 1, j, k);
-    }
+    __syncthreads();
+    // dv is zero at free entries, so these sums run over fixed columns only.
     for (int i = lane; i < (S + 1) * M * D; i += kWave) {
       const int v = i / (M * D);
       const int j = (i / D) % M, d = i % D;
@@ -195,62 +227,81 @@ struct Traj {
       if (fixed_at(v, j)) {
         val = dval(v, j, d);
       } else {
-        // dv is zero at free entries, so these sums run over fixed columns.
+        const double* Dv = Dt + v * M * M;
         double b = 0.0;
 #pragma unroll
-        for (int k = 0; k < M; ++k) {
-          double dkk = 0.0;
-          if (v > 0) dkk += H(v - 1, 1, 1, j, k);
-          if (v < S) dkk += H(v, 0, 0, j, k);
-          b += dkk * dval(v, k, d);
-          if (v < S) b += H(v, 0, 1, j, k) * dval(v + 1, k, d);
-          if (v > 0) b += H(v - 1, 1, 0, j, k) * dval(v - 1, k, d);
+        for (int k = 0; k < M; ++k) b += Dv[j * M + k] * dval(v, k, d);
+        if (v < S) {
+          const double* Ov = Ot + v * M * M;
+#pragma unroll
+          for (int k = 0; k < M; ++k) b += Ov[j * M + k] * dval(v + 1, k, d);
+        }
+        if (v > 0) {
+          const double* Op = Ot + (v - 1) * M * M;
+#pragma unroll
+          for (int k = 0; k < M; ++k) b += Op[k * M + j] * dval(v - 1, k, d);
         }
         val = -b;
       }
       Bt[i] = val;
     }
+    __syncthreads();
+    for (int i = lane; i < (S + 1) * M * M; i += kWave) {
+      const int v = i / (M * M);
+      const int j = (i / M) % M, k = i % M;
+      if (fixed_at(v, j) || fixed_at(v, k)) Dt[i] = (j == k) ? 1.0 : 0.0;
+      if (v < S && (fixed_at(v, j) || fixed_at(v + 1, k))) Ot[i] = 0.0;
+    }
   }
 
-  // Block LDL^T forward sweep over the S+1 vertices, then back substitution.
-  // On exit dv holds every vertex derivative (fixed values untouched).
-  // Sets flag()[0] |= 2 on a non-positive pivot.
+  // Block LDL^T forward sweep and back substitution.  On exit dv holds every
+  // vertex derivative (fixed values untouched).  flag()[0] |= 2 on a
+  // non-positive pivot.
   __device__ void solve() {
     double* Dt = sm + lay->Dt;
     double* Ot = sm + lay->Ot;
+    double* Zt = sm + lay->Zt;
     double* Bt = sm + lay->Bt;
-    double* Lu = sm + lay->Lu;
-    double* dinv = sm + lay->dinv;
     assemble();
     __syncthreads();
+    MTG_STAMP(3);
     for (int v = 0; v <= S; ++v) {
       double* Sv = Dt + v * M * M;
       double* Rv = Bt + v * M * D;
+      if (vertex_fixed(v)) {
+        // Identity block: z_v = values (already in Bt), Z_v = 0 (pinned rows).
+        if (v < S)
+          for (int i = lane; i < M * M; i += kWave) Zt[v * M * M + i] = 0.0;
+        __syncthreads();
+        MTG_STAMP(100 + 2 * v);
+        MTG_STAMP(101 + 2 * v);
+        continue;
+      }
       if (v > 0) {
-        // Schur update with the previous vertex:
-        //   S_v = Dt_v - W^T diag(dinv) W,  r_v = b_v - W^T diag(dinv) y.
-        const double* Wp = Ot + (v - 1) * M * M;
-        const double* Yp = Bt + (v - 1) * M * D;
-        const double* dp = dinv + (v - 1) * M;
+        // Schur step: S_v -= O_{v-1}^T Z_{v-1},  r_v -= O_{v-1}^T z_{v-1}.
+        const double* Op = Ot + (v - 1) * M * M;
+        const double* Zp = Zt + (v - 1) * M * M;
+        const double* zp = Bt + (v - 1) * M * D;
         if (lane < M * M) {
           const int j = lane / M, k = lane % M;
           double s = Sv[lane];
 #pragma unroll
-          for (int m = 0; m < M; ++m) s -= Wp[m * M + j] * dp[m] * Wp[m * M + k];
+          for (int m = 0; m < M; ++m) s -= Op[m * M + j] * Zp[m * M + k];
           Sv[lane] = s;
         } else if (lane < M * M + M * D) {
           const int idx = lane - M * M;
           const int j = idx / D, d = idx % D;
           double s = Rv[idx];
 #pragma unroll
-          for (int m = 0; m < M; ++m) s -= Wp[m * M + j] * dp[m] * Yp[m * D + d];
+          for (int m = 0; m < M; ++m) s -= Op[m * M + j] * zp[m * D + d];
           Rv[idx] = s;
         }
         __syncthreads();
       }
+      MTG_STAMP(100 + 2 * v);
       // Lane -> column: 0..M-1 the coupling block (absent at v = S), then
       // the D right-hand sides.  Each active lane factors S_v = L Delta L^T
-      // in registers (redundantly) and forward-substitutes its column.
+      // in registers (redundantly) and maps its column c to S_v^-1 c.
       int col;
       if (v < S)
         col = lane < M + D ? lane : -1;
@@ -263,6 +314,11 @@ struct Traj {
         for (int i = 0; i < M; ++i)
 #pragma unroll
           for (int j = 0; j <= i; ++j) Lr[i][j] = Sv[i * M + j];
+        const bool isW = col < M;
+        double x[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          x[i] = isW ? Ot[v * M * M + i * M + col] : Rv[i * D + (col - M)];
         bool ok = true;
 #pragma unroll
         for (int j = 0; j < M; ++j) {
@@ -281,11 +337,7 @@ struct Traj {
           }
         }
         if (!ok) atomicOr(&flag()[0], 2);
-        // Unit-lower L[i][j] = Lr[i][j] * inv[j].
-        double x[M];
-        const bool isW = col < M;
-#pragma unroll
-        for (int i = 0; i < M; ++i) x[i] = isW ? Ot[v * M * M + i * M + col] : Rv[i * D + (col - M)];
+        // x <- L^-1 x (unit lower, L[i][k] = Lr[i][k] inv[k]) ...
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           double s = x[i];
@@ -293,62 +345,43 @@ struct Traj {
           for (int k = 0; k < i; ++k) s -= (Lr[i][k] * inv[k]) * x[k];
           x[i] = s;
         }
+        // ... then x <- L^-T Delta^-1 x.
+#pragma unroll
+        for (int i = M - 1; i >= 0; --i) {
+          double s = x[i] * inv[i];
+#pragma unroll
+          for (int k = i + 1; k < M; ++k) s -= (Lr[k][i] * inv[i]) * x[k];
+          x[i] = s;
+        }
         if (isW) {
 #pragma unroll
-          for (int i = 0; i < M; ++i) Ot[v * M * M + i * M + col] = x[i];
+          for (int i = 0; i < M; ++i) Zt[v * M * M + i * M + col] = x[i];
         } else {
 #pragma unroll
           for (int i = 0; i < M; ++i) Rv[i * D + (col - M)] = x[i];
         }
-        if (lane == 0) {
+      }
+      __syncthreads();
+      MTG_STAMP(101 + 2 * v);
+    }
+    MTG_STAMP(4);
+    // Back substitution x_v = z_v - Z_v x_{v+1}, lanes over (i, d).
+    for (int v = S; v >= 0; --v) {
+      if (lane < M * D) {
+        const int i = lane / D, d = lane % D;
+        if (!fixed_at(v, i)) {
+          double s = Bt[v * M * D + lane];
+          if (v < S) {
+            const double* Zv = Zt + v * M * M;
 #pragma unroll
-          for (int i = 0; i < M; ++i) {
-            dinv[v * M + i] = inv[i];
-#pragma unroll
-            for (int j = 0; j < i; ++j) Lu[v * M * M + i * M + j] = Lr[i][j] * inv[j];
+            for (int k = 0; k < M; ++k) s -= Zv[i * M + k] * dval(v + 1, k, d);
           }
+          dv()[(v * M + i) * D + d] = s;
         }
       }
       __syncthreads();
     }
-    // Back substitution x_v = L_v^-T diag(dinv_v) (y_v - W_v x_{v+1}), one
-    // lane per dimension.
-    if (lane < D) {
-      const int d = lane;
-      double xn[M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) xn[i] = 0.0;
-      for (int v = S; v >= 0; --v) {
-        const double* L = Lu + v * M * M;
-        const double* Wv = Ot + v * M * M;
-        const double* Yv = Bt + v * M * D;
-        const double* di = dinv + v * M;
-        double t[M];
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          double s = Yv[i * D + d];
-          if (v < S) {
-#pragma unroll
-            for (int k = 0; k < M; ++k) s -= Wv[i * M + k] * xn[k];
-          }
-          t[i] = s * di[i];
-        }
-#pragma unroll
-        for (int i = M - 1; i >= 0; --i) {
-          double s = t[i];
-#pragma unroll
-          for (int k = i + 1; k < M; ++k) s -= L[k * M + i] * t[k];
-          t[i] = s;
-        }
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          xn[i] = t[i];
-          // Pinned entries come back as their value; keep the input bits.
-          if (!fixed_at(v, i)) dv()[(v * M + i) * D + d] = t[i];
-        }
-      }
-    }
-    __syncthreads();
+    MTG_STAMP(5);
   }
 
   // Wave-wide sum (all 64 lanes receive it).
@@ -358,42 +391,59 @@ struct Traj {
     return x;
   }
 
-  // One pass over (segment, dimension, coefficient k) with e = [x_s; x_{s+1}]:
+  // One lane per (segment, dimension) with e = [x_s; x_{s+1}] in registers:
   //   c_s[d][k] = sum_j A(1)^-1[k][j] T_s^(j mod M - k) e_j   (coefficients,
-  //               linear_impl:254-275; written to `out` when non-null)
-  //   cost     += e_k (H_s e)_k                               (computeCost,
+  //               linear_impl:254-275; written to `out` when kCoeffs)
+  //   cost     += e^T H_s e                                   (computeCost,
   //               linear_impl:113-130: 0.5 c^T Q c == 0.5 e^T H e)
-  // Returns computeCost() on every lane.
-  __device__ double coeffs_and_cost(double* __restrict__ out) const {
+  // Table entries have compile-time indices and are read from global memory
+  // (`tab`, wave-uniform -> scalar loads).  Returns computeCost() on every
+  // lane.
+  template <bool kCoeffs>
+  __device__ double coeffs_and_cost(const double* __restrict__ tab,
+                                    double* __restrict__ out) const {
     double acc = 0.0;
-    const int n = S * D * N;
-    for (int i = lane; i < n; i += kWave) {
-      const int s = i / (D * N);
-      const int rem = i % (D * N);
-      const int d = rem / N;
-      const int k = rem % N;
-      const int lk = k % M;
-      double c = 0.0, h = 0.0;
+    for (int sd = lane; sd < S * D; sd += kWave) {
+      const int s = sd / D, d = sd % D;
+      double e[N];
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        const int l = j % M;
-        const double e = dval(s + j / M, l, d);
-        c += tabA()[k * N + j] * pwr(s, l - k) * e;
-        h += tabH()[k * N + j] * pwr(s, 1 - 2 * r + lk + l) * e;
+      for (int j = 0; j < N; ++j) e[j] = dval(s + j / M, j % M, d);
+      double ph[2 * M - 1];  // T^(1-2r+q), q = 0..2M-2
+#pragma unroll
+      for (int q = 0; q < 2 * M - 1; ++q) ph[q] = pwr(s, 1 - 2 * r + q);
+      double cs = 0.0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        double h = 0.0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) h += tab[k * N + j] * ph[(k % M) + (j % M)] * e[j];
+        cs += h * e[k];
       }
-      if (out) out[i] = c;
-      acc += h * dval(s + k / M, lk, d);
+      acc += cs;
+      if (kCoeffs) {
+        double pa[PWN];  // T^(q - (N-1))
+#pragma unroll
+        for (int q = 0; q < PWN; ++q) pa[q] = pw()[s * PWN + q];
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          double c = 0.0;
+#pragma unroll
+          for (int j = 0; j < N; ++j) c += tab[N * N + k * N + j] * pa[(j % M) - k + N - 1] * e[j];
+          out[sd * N + k] = c;
+        }
+      }
     }
     return 0.5 * wave_sum(acc);
   }
 
-  __device__ double cost() const { return coeffs_and_cost(nullptr); }
+  __device__ double cost(const double* __restrict__ tab) const {
+    return coeffs_and_cost<false>(tab, nullptr);
+  }
 
   // sum_d e_s^T H_s(tau) e_s for segment s at time tau (fixed e): the part of
   // getCostAndGradientDerivative's J_d that depends on T_s.
   __device__ double seg_energy_at(int s, double tau) const {
     double acc = 0.0;
-    // tau powers computed on the fly (per lane, small loops).
     const double inv = 1.0 / tau;
     for (int i = lane; i < D * N * N; i += kWave) {
       const int d = i / (N * N);

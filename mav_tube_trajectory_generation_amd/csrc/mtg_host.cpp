@@ -25,6 +25,7 @@ struct mtg_plan {
   mtg::PlanDev dev{};
   int* d_slots = nullptr;
   int* d_free_map = nullptr;
+  int* d_fixed_map = nullptr;
 };
 
 namespace {
@@ -203,12 +204,16 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fix
   const int M = N / 2;
   // setupConstraintReorderingMatrix (linear_impl:171-252): fixed and free
   // constraints each numbered in (vertex, derivative) order.
-  std::vector<int> slots((S + 1) * M), free_map;
+  std::vector<int> slots((S + 1) * M), free_map, fixed_map;
   int nf = 0, np = 0;
+  uint64_t fmask = 0;
+  const bool use_mask = (S + 1) * M <= 64;
   for (int v = 0; v <= S; ++v)
     for (int k = 0; k < M; ++k) {
       if (fixed_mask[v * M + k]) {
         slots[v * M + k] = nf++;
+        fixed_map.push_back(v * M + k);
+        if (use_mask) fmask |= 1ull << (v * M + k);
       } else {
         slots[v * M + k] = -(np + 1);
         free_map.push_back(v * M + k);
@@ -225,17 +230,27 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fix
     (void)hipFree(p->d_slots);
     return MTG_ERR_HIP;
   }
+  if (hipMalloc(&p->d_fixed_map, (fixed_map.size() + 1) * sizeof(int)) != hipSuccess) {
+    (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_free_map);
+    return MTG_ERR_HIP;
+  }
   hipError_t e = hipMemcpy(p->d_slots, slots.data(), slots.size() * sizeof(int),
                            hipMemcpyHostToDevice);
   if (e == hipSuccess && np)
     e = hipMemcpy(p->d_free_map, free_map.data(), free_map.size() * sizeof(int),
                   hipMemcpyHostToDevice);
+  if (e == hipSuccess && nf)
+    e = hipMemcpy(p->d_fixed_map, fixed_map.data(), fixed_map.size() * sizeof(int),
+                  hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(p->d_slots);
     (void)hipFree(p->d_free_map);
+    (void)hipFree(p->d_fixed_map);
     return MTG_ERR_HIP;
   }
-  p->dev = PlanDev{N, D, r, S, nf, np, tab, p->d_slots, p->d_free_map};
+  p->dev = PlanDev{N, D, r, S, nf, np, tab, p->d_slots, p->d_free_map, p->d_fixed_map,
+                   fmask, use_mask ? 1 : 0};
   *out = p.release();
   return MTG_OK;
 }
@@ -244,6 +259,7 @@ int mtg_plan_destroy(mtg_plan* plan) {
   if (!plan) return MTG_ERR_INVALID_ARG;
   (void)hipFree(plan->d_slots);
   (void)hipFree(plan->d_free_map);
+  (void)hipFree(plan->d_fixed_map);
   delete plan;
   return MTG_OK;
 }

@@ -18,6 +18,9 @@ struct PlanDev {
   const double* tab;       // H(1) then A(1)^-1, N*N each (device)
   const int* slots;        // (S+1)*M: fixed index f >= 0, or -(p+1) for free p
   const int* free_map;     // np: free index p -> v*M + k
+  const int* fixed_map;    // nf: fixed index f -> v*M + k
+  uint64_t fmask;          // bit v*M+k set iff fixed, valid when use_mask
+  int use_mask;            // (S+1)*M <= 64
 };
 
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,

@@ -15,23 +15,22 @@ namespace mtg {
 // solveLinear + computeCost, linear_impl:277-379, 113-130).
 template <int N>
 __global__ __launch_bounds__(kWave) void linear_solve_kernel(
-    int S, int D, int r, int nf, int np, const double* __restrict__ tab,
-    const int* __restrict__ slots, const int* __restrict__ free_map,
-    const double* __restrict__ fixed_vals, const double* __restrict__ times,
-    double* __restrict__ coeffs, double* __restrict__ cost,
-    double* __restrict__ free_vals, int32_t* __restrict__ status) {
+    PlanDev pl, const double* __restrict__ fixed_vals, const double* __restrict__ times,
+    double* __restrict__ coeffs, double* __restrict__ cost, double* __restrict__ free_vals,
+    int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf, np = pl.np;
   const Layout lay = make_layout(N, S, D);
-  Traj<N> t{S, D, r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
-            static_cast<int>(threadIdx.x)};
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
   const int64_t b = blockIdx.x;
-  t.load_static(tab, slots);
+  MTG_STAMP(0);
+  t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times + b * S, fixed_vals + b * D * nf, nf);
   __syncthreads();
-  for (int i = t.lane; i < S; i += kWave) t.T()[i] = times[b * S + i];
-  t.load_fixed(fixed_vals + b * D * nf, nf);
-  __syncthreads();
+  MTG_STAMP(1);
   t.compute_powers();
   __syncthreads();
+  MTG_STAMP(2);
   const int bad_time = t.flag()[0] & 1;
   if (!bad_time) t.solve();
   const int fl = t.flag()[0];
@@ -41,18 +40,18 @@ __global__ __launch_bounds__(kWave) void linear_solve_kernel(
     for (int i = t.lane; i < per; i += kWave) coeffs[b * per + i] = NAN;
     if (cost && t.lane == 0) cost[b] = NAN;
   } else {
-    const double J = t.coeffs_and_cost(coeffs + b * per);
+    const double J = t.template coeffs_and_cost<true>(pl.tab, coeffs + b * per);
     if (cost && t.lane == 0) cost[b] = J;
     if (free_vals) {
-      for (int i = t.lane; i < np * D; i += kWave) {
-        const int d = i / np;
-        const int p = i % np;
-        const int vk = free_map[p];
-        free_vals[b * D * np + i] = t.dv()[vk * D + d];
+      const int M = N / 2;
+      for (int i = t.lane; i < (S + 1) * M * D; i += kWave) {
+        const int sl = t.slot()[i / D];
+        if (sl < 0) free_vals[b * D * np + (i % D) * np + (-sl - 1)] = t.dv()[i];
       }
     }
   }
   if (status && t.lane == 0) status[b] = st;
+  MTG_STAMP(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -111,7 +110,8 @@ __global__ void segment_matrices_kernel(int N, int r, int64_t n,
 // Time-allocation objective J(T) = computeCost() + time_penalty (sum T)^2
 // (objectiveFunctionTime, nonlinear_impl:877-945) with optional gradient.
 template <int N>
-__device__ double objective_at(Traj<N>& t, double time_penalty) {
+__device__ double objective_at(Traj<N>& t, const double* __restrict__ tab,
+                               double time_penalty) {
   // Assumes T() holds the times; recomputes powers and re-solves.
   __syncthreads();
   t.compute_powers();
@@ -119,7 +119,7 @@ __device__ double objective_at(Traj<N>& t, double time_penalty) {
   t.clear_free();
   __syncthreads();
   t.solve();
-  const double J = t.cost();
+  const double J = t.cost(tab);
   double tot = 0.0;
   for (int i = 0; i < t.S; ++i) tot += t.T()[i];  // nonlinear_impl:2768-2774
   __syncthreads();
@@ -131,7 +131,8 @@ __device__ double objective_at(Traj<N>& t, double time_penalty) {
 // times; on exit T() is restored and dv holds the solution at the base times
 // only for grad_mode 1.  Gradient written to g (LDS, S entries).
 template <int N>
-__device__ void gradient_at(Traj<N>& t, const mtg_time_params& p, double* g) {
+__device__ void gradient_at(Traj<N>& t, const double* __restrict__ tab,
+                            const mtg_time_params& p, double* g) {
   const int S = t.S;
   const double inc = p.increment;
   if (p.grad_mode == 1) {
@@ -153,9 +154,9 @@ __device__ void gradient_at(Traj<N>& t, const mtg_time_params& p, double* g) {
     const double tb = Tn <= 0.1 ? 0.1 : Tn + inc;
     __syncthreads();
     if (t.lane == 0) t.T()[n] = ts;
-    const double Js = objective_at(t, p.time_penalty);
+    const double Js = objective_at(t, tab, p.time_penalty);
     if (t.lane == 0) t.T()[n] = tb;
-    const double Jb = objective_at(t, p.time_penalty);
+    const double Jb = objective_at(t, tab, p.time_penalty);
     if (t.lane == 0) {
       t.T()[n] = Tn;
       g[n] = (Jb - Js) / (2.0 * inc);
@@ -166,24 +167,21 @@ __device__ void gradient_at(Traj<N>& t, const mtg_time_params& p, double* g) {
 
 template <int N>
 __global__ __launch_bounds__(kWave) void time_cost_kernel(
-    int S, int D, int r, int nf, const double* __restrict__ tab,
-    const int* __restrict__ slots, const double* __restrict__ fixed_vals,
-    const double* __restrict__ times, mtg_time_params p,
-    double* __restrict__ cost, double* __restrict__ grad,
+    PlanDev pl, const double* __restrict__ fixed_vals, const double* __restrict__ times,
+    mtg_time_params p, double* __restrict__ cost, double* __restrict__ grad,
     int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf;
+  const double* tab = pl.tab;
   const Layout lay = make_layout(N, S, D);
-  Traj<N> t{S, D, r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
-            static_cast<int>(threadIdx.x)};
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
   const int64_t b = blockIdx.x;
-  t.load_static(tab, slots);
-  __syncthreads();
-  for (int i = t.lane; i < S; i += kWave) t.T()[i] = times[b * S + i];
-  t.load_fixed(fixed_vals + b * D * nf, nf);
-  const double J = objective_at(t, p.time_penalty);
+  t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times + b * S, fixed_vals + b * D * nf, nf);
+  const double J = objective_at(t, tab, p.time_penalty);
   const int fl = t.flag()[0];
   double* g = smem + lay.aux;
-  if (grad && p.grad_mode != 0 && !(fl & 1)) gradient_at(t, p, g);
+  if (grad && p.grad_mode != 0 && !(fl & 1)) gradient_at(t, tab, p, g);
   const int fl2 = t.flag()[0];
   if (t.lane == 0) {
     if (cost) cost[b] = (fl & 1) ? NAN : J;
@@ -202,35 +200,32 @@ __global__ __launch_bounds__(kWave) void time_cost_kernel(
 // evaluations (NLopt maxeval semantics, nonlinear_impl:101).
 template <int N>
 __global__ __launch_bounds__(kWave) void time_optimize_kernel(
-    int S, int D, int r, int nf, const double* __restrict__ tab,
-    const int* __restrict__ slots, const double* __restrict__ fixed_vals,
-    double* __restrict__ times_io, mtg_time_params p, int max_evals,
-    double* __restrict__ cost, int32_t* __restrict__ evals_out,
-    int32_t* __restrict__ status) {
+    PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ times_io,
+    mtg_time_params p, int max_evals, double* __restrict__ cost,
+    int32_t* __restrict__ evals_out, int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf;
+  const double* tab = pl.tab;
   const Layout lay = make_layout(N, S, D);
-  Traj<N> t{S, D, r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
-            static_cast<int>(threadIdx.x)};
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
   const int64_t b = blockIdx.x;
   double* Tcur = smem + lay.aux;   // accepted times
   double* T0 = Tcur + S;           // initial times (bounds)
   double* g = T0 + S;              // gradient at Tcur
-  t.load_static(tab, slots);
-  __syncthreads();
+  t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times_io + b * S, fixed_vals + b * D * nf, nf);
   for (int i = t.lane; i < S; i += kWave) {
     const double v = times_io[b * S + i];
-    t.T()[i] = v;
     Tcur[i] = v;
     T0[i] = v;
   }
-  t.load_fixed(fixed_vals + b * D * nf, nf);
   mtg_time_params pg = p;
   pg.grad_mode = 2;
-  double f = objective_at(t, p.time_penalty);
+  double f = objective_at(t, tab, p.time_penalty);
   int evals = 1;
   int fl = t.flag()[0];
   if (!(fl & 1)) {
-    gradient_at(t, pg, g);
+    gradient_at(t, tab, pg, g);
     double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
     constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
     while (evals < max_evals && alpha > 1e-9) {
@@ -249,7 +244,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
         if (t.lane == 0) t.T()[i] = tn;
       }
       if (!moved) break;
-      const double ft = objective_at(t, p.time_penalty);
+      const double ft = objective_at(t, tab, p.time_penalty);
       ++evals;
       if (ft < f) {
         f = ft;
@@ -257,7 +252,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
           for (int i = 0; i < S; ++i) Tcur[i] = t.T()[i];
         __syncthreads();
         alpha = fmin(alpha * 1.5, 1.0);
-        gradient_at(t, pg, g);
+        gradient_at(t, tab, pg, g);
       } else {
         alpha *= 0.5;
         if (t.lane == 0)
@@ -299,8 +294,7 @@ static hipError_t launch_linear_n(const PlanDev& pl, int64_t B, const double* df
   hipError_t e = prepare_lds(linear_solve_kernel<N>, bytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(linear_solve_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
-                     bytes, st, pl.S, pl.D, pl.r, pl.nf, pl.np, pl.tab, pl.slots,
-                     pl.free_map, df, times, coeffs, cost, free_vals, status);
+                     bytes, st, pl, df, times, coeffs, cost, free_vals, status);
   return hipGetLastError();
 }
 
@@ -313,8 +307,7 @@ static hipError_t launch_time_cost_n(const PlanDev& pl, int64_t B, const double*
   hipError_t e = prepare_lds(time_cost_kernel<N>, bytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(time_cost_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
-                     bytes, st, pl.S, pl.D, pl.r, pl.nf, pl.tab, pl.slots, df, times, p,
-                     cost, grad, status);
+                     bytes, st, pl, df, times, p, cost, grad, status);
   return hipGetLastError();
 }
 
@@ -327,8 +320,7 @@ static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* 
   hipError_t e = prepare_lds(time_optimize_kernel<N>, bytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(time_optimize_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
-                     bytes, st, pl.S, pl.D, pl.r, pl.nf, pl.tab, pl.slots, df, times, p,
-                     max_evals, cost, evals, status);
+                     bytes, st, pl, df, times, p, max_evals, cost, evals, status);
   return hipGetLastError();
 }
 
@@ -380,5 +372,12 @@ hipError_t launch_segment_matrices(int N, int r, int64_t n, const double* tab,
 }
 
 size_t linear_lds_bytes(int N, int S, int D) { return make_layout(N, S, D).bytes(); }
+
+#ifdef MTG_STAMPS
+extern "C" int mtg_debug_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mtg_stamps), sizeof(unsigned long long) * n) ==
+                 hipSuccess ? 0 : -3;
+}
+#endif
 
 }  // namespace mtg
