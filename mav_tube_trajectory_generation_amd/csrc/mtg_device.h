@@ -149,24 +149,41 @@ struct Traj {
   }
 
   // All global inputs of one trajectory in a single round of independent
-  // loads: tables, slots, times, and d_f scattered into dv (fixed_map gives
-  // the (vertex, derivative) slot of fixed index f).
+  // loads (first pass of every array issued before any LDS store): tables,
+  // slots, times, and d_f scattered into dv (fixed_map gives the (vertex,
+  // derivative) slot of fixed index f).
   __device__ void load_inputs(const double* __restrict__ tab, const int* __restrict__ slots,
                               const int* __restrict__ fixed_map,
                               const double* __restrict__ times_b,
                               const double* __restrict__ df, int nf) {
-    for (int i = lane; i < 2 * N * N; i += kWave) sm[lay->tabH + i] = tab[i];
-    for (int i = lane; i < (S + 1) * M; i += kWave) slot()[i] = slots[i];
-    for (int i = lane; i < S; i += kWave) T()[i] = times_b[i];
-    // Free entries are zero; fixed ones take d_f (disjoint writes).
-    for (int i = lane; i < (S + 1) * M * D; i += kWave) {
-      const int vk = i / D;
-      if (slots[vk] < 0) dv()[i] = 0.0;
+    constexpr int NT = (2 * N * N + kWave - 1) / kWave;
+    const int nslot = (S + 1) * M, ndf = D * nf;
+    double rt[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int i = lane + q * kWave;
+      rt[q] = i < 2 * N * N ? tab[i] : 0.0;
     }
-    for (int i = lane; i < D * nf; i += kWave) {
-      const int d = i / nf, f = i % nf;
-      dv()[fixed_map[f] * D + d] = df[i];
+    const int rs = lane < nslot ? slots[lane] : 0;
+    const double rtime = lane < S ? times_b[lane] : 0.0;
+    const double rdf = lane < ndf ? df[lane] : 0.0;
+    const int rfm = lane < ndf ? fixed_map[lane % nf] : 0;
+    // dv: zero everything, then scatter the fixed values (same wave, LDS
+    // stores retire in order).
+    for (int i = lane; i < (S + 1) * M * D; i += kWave) dv()[i] = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int i = lane + q * kWave;
+      if (i < 2 * N * N) sm[lay->tabH + i] = rt[q];
     }
+    if (lane < nslot) slot()[lane] = rs;
+    if (lane < S) T()[lane] = rtime;
+    if (lane < ndf) dv()[rfm * D + lane / nf] = rdf;
+    // Remainders for large S (never taken at the benchmark sizes).
+    for (int i = lane + kWave; i < nslot; i += kWave) slot()[i] = slots[i];
+    for (int i = lane + kWave; i < S; i += kWave) T()[i] = times_b[i];
+    for (int i = lane + kWave; i < ndf; i += kWave)
+      dv()[fixed_map[i % nf] * D + i / nf] = df[i];
     if (lane == 0) flag()[0] = 0;
   }
 
@@ -207,6 +224,7 @@ struct Traj {
     double* Dt = sm + lay->Dt;
     double* Ot = sm + lay->Ot;
     double* Bt = sm + lay->Bt;
+#pragma unroll 2
     for (int i = lane; i < (S + 1) * M * M; i += kWave) {
       const int v = i / (M * M);
       const int j = (i / M) % M, k = i % M;
@@ -220,6 +238,7 @@ struct Traj {
     }
     __syncthreads();
     // dv is zero at free entries, so these sums run over fixed columns only.
+#pragma unroll 2
     for (int i = lane; i < (S + 1) * M * D; i += kWave) {
       const int v = i / (M * D);
       const int j = (i / D) % M, d = i % D;
@@ -391,45 +410,47 @@ struct Traj {
     return x;
   }
 
-  // One lane per (segment, dimension) with e = [x_s; x_{s+1}] in registers:
+  // Lanes over (segment, dimension, half) with e = [x_s; x_{s+1}] in
+  // registers; half h covers coefficients / rows k in [hM, hM + M):
   //   c_s[d][k] = sum_j A(1)^-1[k][j] T_s^(j mod M - k) e_j   (coefficients,
   //               linear_impl:254-275; written to `out` when kCoeffs)
-  //   cost     += e^T H_s e                                   (computeCost,
+  //   cost     += e_k (H_s e)_k                               (computeCost,
   //               linear_impl:113-130: 0.5 c^T Q c == 0.5 e^T H e)
-  // Table entries have compile-time indices and are read from global memory
-  // (`tab`, wave-uniform -> scalar loads).  Returns computeCost() on every
-  // lane.
+  // Returns computeCost() on every lane.
   template <bool kCoeffs>
   __device__ double coeffs_and_cost(const double* __restrict__ tab,
                                     double* __restrict__ out) const {
+    (void)tab;
     double acc = 0.0;
-    for (int sd = lane; sd < S * D; sd += kWave) {
+    for (int item = lane; item < 2 * S * D; item += kWave) {
+      const int h = item & 1;
+      const int sd = item >> 1;
       const int s = sd / D, d = sd % D;
       double e[N];
 #pragma unroll
       for (int j = 0; j < N; ++j) e[j] = dval(s + j / M, j % M, d);
-      double ph[2 * M - 1];  // T^(1-2r+q), q = 0..2M-2
-#pragma unroll
-      for (int q = 0; q < 2 * M - 1; ++q) ph[q] = pwr(s, 1 - 2 * r + q);
+      const double* tH = tabH() + h * M * N;
+      const double* ph = pw() + s * PWN + (N - 1) + 1 - 2 * r;  // T^(1-2r+q)
       double cs = 0.0;
+      // Rolled over rows (N table values live per row, not N*M).
+#pragma unroll 1
+      for (int kk = 0; kk < M; ++kk) {
+        double hk = 0.0;
 #pragma unroll
-      for (int k = 0; k < N; ++k) {
-        double h = 0.0;
-#pragma unroll
-        for (int j = 0; j < N; ++j) h += tab[k * N + j] * ph[(k % M) + (j % M)] * e[j];
-        cs += h * e[k];
+        for (int j = 0; j < N; ++j) hk += tH[kk * N + j] * ph[kk + (j % M)] * e[j];
+        cs += hk * dval(s + h, kk, d);
       }
       acc += cs;
       if (kCoeffs) {
-        double pa[PWN];  // T^(q - (N-1))
-#pragma unroll
-        for (int q = 0; q < PWN; ++q) pa[q] = pw()[s * PWN + q];
-#pragma unroll
-        for (int k = 0; k < N; ++k) {
+        // T^(l - k) for l in [0, M), k = hM + kk.
+        const double* tA = tabA() + h * M * N;
+        const double* pws = pw() + s * PWN + (N - 1) - h * M;
+#pragma unroll 1
+        for (int kk = 0; kk < M; ++kk) {
           double c = 0.0;
 #pragma unroll
-          for (int j = 0; j < N; ++j) c += tab[N * N + k * N + j] * pa[(j % M) - k + N - 1] * e[j];
-          out[sd * N + k] = c;
+          for (int j = 0; j < N; ++j) c += tA[kk * N + j] * pws[(j % M) - kk] * e[j];
+          out[sd * N + h * M + kk] = c;
         }
       }
     }
