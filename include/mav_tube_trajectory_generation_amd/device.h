@@ -1,0 +1,93 @@
+// device.h — process-wide HIP device context and small device-buffer helper
+// for the C++ host API.  All compute goes through the C ABI of
+// libmtg_hip.so (include/mtg_hip.h); this header only owns the context and
+// moves host arrays to/from HBM.  There is no CPU fallback: without a HIP
+// device every solve fails its MTG_CHECK (the reference aborts likewise on
+// contract violations).
+#ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_DEVICE_H_
+#define MAV_TUBE_TRAJECTORY_GENERATION_AMD_DEVICE_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdlib>
+#include <mutex>
+#include <vector>
+
+#include "mav_tube_trajectory_generation_amd/check.h"
+#include "mtg_hip.h"
+
+namespace mav_trajectory_generation {
+namespace internal {
+
+// Device of the process-wide context: $MTG_DEVICE or 0.
+inline mtg_ctx* defaultContext() {
+  static std::once_flag once;
+  static mtg_ctx* ctx = nullptr;
+  static int rc = MTG_OK;
+  std::call_once(once, [] {
+    const char* env = std::getenv("MTG_DEVICE");
+    rc = mtg_ctx_create(env ? std::atoi(env) : 0, &ctx);
+  });
+  MTG_CHECK(rc == MTG_OK && ctx != nullptr,
+            "libmtg_hip: no usable HIP device (" << mtg_status_string(rc) << ")");
+  return ctx;
+}
+
+inline void checkStatus(int rc, const char* what) {
+  MTG_CHECK(rc == MTG_OK, what << " failed: " << mtg_status_string(rc));
+}
+
+// Owning HBM buffer of T.
+template <typename T>
+class DeviceBuffer {
+ public:
+  DeviceBuffer() {}
+  explicit DeviceBuffer(size_t n) { resize(n); }
+  ~DeviceBuffer() { release(); }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+
+  void resize(size_t n) {
+    if (n == n_) return;
+    release();
+    n_ = n;
+    if (n) MTG_CHECK(hipMalloc(&p_, n * sizeof(T)) == hipSuccess, "hipMalloc failed");
+  }
+  void upload(const T* src, size_t n) {
+    resize(n);
+    if (n)
+      MTG_CHECK(hipMemcpy(p_, src, n * sizeof(T), hipMemcpyHostToDevice) == hipSuccess,
+                "hipMemcpy H2D failed");
+  }
+  void upload(const std::vector<T>& v) { upload(v.data(), v.size()); }
+  void download(T* dst, size_t n) const {
+    if (n)
+      MTG_CHECK(hipMemcpy(dst, p_, n * sizeof(T), hipMemcpyDeviceToHost) == hipSuccess,
+                "hipMemcpy D2H failed");
+  }
+  std::vector<T> download() const {
+    std::vector<T> v(n_);
+    download(v.data(), n_);
+    return v;
+  }
+  T* get() const { return p_; }
+  size_t size() const { return n_; }
+
+ private:
+  void release() {
+    if (p_) (void)hipFree(p_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+  T* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+inline void synchronize() {
+  MTG_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize failed");
+}
+
+}  // namespace internal
+}  // namespace mav_trajectory_generation
+
+#endif  // MAV_TUBE_TRAJECTORY_GENERATION_AMD_DEVICE_H_

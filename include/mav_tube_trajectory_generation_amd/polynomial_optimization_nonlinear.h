@@ -1,0 +1,273 @@
+// polynomial_optimization_nonlinear.h — PolynomialOptimizationNonLinear<N>,
+// the segment-time optimisation of the reference
+// (include/mav_tube_trajectory_generation/polynomial_optimization_nonlinear.h:
+// 46-674, impl/polynomial_optimization_nonlinear_impl.h "nonlinear_impl"),
+// restricted to the objective on the hot path:
+// kOptimizeTime with the time-only cost callback
+//   J(T) = computeCost() + time_penalty * (sum_i T_i)^2
+// (objectiveFunctionTime, nonlinear_impl:877-945, w_c = 0, no soft
+// constraints).  Both the callback (evaluateTimeCost -> mtg_time_cost) and
+// the whole optimisation loop (optimize -> mtg_time_optimize) run on the
+// device.
+//
+// Semantics and deliberate differences:
+//   * inner solve = the linear solve with the vertices' own constraint
+//     pattern (upstream mav_trajectory_generation semantics).  The fork calls
+//     solveQCQP inside the callback (nonlinear_impl:892); that mode is not
+//     provided yet — solveQCQP() is available on its own;
+//   * NLopt (LN_SBPLX, nonlinear_impl:95-107) is absent; the optimiser is the
+//     device-side projected descent of mtg_time_optimize with the same
+//     bounds [0.1, 2 T0] (:350-378), initial relative step 0.1 (the
+//     initial_stepsize_rel default) and evaluation budget max_iterations
+//     (NLopt maxeval, :101).  Optimiser trajectories therefore differ from NLopt's
+//     (parity unpinned); the callback value is pinned;
+//   * the collision cost (w_c > 0) needs the supereight octree (out of scope,
+//     SURVEY.md §8f rank 4; the reference dereferences a null octree there,
+//     §8a T6): it is ignored with a warning;
+//   * addMaximumMagnitudeConstraint / soft constraints need the extremum
+//     search (§8f rank 1) and return false.
+#ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
+#define MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
+
+#include <chrono>
+#include <ostream>
+#include <utility>
+#include <vector>
+
+#include "mav_tube_trajectory_generation_amd/polynomial_optimization_qcqp.h"
+
+namespace mav_trajectory_generation {
+
+// polynomial_optimization_nonlinear.h:46-210 (fields kept for source
+// compatibility; the ones this build reads are marked).
+struct NonlinearOptimizationParameters {
+  enum OptimizationObjective {
+    kOptimizeFreeConstraints,
+    kOptimizeFreeConstraintsAndTime,
+    kOptimizeTime,
+    kOptimizeFreeConstraintsAndCollision,
+    kOptimizeFreeConstraintsAndCollisionAndTime,
+    kUnknown
+  };
+  struct cost_weights {
+    cost_weights() : w_d(0.1), w_c(10.0), w_t(1.0), w_sc(1.0) {}
+    double w_d;  // read (gradient mode 1)
+    double w_c;
+    double w_t;  // read (gradient mode 1)
+    double w_sc;
+  };
+
+  double f_abs = -1;
+  double f_rel = 0.05;
+  double x_rel = -1;
+  double x_abs = -1;
+  double initial_stepsize_position = 0.05;
+  double initial_stepsize_rel = 0.1;  // the device optimiser uses the default 0.1
+  double equality_constraint_tolerance = 1.0e-3;
+  double inequality_constraint_tolerance = 0.1;
+  int max_iterations = 5;  // read: objective-evaluation budget
+  double max_time = -1;
+  double time_penalty = 500.0;  // read
+  int random_seed = 0;
+  bool use_soft_constraints = true;
+  double soft_constraint_weight = 100.0;
+  bool print_debug_info = false;
+  OptimizationObjective objective = kOptimizeFreeConstraintsAndTime;  // read
+  cost_weights weights;
+  double map_resolution = 0.0;
+  int side = 5;
+  bool use_numeric_grad = false;
+  bool use_continous_distance = false;
+  double increment_time = 0.1;  // read (gradient step)
+  double epsilon = 0.5;
+  double robot_radius = 0.5;
+  double coll_pot_multiplier = 1.0;
+  bool solve_with_position_constraint = false;
+  bool is_collision_safe = true;
+  bool is_simple_numgrad_time = false;
+  bool is_simple_numgrad_constraints = false;
+  double coll_check_time_increment = 0.1;
+  bool is_coll_raise_first_iter = true;
+  double add_coll_raise = 0.0;
+};
+
+// polynomial_optimization_nonlinear.h:212-236.
+class OptimizationInfo {
+ public:
+  void print(std::ostream& stream) const {
+    stream << "--- optimization info ---" << std::endl;
+    stream << "  optimization time:     " << optimization_time << std::endl;
+    stream << "  n_iterations:          " << n_iterations << std::endl;
+    stream << "  stopping reason:       " << stopping_reason << std::endl;
+    stream << "  cost trajectory:       " << cost_trajectory << std::endl;
+    stream << "  cost time:             " << cost_time << std::endl;
+    stream << "  cost collision:        " << cost_collision << std::endl;
+    stream << "  cost soft constraints: " << cost_soft_constraints << std::endl;
+  }
+  int n_iterations = 0;
+  int stopping_reason = -1;  // nlopt::FAILURE
+  double cost_trajectory = 0;
+  double cost_collision = 0;
+  double cost_time = 0;
+  double cost_soft_constraints = 0;
+  double optimization_time = 0;
+};
+
+template <int _N = 10>
+class PolynomialOptimizationNonLinear {
+  static_assert(_N % 2 == 0, "The number of coefficients has to be even.");
+
+ public:
+  enum { N = _N };
+
+  PolynomialOptimizationNonLinear(size_t dimension,
+                                  const NonlinearOptimizationParameters& parameters)
+      : dimension_(dimension), params_(parameters), poly_opt_(dimension), linear_(dimension) {}
+
+  // nonlinear_impl:57-110.
+  bool setupFromVertices(const Vertex::Vector& vertices,
+                         const std::vector<double>& segment_times,
+                         const std::vector<std::pair<double, double>>& radii,
+                         int derivative_to_optimize =
+                             PolynomialOptimization<N>::kHighestDerivativeToOptimize) {
+    vertices_ = vertices;
+    bool ret = poly_opt_.setupFromVertices(vertices, segment_times, radii,
+                                           derivative_to_optimize);
+    ret = linear_.setupFromVertices(vertices, segment_times, derivative_to_optimize) && ret;
+    return ret;
+  }
+
+  bool addMaximumMagnitudeConstraint(int /*derivative_order*/, double /*maximum_value*/) {
+    internal::warn(
+        "addMaximumMagnitudeConstraint: the extremum search is not part of this build "
+        "(SURVEY.md 8f rank 1); constraint ignored");
+    return false;
+  }
+
+  int solveQCQP() { return poly_opt_.solveQCQP(); }
+  bool solveLinear() { return linear_.solveLinear(); }
+
+  // Time-only objective at `segment_times` (objectiveFunctionTime with the
+  // linear inner solve).  grad_mode: 0 none, 1 getCostAndGradientTime
+  // (nonlinear_impl:2495-2584), 2 central differences of J.  `gradient` is
+  // resized to S when grad_mode != 0.
+  double evaluateTimeCost(const std::vector<double>& segment_times, int grad_mode = 0,
+                          std::vector<double>* gradient = nullptr) {
+    const size_t S = linear_.getNumberSegments();
+    MTG_CHECK(segment_times.size() == S, "segment_times has " << segment_times.size()
+                                                              << " entries, need " << S);
+    MTG_CHECK(grad_mode == 0 || gradient != nullptr, "gradient must not be null");
+    warnCollision();
+    internal::DeviceBuffer<double> d_df, d_t, d_cost(1), d_g(S);
+    d_df.upload(packFixed());
+    d_t.upload(segment_times);
+    const mtg_time_params p = timeParams(grad_mode);
+    internal::checkStatus(mtg_time_cost(planOf(), 1, d_df.get(), d_t.get(), &p, d_cost.get(),
+                                        grad_mode ? d_g.get() : nullptr, nullptr, nullptr),
+                          "mtg_time_cost");
+    internal::synchronize();
+    double J = 0.0;
+    d_cost.download(&J, 1);
+    if (grad_mode) *gradient = d_g.download();
+    return J;
+  }
+
+  // Runs the optimisation (objective kOptimizeTime only).  Returns a
+  // positive NLopt-style success code (1) or a negative failure code.
+  int optimize() {
+    MTG_CHECK(params_.objective == NonlinearOptimizationParameters::kOptimizeTime,
+              "only kOptimizeTime is part of this build (SURVEY.md 8a T1-T6)");
+    warnCollision();
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> times;
+    linear_.getSegmentTimes(&times);
+    linear_.solveLinear();  // initial solution (nonlinear_impl:341-349)
+    linear_.getTrajectory(&trajectory_initial_);
+    const size_t S = times.size();
+    internal::DeviceBuffer<double> d_df, d_t, d_cost(1);
+    internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
+    d_df.upload(packFixed());
+    d_t.upload(times);
+    const mtg_time_params p = timeParams(0);
+    const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
+    internal::checkStatus(mtg_time_optimize(planOf(), 1, d_df.get(), d_t.get(), &p, budget,
+                                            d_cost.get(), d_ev.get(), d_st.get(), nullptr),
+                          "mtg_time_optimize");
+    internal::synchronize();
+    d_t.download(times.data(), S);
+    int32_t evals = 0, st = 0;
+    d_ev.download(&evals, 1);
+    d_st.download(&st, 1);
+    linear_.updateSegmentTimes(times);
+    linear_.solveLinear();
+    double tot = 0.0;
+    for (double t : times) tot += t;
+    optimization_info_.n_iterations = evals;
+    optimization_info_.cost_trajectory = linear_.computeCost();
+    optimization_info_.cost_time = tot * tot * params_.time_penalty;
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
+    optimization_info_.optimization_time =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return optimization_info_.stopping_reason;
+  }
+
+  void getTrajectory(Trajectory* trajectory) const { linear_.getTrajectory(trajectory); }
+  void getQCQPTrajectory(Trajectory* trajectory) const { poly_opt_.getTrajectory(trajectory); }
+  void getInitialSolutionTrajectory(Trajectory* trajectory) const {
+    MTG_CHECK(trajectory != nullptr, "trajectory must not be null");
+    MTG_CHECK(!trajectory_initial_.empty(), "optimize() has not run");
+    *trajectory = trajectory_initial_;
+  }
+  void getFreeConstraints(std::vector<VectorXd>* free_constraints) const {
+    linear_.getFreeConstraints(free_constraints);
+  }
+  const PolynomialOptimization<N>& getPolynomialOptimizationRef() const { return linear_; }
+  PolynomialOptimization<N>& getPolynomialOptimizationRef() { return linear_; }
+  const PolynomialOptimizationConstrained<N>& getConstrainedOptimizationRef() const {
+    return poly_opt_;
+  }
+  OptimizationInfo getOptimizationInfo() const { return optimization_info_; }
+
+  // nonlinear_impl:2768-2774.
+  static double computeTotalTrajectoryTime(const std::vector<double>& segment_times) {
+    double t = 0.0;
+    for (double s : segment_times) t += s;
+    return t;
+  }
+
+ private:
+  mtg_time_params timeParams(int grad_mode) const {
+    mtg_time_params p;
+    p.time_penalty = params_.time_penalty;
+    p.increment = params_.increment_time;
+    p.w_d = params_.weights.w_d;
+    p.w_t = params_.weights.w_t;
+    p.grad_mode = grad_mode;
+    return p;
+  }
+  void warnCollision() const {
+    if (params_.weights.w_c > 0.0)
+      internal::warn("collision cost (w_c > 0) is out of scope here and ignored");
+  }
+  std::vector<double> packFixed() const {
+    std::vector<VectorXd> df;
+    linear_.getFixedConstraints(&df);
+    std::vector<double> out;
+    for (const VectorXd& v : df)
+      for (long i = 0; i < v.size(); ++i) out.push_back(v[i]);
+    return out;
+  }
+  const mtg_plan* planOf() const { return linear_.getPlan(); }
+
+  size_t dimension_;
+  NonlinearOptimizationParameters params_;
+  PolynomialOptimizationConstrained<N> poly_opt_;
+  PolynomialOptimization<N> linear_;
+  Vertex::Vector vertices_;
+  Trajectory trajectory_initial_;
+  OptimizationInfo optimization_info_;
+};
+
+}  // namespace mav_trajectory_generation
+
+#endif  // MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_

@@ -118,6 +118,17 @@ int mtg_linear_solve_host(const mtg_plan* plan, int64_t B,
                           double* coeffs, double* cost, double* free_vals,
                           int32_t* status);
 
+/* Coefficients and cost from given fixed AND free derivatives (no solve):
+ * setFreeConstraints -> updateSegmentsFromCompactConstraints
+ * (linear_impl:254-275, 497-506) followed by computeCost (:113-130).
+ * Inputs (device): fixed_vals B x D x n_fixed, free_vals B x D x n_free,
+ * times B x S.  Outputs (device): coeffs B x S x D x N; cost B and status B
+ * nullable. */
+int mtg_coeffs_from_constraints(const mtg_plan* plan, int64_t B,
+                                const double* fixed_vals, const double* free_vals,
+                                const double* times, double* coeffs, double* cost,
+                                int32_t* status, void* stream);
+
 /* Per-segment matrices for a batch of n segment times (device), each N x N:
  * Q(T) = computeQuadraticCostJacobian (linear_impl:557-573),
  * A(T) = setupMappingMatrix (linear_impl:101-111),

@@ -39,6 +39,8 @@ SIGNATURES = {
     "mtg_linear_solve": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mtg_linear_solve_host": (ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, _dp, _dp,
                                              _i32p]),
+    "mtg_coeffs_from_constraints": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp,
+                                                   _vp, _vp, _vp]),
     "mtg_segment_matrices": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                             _vp, _vp, _vp, _vp, _vp, _vp]),
     "mtg_time_cost": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.POINTER(TimeParams),

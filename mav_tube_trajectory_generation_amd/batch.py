@@ -113,6 +113,25 @@ class LinearPlan:
                                      _ptr(o.get("status")), _stream(dev)), "mtg_linear_solve")
         return o
 
+    def coefficients(self, fixed_vals, free_vals, times):
+        """Coefficients and cost from given d_f and d_p, no solve
+        (setFreeConstraints, linear_impl:497-506).  Returns (coeffs, cost,
+        status)."""
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        _require(free_vals, (B, self.D, self.n_free), "free_vals")
+        dev = times.device
+        coeffs = torch.empty((B, self.S, self.D, self.N), dtype=torch.float64, device=dev)
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        check(lib().mtg_coeffs_from_constraints(self._h, B, _ptr(fixed_vals), _ptr(free_vals),
+                                                _ptr(times), _ptr(coeffs), _ptr(cost),
+                                                _ptr(status), _stream(dev)),
+              "mtg_coeffs_from_constraints")
+        return coeffs, cost, status
+
     def time_cost(self, fixed_vals, times, time_penalty=500.0, grad_mode=0, increment=0.1,
                   w_d=0.1, w_t=1.0):
         import torch

@@ -319,6 +319,18 @@ int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_v
   return MTG_OK;
 }
 
+int mtg_coeffs_from_constraints(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                                const double* free_vals, const double* times, double* coeffs,
+                                double* cost, int32_t* status, void* stream) {
+  if (!plan || B < 0 || B > 0x7fffffff || !times || !coeffs) return MTG_ERR_INVALID_ARG;
+  if ((plan->dev.nf > 0 && !fixed_vals) || (plan->dev.np > 0 && !free_vals))
+    return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return from_hip(mtg::launch_coeffs_from_constraints(plan->dev, B, fixed_vals, free_vals,
+                                                      times, coeffs, cost, status,
+                                                      static_cast<hipStream_t>(stream)));
+}
+
 int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* times,
                          double* Q, double* A, double* Ainv, double* H, void* stream) {
   if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || n < 0 || (n && !times))

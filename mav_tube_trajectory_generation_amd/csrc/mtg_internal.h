@@ -26,6 +26,10 @@ struct PlanDev {
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,
                                double* free_vals, int32_t* status, hipStream_t st);
+hipError_t launch_coeffs_from_constraints(const PlanDev& pl, int64_t B, const double* df,
+                                          const double* dp, const double* times,
+                                          double* coeffs, double* cost, int32_t* status,
+                                          hipStream_t st);
 hipError_t launch_time_cost(const PlanDev& pl, int64_t B, const double* df,
                             const double* times, const mtg_time_params& p,
                             double* cost, double* grad, int32_t* status,

@@ -55,6 +55,39 @@ __global__ __launch_bounds__(kWave) void linear_solve_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Coefficients and cost from given fixed and free derivatives, no solve
+// (setFreeConstraints -> updateSegmentsFromCompactConstraints, linear_impl:
+// 254-275, 497-506, and computeCost, :113-130).
+template <int N>
+__global__ __launch_bounds__(kWave) void coeffs_from_constraints_kernel(
+    PlanDev pl, const double* __restrict__ fixed_vals, const double* __restrict__ free_vals,
+    const double* __restrict__ times, double* __restrict__ coeffs, double* __restrict__ cost,
+    int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf, np = pl.np;
+  const Layout lay = make_layout(N, S, D);
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
+  const int64_t b = blockIdx.x;
+  t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times + b * S, fixed_vals + b * D * nf, nf);
+  for (int i = t.lane; i < D * np; i += kWave)
+    t.dv()[pl.free_map[i % np] * D + i / np] = free_vals[b * D * np + i];
+  __syncthreads();
+  t.compute_powers();
+  __syncthreads();
+  const int bad_time = t.flag()[0] & 1;
+  const int64_t per = static_cast<int64_t>(S) * D * N;
+  if (bad_time) {
+    for (int i = t.lane; i < per; i += kWave) coeffs[b * per + i] = NAN;
+    if (cost && t.lane == 0) cost[b] = NAN;
+  } else {
+    const double J = t.template coeffs_and_cost<true>(pl.tab, coeffs + b * per);
+    if (cost && t.lane == 0) cost[b] = J;
+  }
+  if (status && t.lane == 0) status[b] = bad_time ? MTG_TRAJ_BAD_TIME : MTG_TRAJ_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Per-segment matrices Q, A, A^-1, H for a batch of times (accessor parity:
 // linear_impl:101-111, 132-169, 557-573, 318).  One thread per entry.
 __device__ inline double falling(int n, int i) {  // base(n, i) = i!/(i-n)!
@@ -299,6 +332,18 @@ static hipError_t launch_linear_n(const PlanDev& pl, int64_t B, const double* df
 }
 
 template <int N>
+static hipError_t launch_coeffs_n(const PlanDev& pl, int64_t B, const double* df,
+                                  const double* dp, const double* times, double* coeffs,
+                                  double* cost, int32_t* status, hipStream_t st) {
+  const size_t bytes = make_layout(N, pl.S, pl.D).bytes();
+  hipError_t e = prepare_lds(coeffs_from_constraints_kernel<N>, bytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(coeffs_from_constraints_kernel<N>, dim3(static_cast<unsigned>(B)),
+                     dim3(kWave), bytes, st, pl, df, dp, times, coeffs, cost, status);
+  return hipGetLastError();
+}
+
+template <int N>
 static hipError_t launch_time_cost_n(const PlanDev& pl, int64_t B, const double* df,
                                      const double* times, const mtg_time_params& p,
                                      double* cost, double* grad, int32_t* status,
@@ -338,6 +383,15 @@ hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,
                                double* free_vals, int32_t* status, hipStream_t st) {
 #define CALL(n) launch_linear_n<n>(pl, B, df, times, coeffs, cost, free_vals, status, st)
+  MTG_DISPATCH_N(pl.N, CALL)
+#undef CALL
+}
+
+hipError_t launch_coeffs_from_constraints(const PlanDev& pl, int64_t B, const double* df,
+                                          const double* dp, const double* times,
+                                          double* coeffs, double* cost, int32_t* status,
+                                          hipStream_t st) {
+#define CALL(n) launch_coeffs_n<n>(pl, B, df, dp, times, coeffs, cost, status, st)
   MTG_DISPATCH_N(pl.N, CALL)
 #undef CALL
 }

@@ -1,0 +1,576 @@
+// C++ API tests: the reference's own test strategy
+// (test/test_polynomial_optimization.cpp) run against the
+// MI355X shims in include/mav_tube_trajectory_generation_amd/.  The checker
+// is the oracle (oracle/mtg_oracle.h, liboracle.so): test infrastructure,
+// never the thing under test.
+//
+//   test_polynomial_optimization host   -> tests that need no GPU (static
+//        host utilities, generators, and that the solve path fails loudly
+//        without a device)
+//   test_polynomial_optimization gpu    -> the parity tests proper
+#define MTG_CHECK_THROWS 1
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "mav_tube_trajectory_generation_amd/polynomial_optimization_nonlinear.h"
+#include "mtg_oracle.h"
+
+using namespace mav_trajectory_generation;
+
+namespace {
+
+int g_failures = 0;
+int g_checks = 0;
+
+#define EXPECT_TRUE(cond)                                                            \
+  do {                                                                               \
+    ++g_checks;                                                                      \
+    if (!(cond)) {                                                                   \
+      ++g_failures;                                                                  \
+      std::fprintf(stderr, "  FAILED %s:%d: %s\n", __FILE__, __LINE__, #cond);       \
+    }                                                                                \
+  } while (0)
+
+#define EXPECT_LE(a, b)                                                              \
+  do {                                                                               \
+    ++g_checks;                                                                      \
+    const double va_ = (a), vb_ = (b);                                               \
+    if (!(va_ <= vb_)) {                                                             \
+      ++g_failures;                                                                  \
+      std::fprintf(stderr, "  FAILED %s:%d: %s = %.6g > %s = %.6g\n", __FILE__,     \
+                   __LINE__, #a, va_, #b, vb_);                                      \
+    }                                                                                \
+  } while (0)
+
+#define EXPECT_THROW(stmt)                                                           \
+  do {                                                                               \
+    ++g_checks;                                                                      \
+    bool thrown_ = false;                                                            \
+    try {                                                                            \
+      stmt;                                                                          \
+    } catch (const std::logic_error&) {                                              \
+      thrown_ = true;                                                                \
+    }                                                                                \
+    if (!thrown_) {                                                                  \
+      ++g_failures;                                                                  \
+      std::fprintf(stderr, "  FAILED %s:%d: %s did not throw\n", __FILE__, __LINE__, \
+                   #stmt);                                                           \
+    }                                                                                \
+  } while (0)
+
+struct TestCase {
+  const char* group;
+  const char* name;
+  std::function<void()> fn;
+};
+std::vector<TestCase>& registry() {
+  static std::vector<TestCase> r;
+  return r;
+}
+struct Register {
+  Register(const char* g, const char* n, std::function<void()> f) {
+    registry().push_back({g, n, f});
+  }
+};
+#define TEST(group, name)                                             \
+  static void test_##group##_##name();                                \
+  static Register reg_##group##_##name(#group, #name, test_##group##_##name); \
+  static void test_##group##_##name()
+
+// Normwise relative difference ||a - b|| / max(||b||, 1e-300).
+double relErr(const std::vector<double>& a, const std::vector<double>& b) {
+  double num = 0.0, den = 0.0;
+  for (size_t i = 0; i < a.size(); ++i) {
+    num += (a[i] - b[i]) * (a[i] - b[i]);
+    den += b[i] * b[i];
+  }
+  return std::sqrt(num) / std::max(std::sqrt(den), 1e-300);
+}
+double relErr(double a, double b) { return std::fabs(a - b) / std::max(std::fabs(b), 1e-300); }
+
+// Dense oracle vertex form (mask[v*K+k], vals[(v*K+k)*D+d]).
+struct Dense {
+  int S, D, K;
+  std::vector<uint8_t> mask;
+  std::vector<double> vals;
+};
+Dense toDense(const Vertex::Vector& vs, int K) {
+  Dense o{static_cast<int>(vs.size()) - 1, vs.front().D(), K, {}, {}};
+  o.mask.assign(vs.size() * K, 0);
+  o.vals.assign(vs.size() * K * o.D, 0.0);
+  for (size_t v = 0; v < vs.size(); ++v)
+    for (int k = 0; k < K; ++k) {
+      VectorXd val;
+      if (vs[v].getConstraint(k, &val)) {
+        o.mask[v * K + k] = 1;
+        for (int d = 0; d < o.D; ++d) o.vals[(v * K + k) * o.D + d] = val[d];
+      }
+    }
+  return o;
+}
+
+std::vector<double> coeffsOf(const Segment::Vector& segs, int N) {
+  std::vector<double> c;
+  for (const Segment& s : segs)
+    for (int d = 0; d < s.D(); ++d) {
+      const VectorXd v = s[d].getCoefficients();
+      for (int k = 0; k < N; ++k) c.push_back(v[k]);
+    }
+  return c;
+}
+
+// checkPath (test_polynomial_optimization.cpp:113-172).
+void checkPath(const Vertex::Vector& vs, const Segment::Vector& segs, int N) {
+  const int M = N / 2;
+  for (size_t s = 0; s < segs.size(); ++s) {
+    for (int end = 0; end < 2; ++end) {
+      const Vertex& v = vs[s + end];
+      const double t = end ? segs[s].getTime() : 0.0;
+      for (int k = 0; k < M; ++k) {
+        VectorXd want;
+        if (!v.getConstraint(k, &want)) continue;
+        const VectorXd got = segs[s].evaluate(t, k);
+        for (long d = 0; d < want.size(); ++d)
+          EXPECT_LE(std::fabs(got[d] - want[d]), 1e-6 * std::max(1.0, std::fabs(want[d])));
+      }
+    }
+    if (s > 0)
+      for (int k = 0; k < M; ++k) {
+        const VectorXd a = segs[s - 1].evaluate(segs[s - 1].getTime(), k);
+        const VectorXd b = segs[s].evaluate(0.0, k);
+        for (long d = 0; d < a.size(); ++d)
+          EXPECT_LE(std::fabs(a[d] - b[d]), 1e-6 * std::max(1.0, std::fabs(a[d])));
+      }
+  }
+}
+
+// computeCostNumeric (test_utils.h:56-64) vs computeCost, 10 % (checkCost,
+// test_polynomial_optimization.cpp:174-195).
+void checkCost(const Segment::Vector& segs, int r, double cost) {
+  double num = 0.0;
+  const double dt = 1e-3;
+  for (const Segment& s : segs)
+    for (double t = 0.0; t < s.getTime(); t += dt) {
+      const VectorXd v = s.evaluate(t, r);
+      num += v.squaredNorm() * dt;
+    }
+  EXPECT_LE(std::fabs(num - cost), 0.1 * std::fabs(num));
+}
+
+struct Fixture {
+  int D, r, S;
+  unsigned seed;
+  double vmax, amax;
+};
+// The reference's OptimizationParams instances
+// (test_polynomial_optimization.cpp:753-812).
+const Fixture kFixtures[] = {
+    {1, 4, 1, 100, 3.0, 5.0},  // segment_1_dim_1
+    {1, 4, 10, 102, 3.0, 5.0}, // segment_10_dim_1
+    {1, 4, 50, 103, 3.0, 5.0}, // segment_50_dim_1
+    {3, 4, 1, 104, 3.0, 5.0},  // segment_1_dim_3
+    {3, 4, 10, 105, 3.0, 5.0}, // segment_10_dim_3
+    {3, 4, 50, 106, 3.0, 5.0}, // segment_50_dim_3
+    {3, 4, 75, 106, 3.0, 5.0}, // segment_75_dim_3
+    {1, 2, 5, 107, 1.0, 2.0},  // deriv_accel_1
+    {3, 2, 1, 108, 1.0, 2.0},  // deriv_accel_3_1
+    {3, 2, 5, 109, 1.0, 2.0},  // deriv_accel
+    {3, 3, 5, 110, 1.0, 2.0},  // deriv_jerk
+};
+const Fixture& kSeg10Dim3 = kFixtures[4];
+
+Vertex::Vector fixtureVertices(const Fixture& f, int N) {
+  return createRandomVertices(N / 2 - 1, f.S, VectorXd::Constant(f.D, -10.0),
+                              VectorXd::Constant(f.D, 10.0), f.seed);
+}
+
+// ---------------------------------------------------------------- host tests
+
+TEST(host, AMatrixInversion) {
+  // test_polynomial_optimization.cpp:695-705: Schur inverse vs a general
+  // dense inverse at 1e-10 (Eigen's partial-pivot LU there and here).
+  for (double t = 1; t <= 60; t += 1) {
+    PolynomialOptimization<10>::SquareMatrix A, Ai;
+    PolynomialOptimization<10>::setupMappingMatrix(t, &A);
+    PolynomialOptimization<10>::invertMappingMatrix(A, &Ai);
+    const MatrixXd full = internal::smallInverse(A);  // dense 10 x 10 LU inverse
+    for (int i = 0; i < 10; ++i)
+      for (int j = 0; j < 10; ++j)
+        EXPECT_LE(std::fabs(Ai(i, j) - full(i, j)), 1e-10);
+  }
+}
+
+TEST(host, QuadraticCostJacobianMatchesOracle) {
+  for (int r = 0; r < 5; ++r)
+    for (double t : {0.1, 1.0, 3.7, 12.0}) {
+      PolynomialOptimization<10>::SquareMatrix Q;
+      PolynomialOptimization<10>::computeQuadraticCostJacobian(r, t, &Q);
+      std::vector<double> q(100), got(Q.data(), Q.data() + 100);
+      orc_segment_matrices(10, r, t, q.data(), nullptr, nullptr, nullptr);
+      EXPECT_LE(relErr(got, q), 1e-14);
+    }
+}
+
+TEST(host, MappingMatrixMatchesOracle) {
+  for (double t : {0.1, 1.0, 3.7, 12.0}) {
+    PolynomialOptimization<10>::SquareMatrix A, Ai;
+    PolynomialOptimization<10>::setupMappingMatrix(t, &A);
+    PolynomialOptimization<10>::invertMappingMatrix(A, &Ai);
+    std::vector<double> a(100), ai(100);
+    orc_segment_matrices(10, 4, t, nullptr, a.data(), ai.data(), nullptr);
+    EXPECT_LE(relErr(std::vector<double>(A.data(), A.data() + 100), a), 0.0);
+    EXPECT_LE(relErr(std::vector<double>(Ai.data(), Ai.data() + 100), ai), 1e-13);
+  }
+}
+
+TEST(host, RandomVerticesBitIdentical) {
+  for (const Fixture& f : kFixtures) {
+    const Vertex::Vector vs = fixtureVertices(f, 10);
+    const Dense d = toDense(vs, 5);
+    std::vector<double> lo(f.D, -10.0), hi(f.D, 10.0);
+    std::vector<uint8_t> mask((f.S + 1) * 5);
+    std::vector<double> vals((f.S + 1) * 5 * f.D);
+    orc_random_vertices(4, f.S, f.D, lo.data(), hi.data(), f.seed, 5, mask.data(),
+                        vals.data());
+    EXPECT_TRUE(mask == d.mask);
+    EXPECT_TRUE(vals == d.vals);  // bit-identical
+  }
+}
+
+TEST(host, SolveFailsLoudlyWithoutDevice) {
+  // No CPU fallback: the plan cannot be created without a HIP device.
+  const Vertex::Vector vs = fixtureVertices(kSeg10Dim3, 10);
+  PolynomialOptimization<10> opt(3);
+  EXPECT_THROW(opt.setupFromVertices(vs, estimateSegmentTimes(vs, 3.0, 5.0), 4));
+}
+
+TEST(host, ContractChecks) {
+  // linear_impl:50-55, 66-67: derivative out of range, size mismatch.
+  const Vertex::Vector vs = fixtureVertices(kSeg10Dim3, 10);
+  PolynomialOptimization<10> opt(3);
+  EXPECT_THROW(opt.setupFromVertices(vs, estimateSegmentTimes(vs, 3.0, 5.0), 5));
+  EXPECT_THROW(opt.setupFromVertices(vs, std::vector<double>(2, 1.0), 4));
+}
+
+// ----------------------------------------------------------------- gpu tests
+
+TEST(gpu, TwoVerticesSetup) {
+  // test_polynomial_optimization.cpp:707-751 (Matlab solution).
+  Vertex start(1);
+  for (int k = 0; k <= 4; ++k) start.addConstraint(k, 0.0);
+  Vertex goal = start;
+  goal.addConstraint(derivative_order::POSITION, 5.0);
+  PolynomialOptimization<10> opt(1);
+  Vertex::Vector vs{start, goal};
+  opt.setupFromVertices(vs, {5.0}, derivative_order::SNAP);
+  EXPECT_TRUE(opt.solveLinear());
+  Segment::Vector segs;
+  opt.getSegments(&segs);
+  checkPath(vs, segs, 10);
+  const double matlab[10] = {-0.000000000000004, 0.000000000000004, -0.000000000000006,
+                             0.000000000000003,  -0.000000000000001, 0.201600000000015,
+                             -0.134400000000012, 0.034560000000004,  -0.004032000000000,
+                             0.000179200000000};
+  const VectorXd c = segs[0][0].getCoefficients();
+  for (int k = 0; k < 10; ++k) EXPECT_LE(std::fabs(c[k] - matlab[k]), 1e-13);
+}
+
+template <int N>
+void runFixture(const Fixture& f) {
+  const Vertex::Vector vs = fixtureVertices(f, N);
+  const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+  PolynomialOptimization<N> opt(f.D);
+  opt.setupFromVertices(vs, times, f.r);
+  EXPECT_TRUE(opt.solveLinear());
+  Segment::Vector segs;
+  opt.getSegments(&segs);
+  checkPath(vs, segs, N);
+  checkCost(segs, f.r, opt.computeCost());
+
+  const Dense d = toDense(vs, N / 2);
+  std::vector<double> coeffs(f.S * f.D * N), df(f.D * (f.S + 1) * N / 2), dp(f.D * (f.S + 1) * N / 2);
+  double cost = 0.0;
+  int nf = 0, np = 0;
+  EXPECT_TRUE(orc_linear_solve(N, f.D, f.r, f.S, N / 2, d.mask.data(), d.vals.data(),
+                               times.data(), coeffs.data(), &cost, df.data(), dp.data(), &nf,
+                               &np) == 0);
+  EXPECT_TRUE(static_cast<size_t>(nf) == opt.getNumberFixedConstraints());
+  EXPECT_TRUE(static_cast<size_t>(np) == opt.getNumberFreeConstraints());
+  EXPECT_LE(relErr(coeffsOf(segs, N), coeffs), 1e-6);
+  EXPECT_LE(relErr(opt.computeCost(), cost), 1e-6);
+  std::vector<VectorXd> fixed, free_c;
+  opt.getFixedConstraints(&fixed);
+  opt.getFreeConstraints(&free_c);
+  std::vector<double> gf, gp;
+  for (int dd = 0; dd < f.D; ++dd) {
+    for (long i = 0; i < fixed[dd].size(); ++i) gf.push_back(fixed[dd][i]);
+    for (long i = 0; i < free_c[dd].size(); ++i) gp.push_back(free_c[dd][i]);
+  }
+  df.resize(f.D * nf);
+  dp.resize(f.D * np);
+  EXPECT_TRUE(gf == df);
+  EXPECT_LE(relErr(gp, dp), 1e-6);
+}
+
+TEST(gpu, ReferenceFixturesN10) {
+  for (const Fixture& f : kFixtures) runFixture<10>(f);
+}
+
+TEST(gpu, OtherOrders) {
+  for (const Fixture& f : kFixtures) {
+    Fixture g = f;
+    g.r = std::min(f.r, 2);
+    runFixture<6>(g);
+    g.r = std::min(f.r, 3);
+    runFixture<8>(g);
+  }
+}
+
+TEST(gpu, ConstraintPacking) {
+  // test_polynomial_optimization.cpp:510-570: feeding the solved free
+  // constraints back reproduces the segments; moving them off the optimum
+  // raises the cost.
+  const Fixture f = kSeg10Dim3;
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  PolynomialOptimization<10> opt(f.D);
+  opt.setupFromVertices(vs, estimateSegmentTimes(vs, f.vmax, f.amax), f.r);
+  opt.solveLinear();
+  Segment::Vector s0, s1;
+  opt.getSegments(&s0);
+  const double c0 = opt.computeCost();
+  std::vector<VectorXd> fc;
+  opt.getFreeConstraints(&fc);
+  opt.setFreeConstraints(fc);
+  opt.getSegments(&s1);
+  EXPECT_LE(relErr(coeffsOf(s1, 10), coeffsOf(s0, 10)), 1e-12);
+  EXPECT_LE(relErr(opt.computeCost(), c0), 1e-12);
+  fc[1][3] += 0.5;
+  opt.setFreeConstraints(fc);
+  EXPECT_TRUE(opt.computeCost() > c0);
+  Segment::Vector s2;
+  opt.getSegments(&s2);
+  checkPath(vs, s2, 10);  // still meets the fixed constraints and continuity
+}
+
+TEST(gpu, AccessorsMatchOracle) {
+  const Fixture f = kSeg10Dim3;
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+  PolynomialOptimization<10> opt(f.D);
+  opt.setupFromVertices(vs, times, f.r);
+  const Dense d = toDense(vs, 5);
+  const size_t n = opt.getNumberFixedConstraints() + opt.getNumberFreeConstraints();
+  const size_t na = opt.getNumberAllConstraints(), nc = 10 * f.S;
+  std::vector<double> R(n * n), M(na * n), A(nc * nc), Ai(nc * nc), Mp(n * na);
+  EXPECT_TRUE(orc_linear_matrices(10, f.D, f.r, f.S, 5, d.mask.data(), d.vals.data(),
+                                  times.data(), R.data(), M.data(), A.data(), Ai.data(),
+                                  Mp.data()) == 0);
+  MatrixXd gR, gM, gA, gAi, gMp;
+  opt.getR(&gR);
+  opt.getM(&gM);
+  opt.getA(&gA);
+  opt.getAInverse(&gAi);
+  opt.getMpinv(&gMp);
+  auto vec = [](const MatrixXd& m) {
+    return std::vector<double>(m.data(), m.data() + m.rows() * m.cols());
+  };
+  EXPECT_LE(relErr(vec(gR), R), 1e-9);
+  EXPECT_TRUE(vec(gM) == M);
+  EXPECT_LE(relErr(vec(gA), A), 1e-15);
+  EXPECT_LE(relErr(vec(gAi), Ai), 1e-12);
+  EXPECT_TRUE(vec(gMp) == Mp);
+}
+
+TEST(gpu, StaleCostAfterTimeUpdate) {
+  // computeCost after updateSegmentTimes without a re-solve uses the new Q
+  // with the old coefficients (linear_impl:113-130, 277-304).
+  const Fixture f = kSeg10Dim3;
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+  PolynomialOptimization<10> opt(f.D);
+  opt.setupFromVertices(vs, times, f.r);
+  opt.solveLinear();
+  Segment::Vector segs;
+  opt.getSegments(&segs);
+  for (double& t : times) t *= 1.3;
+  opt.updateSegmentTimes(times);
+  double want = 0.0;
+  for (int s = 0; s < f.S; ++s) {
+    std::vector<double> Q(100);
+    orc_segment_matrices(10, f.r, times[s], Q.data(), nullptr, nullptr, nullptr);
+    for (int dd = 0; dd < f.D; ++dd) {
+      const VectorXd c = segs[s][dd].getCoefficients();
+      for (int i = 0; i < 10; ++i)
+        for (int j = 0; j < 10; ++j) want += c[i] * Q[i * 10 + j] * c[j];
+    }
+  }
+  EXPECT_LE(relErr(opt.computeCost(), 0.5 * want), 1e-12);
+  opt.solveLinear();  // re-solve at the new times lowers the cost
+  EXPECT_TRUE(opt.computeCost() <= 0.5 * want * (1 + 1e-12));
+}
+
+TEST(gpu, FullyConstrained) {
+  Vertex::Vector vs = fixtureVertices(kSeg10Dim3, 10);
+  for (Vertex& v : vs)
+    for (int k = 1; k <= 4; ++k)
+      if (!v.hasConstraint(k)) v.addConstraint(k, 0.25 * k);
+  PolynomialOptimization<10> opt(3);
+  const std::vector<double> times = estimateSegmentTimes(vs, 3.0, 5.0);
+  opt.setupFromVertices(vs, times, 4);
+  EXPECT_TRUE(opt.getNumberFreeConstraints() == 0);
+  EXPECT_TRUE(opt.solveLinear());
+  Segment::Vector segs;
+  opt.getSegments(&segs);
+  checkPath(vs, segs, 10);
+  const Dense d = toDense(vs, 5);
+  const int S = kSeg10Dim3.S;
+  std::vector<double> coeffs(S * 3 * 10);
+  double cost = 0.0;
+  orc_linear_solve(10, 3, 4, S, 5, d.mask.data(), d.vals.data(), times.data(), coeffs.data(),
+                   &cost, nullptr, nullptr, nullptr, nullptr);
+  EXPECT_LE(relErr(coeffsOf(segs, 10), coeffs), 1e-9);
+  EXPECT_LE(relErr(opt.computeCost(), cost), 1e-9);
+}
+
+// src/main.cpp:26-75 geometry (4 segments, radii 0.15).
+Vertex::Vector mainCppVertices() {
+  const double pts[5][3] = {{2.7, 9.5, 4.8},
+                            {3.50796, 4.34802, 4.56653},
+                            {3.95552, 3.23008, 4.75131},
+                            {5.06673, 2.31032, 4.79433},
+                            {7.0, 2.2, 4.8}};
+  Vertex::Vector vs;
+  for (int v = 0; v < 5; ++v) {
+    Vertex x(3);
+    VectorXd p{pts[v][0], pts[v][1], pts[v][2]};
+    if (v == 0 || v == 4)
+      x.makeStartOrEnd(p, 4);
+    else
+      x.addConstraint(derivative_order::POSITION, p);
+    vs.push_back(x);
+  }
+  return vs;
+}
+
+TEST(gpu, TubeQCQPMainFixture) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> times = estimateSegmentTimes(vs, 2.0, 2.0);
+  const std::vector<std::pair<double, double>> radii(4, {0.15, 0.15});
+  PolynomialOptimizationConstrained<10> opt(3);
+  opt.setupFromVertices(vs, times, radii, 4);
+  EXPECT_TRUE(opt.getNumberFixedConstraints() == 10);
+  EXPECT_TRUE(opt.getNumberFreeConstraints() == 15);
+  EXPECT_TRUE(opt.solveQCQP() == 0);
+  const Dense d = toDense(vs, 5);
+  std::vector<double> rad(8, 0.15), x(45), coeffs(4 * 3 * 10);
+  double cost = 0.0;
+  int iters = 0;
+  EXPECT_TRUE(orc_tube_qcqp_solve(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), times.data(),
+                                  times.data(), rad.data(), 1e-10, 100, x.data(),
+                                  coeffs.data(), &cost, &iters) == 0);
+  Segment::Vector segs;
+  opt.getSegments(&segs);
+  EXPECT_LE(relErr(coeffsOf(segs, 10), coeffs), 1e-6);
+  EXPECT_LE(relErr(opt.computeCost(), cost), 1e-6);
+  std::vector<VectorXd> fc;
+  opt.getFreeConstraints(&fc);
+  std::vector<double> gx;
+  for (const VectorXd& v : fc)
+    for (long i = 0; i < v.size(); ++i) gx.push_back(v[i]);
+  EXPECT_LE(relErr(gx, x), 1e-6);
+  const std::vector<double> res = opt.getConstraintResiduals();
+  EXPECT_TRUE(static_cast<int>(res.size()) == orc_tube_num_constraints(10, 4));
+  double worst = -1e300;
+  for (double r : res) worst = std::max(worst, r);
+  EXPECT_LE(worst, 1e-8);
+  // Start/end constraints and continuity hold; intermediate positions are
+  // free (they define the tube only).
+  Vertex::Vector ends{vs.front(), vs.back()};
+  EXPECT_LE(segs.front().evaluate(0.0, 0)[0] - 2.7, 1e-9);
+  // The unconstrained tube-pattern solve is no costlier than the QCQP.
+  const double qcqp_cost = opt.computeCost();
+  opt.solveLinear();
+  EXPECT_LE(opt.computeCost(), qcqp_cost * (1 + 1e-9));
+}
+
+TEST(gpu, TimeCostMatchesOracle) {
+  const Fixture f = kSeg10Dim3;
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.weights.w_c = 0.0;
+  PolynomialOptimizationNonLinear<10> opt(f.D, p);
+  opt.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}),
+                        f.r);
+  const Dense d = toDense(vs, 5);
+  for (int mode = 0; mode <= 2; ++mode) {
+    std::vector<double> g, og(f.S);
+    const double J = opt.evaluateTimeCost(times, mode, mode ? &g : nullptr);
+    double oJ = 0.0;
+    EXPECT_TRUE(orc_time_cost(10, f.D, f.r, f.S, 5, d.mask.data(), d.vals.data(), times.data(),
+                              p.time_penalty, mode, p.increment_time, p.weights.w_d,
+                              p.weights.w_t, &oJ, og.data()) == 0);
+    EXPECT_LE(relErr(J, oJ), 1e-9);
+    if (mode) EXPECT_LE(relErr(g, og), 1e-5);
+  }
+}
+
+TEST(gpu, OptimizeTimeLowersObjective) {
+  const Fixture f = kSeg10Dim3;
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  const std::vector<double> t0 = estimateSegmentTimes(vs, f.vmax, f.amax);
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.weights.w_c = 0.0;
+  p.max_iterations = 50;
+  PolynomialOptimizationNonLinear<10> opt(f.D, p);
+  opt.setupFromVertices(vs, t0, std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}), f.r);
+  const double J0 = opt.evaluateTimeCost(t0);
+  EXPECT_TRUE(opt.optimize() > 0);
+  std::vector<double> t1;
+  opt.getPolynomialOptimizationRef().getSegmentTimes(&t1);
+  const OptimizationInfo info = opt.getOptimizationInfo();
+  EXPECT_TRUE(info.n_iterations <= 50 && info.n_iterations >= 1);
+  const double J1 = opt.evaluateTimeCost(t1);
+  EXPECT_LE(J1, J0);
+  EXPECT_LE(relErr(J1, info.cost_trajectory + info.cost_time), 1e-9);
+  for (size_t i = 0; i < t1.size(); ++i) {
+    EXPECT_TRUE(t1[i] >= 0.1 - 1e-15);
+    EXPECT_TRUE(t1[i] <= 2.0 * t0[i] + 1e-12);
+  }
+  Trajectory traj;
+  opt.getTrajectory(&traj);
+  Segment::Vector segs;
+  traj.getSegments(&segs);
+  checkPath(vs, segs, 10);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string group = argc > 1 ? argv[1] : "host";
+  int run = 0, failed_tests = 0;
+  for (const TestCase& t : registry()) {
+    if (group != "all" && group != t.group) continue;
+    const int before = g_failures;
+    std::printf("[ RUN      ] %s.%s\n", t.group, t.name);
+    try {
+      t.fn();
+    } catch (const std::exception& e) {
+      ++g_failures;
+      std::fprintf(stderr, "  EXCEPTION: %s\n", e.what());
+    }
+    const bool ok = g_failures == before;
+    failed_tests += ok ? 0 : 1;
+    std::printf("[ %s ] %s.%s\n", ok ? "      OK" : " FAILED ", t.group, t.name);
+    ++run;
+  }
+  std::printf("%d tests, %d checks, %d failed tests\n", run, g_checks, failed_tests);
+  return failed_tests == 0 && run > 0 ? 0 : 1;
+}

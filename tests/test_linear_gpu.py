@@ -244,3 +244,34 @@ def test_segment_matrices(ctx, dev, oracle):
         assert np.allclose(Ai[i], Aio, atol=1e-9, rtol=0)
         assert np.allclose(Q[i], Qo, rtol=1e-13, atol=0)
         assert np.max(np.abs(H[i] - Ho)) <= 1e-8 * np.max(np.abs(Ho))
+
+
+def test_coefficients_from_constraints(ctx, dev, oracle):
+    """mtg_coeffs_from_constraints (setFreeConstraints ->
+    updateSegmentsFromCompactConstraints, linear_impl:254-275, 497-506):
+    feeding the solved d_p back reproduces the solve; a perturbed d_p gives
+    the oracle's A^-1 M [d_f; d_p] and a higher cost."""
+    import mav_tube_trajectory_generation_amd as mtg
+    N, D, S, B = 10, 3, 10, 64
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=105)
+    plan, out = _solve_gpu(ctx, dev, N, 4, mask, fixed, times)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    c, cost, st = plan.coefficients(T(fixed), T(out["free"]), T(times))
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert rel_err_coeffs(c.cpu().numpy(), out["coeffs"]) <= 1e-12
+    assert np.max(np.abs(cost.cpu().numpy() - out["cost"]) / out["cost"]) <= 1e-12
+    rng = np.random.default_rng(3)
+    dp = out["free"] + rng.normal(0.0, 0.3, out["free"].shape)
+    c2, cost2, _ = plan.coefficients(T(fixed), T(dp), T(times))
+    c2, cost2 = c2.cpu().numpy(), cost2.cpu().numpy()
+    assert np.all(cost2 > out["cost"])
+    for b in (0, 17, 63):
+        v = standard_vertices(N, S, D, 105 + b)
+        m = oracle.linear_matrices(N, 4, v, times[b])
+        nf = fixed.shape[2]
+        for d in range(D):
+            dall = np.concatenate([fixed[b, d], dp[b, d]])
+            want = (m["Ainv"] @ m["M"] @ dall).reshape(S, N)
+            assert rel_err_coeffs(c2[b, :, d], want) <= 1e-9, (b, d)
+        assert nf == m["M"].shape[1] - dp.shape[2]
