@@ -49,9 +49,25 @@ __device__ unsigned long long g_mtg_stamps[512];
     }                                                                       \
     __builtin_amdgcn_sched_barrier(0);                                      \
   } while (0)
+// Accumulating variant: adds the cycles since `last` to slot and resets
+// `last` (phase totals over loop iterations).
+#define MTG_TACC(slot, last)                                                \
+  do {                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                              \
+      unsigned long long t_;                                                \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      atomicAdd(&g_mtg_stamps[(slot)], t_ - (last)); /* no-return: no wait */ \
+      (last) = t_;                                                          \
+    }                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+  } while (0)
 #else
 #define MTG_STAMP(slot) \
   do {                  \
+  } while (0)
+#define MTG_TACC(slot, last) \
+  do {                       \
   } while (0)
 #endif
 

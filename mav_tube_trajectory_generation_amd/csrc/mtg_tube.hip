@@ -45,7 +45,7 @@ __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
 }
 
 template <int N>
-__global__ __launch_bounds__(kWave) void tube_solve_kernel(
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void tube_solve_kernel(
     int S, int r, const double* __restrict__ tab, const double* __restrict__ positions,
     const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
     const double* __restrict__ times, const double* __restrict__ radii, double tol,
@@ -98,6 +98,13 @@ __global__ __launch_bounds__(kWave) void tube_solve_kernel(
                            : (st == 0 ? MTG_TRAJ_OK : MTG_TRAJ_NOT_CONVERGED);
   }
 }
+
+#ifdef MTG_STAMPS
+extern "C" int mtg_debug_tube_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mtg_stamps), sizeof(unsigned long long) * n) ==
+                 hipSuccess ? 0 : -3;
+}
+#endif
 
 size_t tube_lds_bytes(int N, int S) {
   if (S < 2) return 0;

@@ -39,10 +39,11 @@ struct TubeLayout {
   int x, dx, rd, rhs;     // nv*3M each
   int cp, dcp, acc;       // S*N*3 each
   int s, lam, g, ds, dl, prod;  // ncon each
-  int Lk;                 // nv*BS*BS  (K blocks -> L^-1)
-  int W;                  // max(nv-1,1)*BS*BS (also G per control point: S*N*9)
-  int dinv;               // nv*BS
-  int tmp;                // BS*BS
+  int Li;                 // nv*BS*BS  unit lower L_a^-1, row-major
+  int W;                  // max(nv-1,1)*BS*BS  W_a = L_a^-1 C_a, row-major
+  int dinv;               // nv*BS     1 / pivots of S_a = L_a D_a L_a^T
+  int Gc;                 // S*N*9  per control point: sum lam Hess + lam/s w w^T
+  int tmp;                // BS
   int red;                // 64
   int ndouble;
   size_t bytes() const { return sizeof(double) * ndouble; }
@@ -82,12 +83,11 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   l.ds = o;   o += nc;
   l.dl = o;   o += nc;
   l.prod = o; o += nc;
-  l.Lk = o;   o += nv * BS * BS;
-  const int wsz = (nv > 1 ? nv - 1 : 1) * BS * BS;
-  const int gsz = S * N * 9;
-  l.W = o;    o += wsz > gsz ? wsz : gsz;
+  l.Li = o;   o += nv * BS * BS;
+  l.W = o;    o += (nv > 1 ? nv - 1 : 1) * BS * BS;
   l.dinv = o; o += nv * BS;
-  l.tmp = o;  o += BS * BS;
+  l.Gc = o;   o += S * N * 9;
+  l.tmp = o;  o += BS;
   l.red = o;  o += kWave;
   l.ndouble = o;
   return l;
@@ -378,128 +378,190 @@ struct Tube {
   }
 
   // --------------------------------------------------------- KKT assembly
-  // G per control point -> W region; K_a = P_a (x) I + sum G (x) beta beta^T.
-  __device__ void assemble_kkt(bool with_constraints) {
-    double* Gcp = sm + L->W;
-    if (with_constraints) {
-      for (int cpi = lane; cpi < S * N; cpi += kWave) {
-        const int i = cpi / N, j = cpi % N;
-        double G[9];
+  // Per control point: G = sum_k lam_k Hess_k + (lam_k / s_k) w_k w_k^T over
+  // the (at most 3) constraints acting on it.  The diagonal KKT block of
+  // vertex a is K_a = I_3 (x) Pd_a + sum_cp G_cp (x) beta_cp beta_cp^T; its
+  // columns are built in registers by factor().
+  __device__ void assemble_g() {
+    double* Gcp = sm + L->Gc;
+    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+      const int i = cpi / N, j = cpi % N;
+      double G[9];
 #pragma unroll
-        for (int e = 0; e < 9; ++e) G[e] = 0.0;
+      for (int e = 0; e < 9; ++e) G[e] = 0.0;
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const int k = con_at(i, j, t);
-          if (k < 0) continue;
-          double w[3];
-          con_eval(k, L->cp, w);
-          int ii, jj, type;
-          con_of(k, &ii, &jj, &type);
-          const double lam = sm[L->lam + k], s = sm[L->s + k];
-          const double ws = lam / s;
-          for (int a = 0; a < 3; ++a)
-            for (int e = 0; e < 3; ++e)
-              G[a * 3 + e] += lam * con_hess(type, i, a, e) + ws * w[a] * w[e];
-        }
-        for (int e = 0; e < 9; ++e) Gcp[cpi * 9 + e] = G[e];
+      for (int t = 0; t < 3; ++t) {
+        const int k = con_at(i, j, t);
+        if (k < 0) continue;
+        double w[3];
+        con_eval(k, L->cp, w);
+        int ii, jj, type;
+        con_of(k, &ii, &jj, &type);
+        const double lam = sm[L->lam + k], s = sm[L->s + k];
+        const double ws = lam / s;
+        for (int a = 0; a < 3; ++a)
+          for (int e = 0; e < 3; ++e)
+            G[a * 3 + e] += lam * con_hess(type, i, a, e) + ws * w[a] * w[e];
       }
-      __syncthreads();
-    }
-    for (int idx = lane; idx < nv * BS * BS; idx += kWave) {
-      const int a = idx / (BS * BS);
-      const int row = (idx / BS) % BS, col = idx % BS;
-      if (col > row) continue;  // the factorisation reads the lower triangle
-      const int d = row / M, m = row % M, d2 = col / M, m2 = col % M;
-      double v = (d == d2) ? sm[L->Pd + a * M * M + m * M + m2] : 0.0;
-      if (with_constraints) {
-        const int u = a + 1;
-        for (int j = M; j < N; ++j)
-          v += Gcp[((u - 1) * N + j) * 9 + d * 3 + d2] * beta(u - 1, j, m) * beta(u - 1, j, m2);
-        for (int j = 0; j < M; ++j)
-          v += Gcp[(u * N + j) * 9 + d * 3 + d2] * beta(u, j, m) * beta(u, j, m2);
-      }
-      sm[L->Lk + idx] = v;
+      for (int e = 0; e < 9; ++e) Gcp[cpi * 9 + e] = G[e];
     }
     __syncthreads();
   }
 
-  // --------------------------------------------------------- factorisation
-  // Block LDL^T: Lk_a <- unit L_a^-1 (lower), dinv_a, W_a = L_a^-1 K_{a,a+1}.
-  // Sets *fail = 1 on a non-positive pivot.
-  __device__ void factor(int* fail) {
-    double* tmp = sm + L->tmp;
-    for (int a = 0; a < nv; ++a) {
-      double* A = sm + L->Lk + a * BS * BS;
-      if (a > 0) {
-        const double* Wp = sm + L->W + (a - 1) * BS * BS;
-        const double* dp = sm + L->dinv + (a - 1) * BS;
-        for (int idx = lane; idx < BS * BS; idx += kWave) {
-          const int i = idx / BS, k = idx % BS;
-          if (k > i) continue;
-          double v = A[idx];
-          for (int t = 0; t < BS; ++t) v -= Wp[t * BS + i] * dp[t] * Wp[t * BS + k];
-          A[idx] = v;
-        }
-        __syncthreads();
-      }
-      // Right-looking LDL^T on the lower triangle.
-      for (int j = 0; j < BS; ++j) {
-        const double dj = A[j * BS + j];
-        if (lane == 0 && !(dj > 0.0)) *fail = 1;
-        const double inv = rcp64(dj > 0.0 ? dj : 1.0);
-        const int rem = BS - 1 - j;
-        for (int t = lane; t < rem * rem; t += kWave) {
-          const int i = j + 1 + t / rem, k = j + 1 + t % rem;
-          if (k > i) continue;
-          A[i * BS + k] -= A[i * BS + j] * inv * A[k * BS + j];
-        }
-        __syncthreads();
-      }
-      if (lane < BS) sm[L->dinv + a * BS + lane] = rcp64(A[lane * BS + lane] > 0.0 ? A[lane * BS + lane] : 1.0);
-      __syncthreads();
-      // Unit L in place (lower, strictly): L[i][j] = A[i][j] * dinv[j].
-      for (int idx = lane; idx < BS * BS; idx += kWave) {
-        const int i = idx / BS, j = idx % BS;
-        if (j < i) A[idx] *= sm[L->dinv + a * BS + j];
-      }
-      __syncthreads();
-      // Column c of L^-1 (unit lower): x = e_c, x_i = -sum_{k<i} L[i][k] x_k,
-      // built in LDS (tmp) by lane c (no private arrays -> no scratch).
-      if (lane < BS) {
-        const int c = lane;
-        for (int i = 0; i < BS; ++i) {
-          double v;
-          if (i < c) {
-            v = 0.0;
-          } else if (i == c) {
-            v = 1.0;
-          } else {
-            v = 0.0;
-            for (int k = c; k < i; ++k) v -= A[i * BS + k] * tmp[k * BS + c];
-          }
-          tmp[i * BS + c] = v;
-        }
-      }
-      __syncthreads();
-      for (int idx = lane; idx < BS * BS; idx += kWave) A[idx] = tmp[idx];
-      __syncthreads();
-      // W_a = L_a^-1 (I_3 (x) Po_a)
-      if (a < nv - 1) {
-        double* Wa = sm + L->W + a * BS * BS;
-        const double* P = sm + L->Po + a * M * M;
-        for (int idx = lane; idx < BS * BS; idx += kWave) {
-          const int i = idx / BS, col = idx % BS;
-          const int d2 = col / M, m2 = col % M;
-          double v = 0.0;
-          for (int t = 0; t < M; ++t) v += A[i * BS + d2 * M + t] * P[t * M + m2];
-          Wa[idx] = v;
-        }
-        __syncthreads();
-      }
-    }
+  // 64-bit lane broadcast (uniform source lane).
+  __device__ static double bcast(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(b & 0xffffffffLL), src);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), src);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) |
+                                (static_cast<unsigned int>(lo)));
   }
 
-  // Solve K dx = rhs with the factors (rhs overwritten by y).
+  // --------------------------------------------------------- factorisation
+  // Block LDL^T of the block-tridiagonal KKT matrix.  For vertex block a:
+  //   S_a = K_a - W_{a-1}^T D_{a-1}^-1 W_{a-1} = L_a D_a L_a^T,
+  //   W_a = L_a^-1 C_a,   C_a = I_3 (x) Po_a (coupling to block a+1).
+  // The elimination runs on [S_a | I | C_a] held column-per-lane in
+  // registers (lanes 0..BS-1, BS..2BS-1, 2BS..3BS-1); the pivot column is
+  // broadcast with v_readlane, so a block needs no LDS traffic and no
+  // barrier inside.  Afterwards lanes BS.. hold L_a^-1 (unit lower) and
+  // lanes 2BS.. hold W_a; the pivots are D_a.  S_a is SPD (no pivoting); a
+  // non-positive pivot sets *fail.
+  __device__ void factor(int* fail, bool with_constraints) {
+    const double* Gcp = sm + L->Gc;
+    int bad = 0;
+    unsigned long long tf = 0;
+    MTG_TACC(511, tf);
+    for (int a = 0; a < nv; ++a) {
+      const int u = a + 1;  // vertex
+      double col[BS];
+      const int c = lane;
+      // Lane roles: 0 = column c of S_a, 1 = identity column, 2 = column of
+      // C_a, 3 = idle.  Loads are unconditional (clamped indices) and the
+      // role only selects values, so the build has no divergent branches.
+      const int role = c < BS ? 0 : c < 2 * BS ? 1 : (c < 3 * BS && a < nv - 1) ? 2 : 3;
+      const int cc = c < BS ? c : c < 2 * BS ? c - BS : c < 3 * BS ? c - 2 * BS : 0;
+      const int d2 = cc / M, m2 = cc % M;
+      {
+        const double* Pd = sm + L->Pd + a * M * M;
+        const double* Po = sm + L->Po + (a < nv - 1 ? a : 0) * M * M;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const double pd = Pd[m * M + m2], po = Po[m * M + m2];
+          const double v = role == 0 ? pd : role == 2 ? po : 0.0;
+#pragma unroll
+          for (int d = 0; d < 3; ++d) col[d * M + m] = (d == d2) ? v : 0.0;
+        }
+        if (role == 1) {
+#pragma unroll
+          for (int i = 0; i < BS; ++i) col[i] = (i == cc) ? 1.0 : 0.0;
+        }
+      }
+      MTG_TACC(220, tf);
+      if (with_constraints) {
+        // sum over the control points of vertex u (segment u-1, j = M..N-1;
+        // segment u, j = 0..M-1) of G[d][d2] beta[m] beta[m2]; lanes of
+        // role != 0 accumulate zeros.  Loads of control point q+1 are issued
+        // before the arithmetic of q (sched barriers keep them there).
+        const double on = role == 0 ? 1.0 : 0.0;
+        double bt[M], g3[3], bt2[M], g32[3];
+        auto load_cp = [&](int q, double* b, double* g) {
+          const int i = q < M ? u - 1 : u;
+          const int j = q < M ? q + M : q - M;
+          const int cpi = i * N + j;
+#pragma unroll
+          for (int m = 0; m < M; ++m) b[m] = sm[L->bet + cpi * M + m];
+#pragma unroll
+          for (int d = 0; d < 3; ++d) g[d] = Gcp[cpi * 9 + d * 3 + d2];
+        };
+        load_cp(0, bt, g3);
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+          if (q + 1 < N) load_cp(q + 1, bt2, g32);
+          __builtin_amdgcn_sched_barrier(0);
+          double bm2 = bt[0];
+#pragma unroll
+          for (int m = 1; m < M; ++m) bm2 = (m == m2) ? bt[m] : bm2;
+          bm2 *= on;
+#pragma unroll
+          for (int d = 0; d < 3; ++d) {
+            const double gd = g3[d] * bm2;
+#pragma unroll
+            for (int m = 0; m < M; ++m) col[d * M + m] = fma(gd, bt[m], col[d * M + m]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int m = 0; m < M; ++m) bt[m] = bt2[m];
+#pragma unroll
+          for (int d = 0; d < 3; ++d) g3[d] = g32[d];
+        }
+      }
+      MTG_TACC(221, tf);
+      if (a > 0) {
+        // S_a[:, c] -= sum_t W[t][:] dinv[t] W[t][c]  (W = W_{a-1}); row
+        // t+1 is loaded while row t is applied.
+        const double* Wp = sm + L->W + (a - 1) * BS * BS;
+        const double* dp = sm + L->dinv + (a - 1) * BS;
+        const double on = role == 0 ? 1.0 : 0.0;
+        double wr[BS], wn[BS], wc, dt, wcn = 0.0, dtn = 0.0;
+#pragma unroll
+        for (int i = 0; i < BS; ++i) wr[i] = Wp[i];
+        wc = Wp[cc];
+        dt = dp[0];
+#pragma unroll
+        for (int t = 0; t < BS; ++t) {
+          if (t + 1 < BS) {
+#pragma unroll
+            for (int i = 0; i < BS; ++i) wn[i] = Wp[(t + 1) * BS + i];
+            wcn = Wp[(t + 1) * BS + cc];
+            dtn = dp[t + 1];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          const double w = wc * dt * on;
+#pragma unroll
+          for (int i = 0; i < BS; ++i) col[i] = fma(-wr[i], w, col[i]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < BS; ++i) wr[i] = wn[i];
+          wc = wcn;
+          dt = dtn;
+        }
+      }
+      // Forward elimination (below the pivot) on all columns at once; the
+      // pivot column is broadcast with v_readlane.
+      MTG_TACC(222, tf);
+      double dj_own = 0.0;  // pivot j, kept by lane j
+#pragma unroll
+      for (int j = 0; j < BS; ++j) {
+        const double piv = bcast(col[j], j);
+        bad |= !(piv > 0.0);
+        dj_own = lane == j ? piv : dj_own;
+        if (j == BS - 1) break;
+        const double f = col[j] * rcp64(piv > 0.0 ? piv : 1.0);
+#pragma unroll
+        for (int i = j + 1; i < BS; ++i) col[i] = fma(-bcast(col[i], j), f, col[i]);
+      }
+      MTG_TACC(223, tf);
+      // Lanes BS.. store L_a^-1 columns, lanes 2BS.. W_a columns, the rest
+      // write into the scratch column `tmp` (same instruction stream).
+      {
+        const bool keep = role == 1 || role == 2;
+        double* dst = keep ? sm + (role == 1 ? L->Li : L->W) + a * BS * BS + cc
+                           : sm + L->tmp;
+        const int stride = keep ? BS : 0;
+#pragma unroll
+        for (int i = 0; i < BS; ++i) dst[i * stride] = col[i];
+        if (c < BS) sm[L->dinv + a * BS + c] = rcp64(dj_own > 0.0 ? dj_own : 1.0);
+      }
+      __syncthreads();
+      MTG_TACC(224, tf);
+    }
+    if (bad && lane == 0) *fail = 1;
+  }
+
+  // Solve K out = rhs with the block factors (rhs overwritten by y):
+  // forward y_a = L_a^-1 (rhs_a - W_{a-1}^T D_{a-1}^-1 y_{a-1}), backward
+  // out_a = L_a^-T D_a^-1 (y_a - W_a out_{a+1}).
   __device__ void solve(int rhs_off, int out_off) {
     double* tmp = sm + L->tmp;
     double* y = sm + rhs_off;
@@ -510,15 +572,17 @@ struct Tube {
         if (a > 0) {
           const double* Wp = sm + L->W + (a - 1) * BS * BS;
           const double* dp = sm + L->dinv + (a - 1) * BS;
+#pragma unroll
           for (int k = 0; k < BS; ++k) t -= Wp[k * BS + lane] * dp[k] * y[(a - 1) * BS + k];
         }
         tmp[lane] = t;
       }
       __syncthreads();
       if (lane < BS) {
-        const double* Li = sm + L->Lk + a * BS * BS;
+        const double* Li = sm + L->Li + a * BS * BS + lane * BS;
         double v = 0.0;
-        for (int k = 0; k <= lane; ++k) v += Li[lane * BS + k] * tmp[k];
+#pragma unroll
+        for (int k = 0; k < BS; ++k) v += (k <= lane ? Li[k] : 0.0) * tmp[k];
         y[a * BS + lane] = v;
       }
       __syncthreads();
@@ -527,16 +591,18 @@ struct Tube {
       if (lane < BS) {
         double t = y[a * BS + lane];
         if (a < nv - 1) {
-          const double* Wa = sm + L->W + a * BS * BS;
-          for (int k = 0; k < BS; ++k) t -= Wa[lane * BS + k] * xo[(a + 1) * BS + k];
+          const double* Wa = sm + L->W + a * BS * BS + lane * BS;
+#pragma unroll
+          for (int k = 0; k < BS; ++k) t -= Wa[k] * xo[(a + 1) * BS + k];
         }
         tmp[lane] = t * sm[L->dinv + a * BS + lane];
       }
       __syncthreads();
       if (lane < BS) {
-        const double* Li = sm + L->Lk + a * BS * BS;
+        const double* Li = sm + L->Li + a * BS * BS;
         double v = 0.0;
-        for (int k = lane; k < BS; ++k) v += Li[k * BS + lane] * tmp[k];
+#pragma unroll
+        for (int k = 0; k < BS; ++k) v += (k >= lane ? Li[k * BS + lane] : 0.0) * tmp[k];
         xo[a * BS + lane] = v;
       }
       __syncthreads();
@@ -586,7 +652,10 @@ struct Tube {
       sm[L->rhs + idx] = -sm[L->rd + idx] - gather_cp(L->acc, a, d, m);
     }
     __syncthreads();
+    unsigned long long tl = 0;
+    MTG_TACC(511, tl);
     solve(L->rhs, L->dx);
+    MTG_TACC(210, tl);
     control_point_steps(sm + L->dx, L->dcp);
     __syncthreads();
     for (int k = lane; k < nc; k += kWave) {
@@ -627,8 +696,7 @@ struct Tube {
     if (lane == 0) *fail = 0;
     __syncthreads();
     // Unconstrained start: P x = -q.
-    assemble_kkt(false);
-    factor(fail);
+    factor(fail, false);
     __syncthreads();
     if (*fail) {
       if (lane == 0) *bad |= 2;
@@ -653,6 +721,8 @@ struct Tube {
     __syncthreads();
     int it = 0;
     *status = 1;
+    unsigned long long tl = 0;
+    MTG_TACC(511, tl);
     for (it = 0; it < max_iter; ++it) {
       // Residuals at the current point.
       control_points(sm + L->x, L->cp);
@@ -698,11 +768,14 @@ struct Tube {
         break;
       }
       const bool near = rdn <= 1e3 * tol * (1.0 + qn) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
-      assemble_kkt(true);
+      MTG_TACC(200, tl);
+      assemble_g();
+      MTG_TACC(201, tl);
       if (lane == 0) *fail = 0;
       __syncthreads();
-      factor(fail);
+      factor(fail, true);
       __syncthreads();
+      MTG_TACC(202, tl);
       if (*fail) {
         *status = near ? 0 : 2;
         break;
@@ -711,6 +784,7 @@ struct Tube {
       for (int k = lane; k < nc; k += kWave) sm[L->prod + k] = sm[L->s + k] * sm[L->lam + k];
       __syncthreads();
       direction();
+      MTG_TACC(203, tl);
       const double a_aff = max_step();
       double mua = 0.0;
       for (int k = lane; k < nc; k += kWave)
@@ -723,7 +797,9 @@ struct Tube {
       for (int k = lane; k < nc; k += kWave)
         sm[L->prod + k] = sm[L->s + k] * sm[L->lam + k] + sm[L->ds + k] * sm[L->dl + k] - sigma * mu;
       __syncthreads();
+      MTG_TACC(204, tl);
       direction();
+      MTG_TACC(205, tl);
       const double alpha = fmin(1.0, 0.99 * max_step());
       double dxn = 0.0;
       for (int idx = lane; idx < nv * BS; idx += kWave) dxn = fmax(dxn, fabs(sm[L->dx + idx]));
@@ -738,6 +814,7 @@ struct Tube {
         sm[L->lam + k] += alpha * sm[L->dl + k];
       }
       __syncthreads();
+      MTG_TACC(206, tl);
     }
     return it;
   }
