@@ -43,7 +43,7 @@ struct TubeLayout {
   int W;                  // max(nv-1,1)*BS*BS  W_a = L_a^-1 C_a, row-major
   int dinv;               // nv*BS     1 / pivots of S_a = L_a D_a L_a^T
   int Gc;                 // S*N*9  per control point: sum lam Hess + lam/s w w^T
-  int tmp;                // BS
+  int tmp;                // BS*BS+1 (U columns in factor, solve scratch; last = dummy)
   int red;                // 64
   int ndouble;
   size_t bytes() const { return sizeof(double) * ndouble; }
@@ -87,7 +87,7 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   l.W = o;    o += (nv > 1 ? nv - 1 : 1) * BS * BS;
   l.dinv = o; o += nv * BS;
   l.Gc = o;   o += S * N * 9;
-  l.tmp = o;  o += BS;
+  l.tmp = o;  o += BS * BS + 1;
   l.red = o;  o += kWave;
   l.ndouble = o;
   return l;
@@ -408,6 +408,12 @@ struct Tube {
     __syncthreads();
   }
 
+  // 1.0 if x == 0 else 0.0, by integer arithmetic: a compare would yield a
+  // lane mask (SGPR pair) that the compiler hoists and keeps live.
+  __device__ static double is_zero(int x) {
+    return static_cast<double>(((x | -x) >> 31) + 1);
+  }
+
   // 64-bit lane broadcast (uniform source lane).
   __device__ static double bcast(double v, int src) {
     const long long b = __double_as_longlong(v);
@@ -437,25 +443,26 @@ struct Tube {
       double col[BS];
       const int c = lane;
       // Lane roles: 0 = column c of S_a, 1 = identity column, 2 = column of
-      // C_a, 3 = idle.  Loads are unconditional (clamped indices) and the
-      // role only selects values, so the build has no divergent branches.
+      // C_a, 3 = idle.  Loads are unconditional (clamped indices) and roles
+      // enter as exact 0/1 factors (VGPR values: no lane masks kept live).
       const int role = c < BS ? 0 : c < 2 * BS ? 1 : (c < 3 * BS && a < nv - 1) ? 2 : 3;
       const int cc = c < BS ? c : c < 2 * BS ? c - BS : c < 3 * BS ? c - 2 * BS : 0;
       const int d2 = cc / M, m2 = cc % M;
+      const double r0 = is_zero(role), r1 = is_zero(role - 1), r2 = is_zero(role - 2);
       {
         const double* Pd = sm + L->Pd + a * M * M;
         const double* Po = sm + L->Po + (a < nv - 1 ? a : 0) * M * M;
+        double ind[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) ind[d] = is_zero(d - d2);
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const double pd = Pd[m * M + m2], po = Po[m * M + m2];
-          const double v = role == 0 ? pd : role == 2 ? po : 0.0;
+          const double v = Pd[m * M + m2] * r0 + Po[m * M + m2] * r2;
 #pragma unroll
-          for (int d = 0; d < 3; ++d) col[d * M + m] = (d == d2) ? v : 0.0;
+          for (int d = 0; d < 3; ++d) col[d * M + m] = v * ind[d];
         }
-        if (role == 1) {
 #pragma unroll
-          for (int i = 0; i < BS; ++i) col[i] = (i == cc) ? 1.0 : 0.0;
-        }
+        for (int i = 0; i < BS; ++i) col[i] += r1 * is_zero(i - cc);
       }
       MTG_TACC(220, tf);
       if (with_constraints) {
@@ -463,8 +470,8 @@ struct Tube {
         // segment u, j = 0..M-1) of G[d][d2] beta[m] beta[m2]; lanes of
         // role != 0 accumulate zeros.  Loads of control point q+1 are issued
         // before the arithmetic of q (sched barriers keep them there).
-        const double on = role == 0 ? 1.0 : 0.0;
-        double bt[M], g3[3], bt2[M], g32[3];
+        const double on = r0;
+        double bt[M], g3[3], bt2[M], g32[3], bm, bm_n = 0.0;
         auto load_cp = [&](int q, double* b, double* g) {
           const int i = q < M ? u - 1 : u;
           const int j = q < M ? q + M : q - M;
@@ -473,16 +480,14 @@ struct Tube {
           for (int m = 0; m < M; ++m) b[m] = sm[L->bet + cpi * M + m];
 #pragma unroll
           for (int d = 0; d < 3; ++d) g[d] = Gcp[cpi * 9 + d * 3 + d2];
+          return sm[L->bet + cpi * M + m2];
         };
-        load_cp(0, bt, g3);
+        bm = load_cp(0, bt, g3);
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-          if (q + 1 < N) load_cp(q + 1, bt2, g32);
+          if (q + 1 < N) bm_n = load_cp(q + 1, bt2, g32);
           __builtin_amdgcn_sched_barrier(0);
-          double bm2 = bt[0];
-#pragma unroll
-          for (int m = 1; m < M; ++m) bm2 = (m == m2) ? bt[m] : bm2;
-          bm2 *= on;
+          const double bm2 = bm * on;
 #pragma unroll
           for (int d = 0; d < 3; ++d) {
             const double gd = g3[d] * bm2;
@@ -494,6 +499,7 @@ struct Tube {
           for (int m = 0; m < M; ++m) bt[m] = bt2[m];
 #pragma unroll
           for (int d = 0; d < 3; ++d) g3[d] = g32[d];
+          bm = bm_n;
         }
       }
       MTG_TACC(221, tf);
@@ -502,7 +508,7 @@ struct Tube {
         // t+1 is loaded while row t is applied.
         const double* Wp = sm + L->W + (a - 1) * BS * BS;
         const double* dp = sm + L->dinv + (a - 1) * BS;
-        const double on = role == 0 ? 1.0 : 0.0;
+        const double on = r0;
         double wr[BS], wn[BS], wc, dt, wcn = 0.0, dtn = 0.0;
 #pragma unroll
         for (int i = 0; i < BS; ++i) wr[i] = Wp[i];
@@ -530,28 +536,32 @@ struct Tube {
       // Forward elimination (below the pivot) on all columns at once; the
       // pivot column is broadcast with v_readlane.
       MTG_TACC(222, tf);
-      double dj_own = 0.0;  // pivot j, kept by lane j
+      double pmin = 1.0;
 #pragma unroll
       for (int j = 0; j < BS; ++j) {
         const double piv = bcast(col[j], j);
-        bad |= !(piv > 0.0);
-        dj_own = lane == j ? piv : dj_own;
+        pmin = fmin(pmin, piv);
         if (j == BS - 1) break;
         const double f = col[j] * rcp64(piv > 0.0 ? piv : 1.0);
 #pragma unroll
         for (int i = j + 1; i < BS; ++i) col[i] = fma(-bcast(col[i], j), f, col[i]);
       }
+      bad |= !(pmin > 0.0);
       MTG_TACC(223, tf);
-      // Lanes BS.. store L_a^-1 columns, lanes 2BS.. W_a columns, the rest
-      // write into the scratch column `tmp` (same instruction stream).
+      // Lanes 0.. store U columns (scratch: the pivots), BS.. L_a^-1 columns,
+      // 2BS.. W_a columns; idle lanes write one dummy slot.
       {
-        const bool keep = role == 1 || role == 2;
-        double* dst = keep ? sm + (role == 1 ? L->Li : L->W) + a * BS * BS + cc
-                           : sm + L->tmp;
-        const int stride = keep ? BS : 0;
+        const int base = role == 0 ? L->tmp : role == 1 ? L->Li + a * BS * BS
+                       : role == 2 ? L->W + a * BS * BS : L->tmp + BS * BS;
+        const int stride = role == 3 ? 0 : BS;
+        double* dst = sm + base + (role == 3 ? 0 : cc);
 #pragma unroll
         for (int i = 0; i < BS; ++i) dst[i * stride] = col[i];
-        if (c < BS) sm[L->dinv + a * BS + c] = rcp64(dj_own > 0.0 ? dj_own : 1.0);
+      }
+      __syncthreads();
+      if (c < BS) {
+        const double p = sm[L->tmp + c * BS + c];
+        sm[L->dinv + a * BS + c] = rcp64(p > 0.0 ? p : 1.0);
       }
       __syncthreads();
       MTG_TACC(224, tf);
@@ -559,52 +569,71 @@ struct Tube {
     if (bad && lane == 0) *fail = 1;
   }
 
-  // Solve K out = rhs with the block factors (rhs overwritten by y):
-  // forward y_a = L_a^-1 (rhs_a - W_{a-1}^T D_{a-1}^-1 y_{a-1}), backward
-  // out_a = L_a^-T D_a^-1 (y_a - W_a out_{a+1}).
+  // Solve K out = rhs with the block factors (rhs overwritten by y).
+  // Lanes 0..BS-1 own one row each; matrix rows are loaded before the
+  // values of the recurrence (sched barriers keep them there).  L_a^-1 is
+  // stored with exact zeros above the diagonal, so full-length sums equal
+  // the triangular ones.
   __device__ void solve(int rhs_off, int out_off) {
     double* tmp = sm + L->tmp;
     double* y = sm + rhs_off;
     double* xo = sm + out_off;
+    const bool act = lane < BS;
+    const int i = act ? lane : 0;
     for (int a = 0; a < nv; ++a) {
-      if (lane < BS) {
-        double t = y[a * BS + lane];
-        if (a > 0) {
-          const double* Wp = sm + L->W + (a - 1) * BS * BS;
-          const double* dp = sm + L->dinv + (a - 1) * BS;
+      double wc[BS], dpv[BS], lr[BS], v1[BS];
+      const double* Wp = sm + L->W + (a > 0 ? a - 1 : 0) * BS * BS;
+      const double* dp = sm + L->dinv + (a > 0 ? a - 1 : 0) * BS;
+      const double* Li = sm + L->Li + a * BS * BS;
 #pragma unroll
-          for (int k = 0; k < BS; ++k) t -= Wp[k * BS + lane] * dp[k] * y[(a - 1) * BS + k];
-        }
-        tmp[lane] = t;
+      for (int k = 0; k < BS; ++k) wc[k] = Wp[k * BS + i];
+#pragma unroll
+      for (int k = 0; k < BS; ++k) dpv[k] = dp[k];
+#pragma unroll
+      for (int k = 0; k < BS; ++k) lr[k] = Li[i * BS + k];
+      double t = y[a * BS + i];
+#pragma unroll
+      for (int k = 0; k < BS; ++k) v1[k] = y[(a > 0 ? a - 1 : 0) * BS + k];
+      __builtin_amdgcn_sched_barrier(0);
+      if (a > 0) {
+#pragma unroll
+        for (int k = 0; k < BS; ++k) t -= wc[k] * dpv[k] * v1[k];
       }
+      if (act) tmp[i] = t;
       __syncthreads();
-      if (lane < BS) {
-        const double* Li = sm + L->Li + a * BS * BS + lane * BS;
-        double v = 0.0;
 #pragma unroll
-        for (int k = 0; k < BS; ++k) v += (k <= lane ? Li[k] : 0.0) * tmp[k];
-        y[a * BS + lane] = v;
-      }
+      for (int k = 0; k < BS; ++k) v1[k] = tmp[k];
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < BS; ++k) v += lr[k] * v1[k];
+      if (act) y[a * BS + i] = v;
       __syncthreads();
     }
     for (int a = nv - 1; a >= 0; --a) {
-      if (lane < BS) {
-        double t = y[a * BS + lane];
-        if (a < nv - 1) {
-          const double* Wa = sm + L->W + a * BS * BS + lane * BS;
+      double wr[BS], lc[BS], v1[BS];
+      const double* Wa = sm + L->W + (a < nv - 1 ? a : 0) * BS * BS;
+      const double* Li = sm + L->Li + a * BS * BS;
 #pragma unroll
-          for (int k = 0; k < BS; ++k) t -= Wa[k] * xo[(a + 1) * BS + k];
-        }
-        tmp[lane] = t * sm[L->dinv + a * BS + lane];
+      for (int k = 0; k < BS; ++k) wr[k] = Wa[i * BS + k];
+#pragma unroll
+      for (int k = 0; k < BS; ++k) lc[k] = Li[k * BS + i];
+      double t = y[a * BS + i];
+      const double di = sm[L->dinv + a * BS + i];
+#pragma unroll
+      for (int k = 0; k < BS; ++k) v1[k] = xo[(a < nv - 1 ? a + 1 : 0) * BS + k];
+      __builtin_amdgcn_sched_barrier(0);
+      if (a < nv - 1) {
+#pragma unroll
+        for (int k = 0; k < BS; ++k) t -= wr[k] * v1[k];
       }
+      if (act) tmp[i] = t * di;
       __syncthreads();
-      if (lane < BS) {
-        const double* Li = sm + L->Li + a * BS * BS;
-        double v = 0.0;
 #pragma unroll
-        for (int k = 0; k < BS; ++k) v += (k >= lane ? Li[k * BS + lane] : 0.0) * tmp[k];
-        xo[a * BS + lane] = v;
-      }
+      for (int k = 0; k < BS; ++k) v1[k] = tmp[k];
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < BS; ++k) v += lc[k] * v1[k];
+      if (act) xo[a * BS + i] = v;
       __syncthreads();
     }
   }
