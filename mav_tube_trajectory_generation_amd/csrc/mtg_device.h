@@ -235,57 +235,47 @@ struct Traj {
     return dv()[(v * M + k) * D + d];
   }
 
-  // Blocks of R in vertex order, b = -R_pf d_f, then pinning.
+  // Blocks of R in vertex order, b = -R_pf d_f, then pinning, in one pass:
+  // lane (v, j) builds row j of D_v and O_v, column j of O_{v-1} and b_v[j]
+  // in registers from rows j and M+j of H(1) (plus column M+j) and the
+  // powers of segments v-1 and v, then writes the pinned rows.
   __device__ void assemble() {
     double* Dt = sm + lay->Dt;
     double* Ot = sm + lay->Ot;
     double* Bt = sm + lay->Bt;
-#pragma unroll 2
-    for (int i = lane; i < (S + 1) * M * M; i += kWave) {
-      const int v = i / (M * M);
-      const int j = (i / M) % M, k = i % M;
-      double val = 0.0;
-      if (v > 0) val += H(v - 1, 1, 1, j, k);
-      if (v < S) {
-        val += H(v, 0, 0, j, k);
-        Ot[i] = H(v, 0, 1, j, k);
+    const double* tH = tabH();
+    for (int row = lane; row < (S + 1) * M; row += kWave) {
+      const int v = row / M, j = row % M;
+      const double fl = v > 0 ? 1.0 : 0.0, fr = v < S ? 1.0 : 0.0;
+      const int sl = v > 0 ? v - 1 : 0, sr = v < S ? v : S - 1;
+      double Dr[M], Or[M], Oc[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const double pl = pwr(sl, 1 - 2 * r + j + k), pr = pwr(sr, 1 - 2 * r + j + k);
+        Dr[k] = fl * (tH[(M + j) * N + M + k] * pl) + fr * (tH[j * N + k] * pr);  // H(v-1,1,1)+H(v,0,0)
+        Or[k] = fr * (tH[j * N + M + k] * pr);                                    // H(v,0,1)[j][k]
+        Oc[k] = fl * (tH[k * N + M + j] * pl);                                    // H(v-1,0,1)[k][j]
       }
-      Dt[i] = val;
-    }
-    __syncthreads();
-    // dv is zero at free entries, so these sums run over fixed columns only.
-#pragma unroll 2
-    for (int i = lane; i < (S + 1) * M * D; i += kWave) {
-      const int v = i / (M * D);
-      const int j = (i / D) % M, d = i % D;
-      double val;
-      if (fixed_at(v, j)) {
-        val = dval(v, j, d);
-      } else {
-        const double* Dv = Dt + v * M * M;
+      const int v0 = v > 0 ? v - 1 : 0, v2 = v < S ? v + 1 : S;
+      // dv is zero at free entries: the sums run over fixed columns only.
+      const bool fj = fixed_at(v, j);
+#pragma unroll
+      for (int d = 0; d < kMaxD; ++d) {
+        if (d >= D) break;
         double b = 0.0;
 #pragma unroll
-        for (int k = 0; k < M; ++k) b += Dv[j * M + k] * dval(v, k, d);
-        if (v < S) {
-          const double* Ov = Ot + v * M * M;
-#pragma unroll
-          for (int k = 0; k < M; ++k) b += Ov[j * M + k] * dval(v + 1, k, d);
+        for (int k = 0; k < M; ++k) {
+          b = fma(Dr[k], dval(v, k, d), b);
+          b = fma(Or[k], dval(v2, k, d), b);
+          b = fma(Oc[k], dval(v0, k, d), b);
         }
-        if (v > 0) {
-          const double* Op = Ot + (v - 1) * M * M;
-#pragma unroll
-          for (int k = 0; k < M; ++k) b += Op[k * M + j] * dval(v - 1, k, d);
-        }
-        val = -b;
+        Bt[(v * M + j) * D + d] = fj ? dval(v, j, d) : -b;
       }
-      Bt[i] = val;
-    }
-    __syncthreads();
-    for (int i = lane; i < (S + 1) * M * M; i += kWave) {
-      const int v = i / (M * M);
-      const int j = (i / M) % M, k = i % M;
-      if (fixed_at(v, j) || fixed_at(v, k)) Dt[i] = (j == k) ? 1.0 : 0.0;
-      if (v < S && (fixed_at(v, j) || fixed_at(v + 1, k))) Ot[i] = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        Dt[(v * M + j) * M + k] = (fj || fixed_at(v, k)) ? (j == k ? 1.0 : 0.0) : Dr[k];
+        if (v < S) Ot[(v * M + j) * M + k] = (fj || fixed_at(v + 1, k)) ? 0.0 : Or[k];
+      }
     }
   }
 
