@@ -83,7 +83,8 @@ struct Layout {
   int dv;          // (S+1)*M*D vertex derivatives (fixed values, then x)
   int Dt;          // (S+1)*M*M diagonal blocks -> pinned -> Schur complements
   int Ot;          // S*M*M     coupling blocks -> pinned
-  int Zt;          // S*M*M     Z_v = S_v^-1 O_v
+  int Zt;          // (S+1)*M*M Z_v of the two sweeps (see solve)
+  int Tm;          // M*M       backward sweep's Schur term at the middle vertex
   int Bt;          // (S+1)*M*D right-hand sides -> z_v = S_v^-1 r_v
   int aux;         // 4*S extra (optimiser state)
   int ndouble;
@@ -103,7 +104,8 @@ __host__ __device__ inline Layout make_layout(int N, int S, int D) {
   l.dv = o;   o += (S + 1) * M * D;
   l.Dt = o;   o += (S + 1) * M * M;
   l.Ot = o;   o += S * M * M;
-  l.Zt = o;   o += S * M * M;
+  l.Zt = o;   o += (S + 1) * M * M;
+  l.Tm = o;   o += M * M;
   l.Bt = o;   o += (S + 1) * M * D;
   l.aux = o;  o += 4 * S + 8;
   l.ndouble = o;
@@ -279,7 +281,61 @@ struct Traj {
     }
   }
 
-  // Block LDL^T forward sweep and back substitution.  On exit dv holds every
+  // LDL^T of the M x M block P (row-major, lower triangle) held in registers
+  // (Lr), then x <- P^-1 x.  Lr[i][k] (k < i) ends as L[i][k] * delta_k and
+  // inv[k] = 1 / delta_k.  Returns false on a non-positive pivot.
+  __device__ static bool ldlt(double (&Lr)[M][M], double (&inv)[M]) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double dj = Lr[j][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) dj -= Lr[j][k] * (Lr[j][k] * inv[k]);
+      ok = ok && (dj > 0.0);
+      inv[j] = rcp64(dj > 0.0 ? dj : 1.0);
+#pragma unroll
+      for (int i = j + 1; i < M; ++i) {
+        double s = Lr[i][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= Lr[i][k] * (Lr[j][k] * inv[k]);
+        Lr[i][j] = s;
+      }
+    }
+    return ok;
+  }
+  __device__ static void ldlt_apply(const double (&Lr)[M][M], const double (&inv)[M],
+                                    double (&x)[M]) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      double s = x[i];
+#pragma unroll
+      for (int k = 0; k < i; ++k) s -= (Lr[i][k] * inv[k]) * x[k];
+      x[i] = s;
+    }
+#pragma unroll
+    for (int i = M - 1; i >= 0; --i) {
+      double s = x[i] * inv[i];
+#pragma unroll
+      for (int k = i + 1; k < M; ++k) s -= (Lr[k][i] * inv[i]) * x[k];
+      x[i] = s;
+    }
+  }
+
+  // Twisted block LDL^T: two sweeps run at once and meet at the middle
+  // vertex mid = (S+1)/2.  Lanes 0..31 sweep forward over v = 0..mid-1,
+  // lanes 32..63 backward over v = S..mid+1 (the same recurrence on the
+  // reversed chain, whose couplings are the transposed blocks: the two
+  // groups run one instruction stream with per-lane addresses and strides).
+  // In a group, lane c < M owns column c of the coupling block, lane M + d
+  // right-hand side d.  Per step each active lane reads the Schur complement
+  // S_v, factors it in registers and maps its column: Z_v[:, c] =
+  // S_v^-1 P[:, c] (P = coupling to the next vertex of the sweep) or
+  // z_v = S_v^-1 (b_v - Q^T z_prev) (Q = coupling from the previous one;
+  // z_prev stays in registers); the coupling lanes then write column c of the
+  // next Schur complement, S_next[:, c] = D_next[:, c] - P^T Z_v[:, c].  The
+  // middle vertex combines both sweeps; back substitution
+  // x_v = z_v - Z_v x_(toward mid) runs outward from it, both halves at once.
+  // Fully fixed vertices skip the factorisation.  On exit dv holds every
   // vertex derivative (fixed values untouched).  flag()[0] |= 2 on a
   // non-positive pivot.
   __device__ void solve() {
@@ -287,121 +343,160 @@ struct Traj {
     double* Ot = sm + lay->Ot;
     double* Zt = sm + lay->Zt;
     double* Bt = sm + lay->Bt;
+    double* Tm = sm + lay->Tm;
+    constexpr int MM = M * M;
     assemble();
+    for (int i = lane; i < MM; i += kWave) Tm[i] = 0.0;
     __syncthreads();
     MTG_STAMP(3);
-    for (int v = 0; v <= S; ++v) {
-      double* Sv = Dt + v * M * M;
-      double* Rv = Bt + v * M * D;
-      if (vertex_fixed(v)) {
-        // Identity block: z_v = values (already in Bt), Z_v = 0 (pinned rows).
-        if (v < S)
-          for (int i = lane; i < M * M; i += kWave) Zt[v * M * M + i] = 0.0;
-        __syncthreads();
-        MTG_STAMP(100 + 2 * v);
-        MTG_STAMP(101 + 2 * v);
-        continue;
-      }
-      if (v > 0) {
-        // Schur step: S_v -= O_{v-1}^T Z_{v-1},  r_v -= O_{v-1}^T z_{v-1}.
-        const double* Op = Ot + (v - 1) * M * M;
-        const double* Zp = Zt + (v - 1) * M * M;
-        const double* zp = Bt + (v - 1) * M * D;
-        if (lane < M * M) {
-          const int j = lane / M, k = lane % M;
-          double s = Sv[lane];
+    const int mid = (S + 1) / 2;
+    const int grp = lane >> 5, gl = lane & 31;
+    const bool zl = gl < M;                    // coupling-column lane
+    const bool rl = gl >= M && gl < M + D;     // right-hand-side lane
+    const int c = zl ? gl : 0;
+    const int d = rl ? gl - M : 0;
+    const int nsteps = grp == 0 ? mid : S - mid;
+    const int kmax = mid > S - mid ? mid : S - mid;
+    double zprev[M];
 #pragma unroll
-          for (int m = 0; m < M; ++m) s -= Op[m * M + j] * Zp[m * M + k];
-          Sv[lane] = s;
-        } else if (lane < M * M + M * D) {
-          const int idx = lane - M * M;
-          const int j = idx / D, d = idx % D;
-          double s = Rv[idx];
+    for (int i = 0; i < M; ++i) zprev[i] = 0.0;
+    bool ok = true;
+    for (int k = 0; k < kmax; ++k) {
+      MTG_STAMP(100 + 2 * k);
+      const bool act = k < nsteps && (zl || rl);
+      // Vertex of this step and its neighbours along the sweep.
+      const int v = grp == 0 ? k : S - k;
+      const int vn = grp == 0 ? v + 1 : v - 1;       // next (toward mid)
+      const int vp = grp == 0 ? v - 1 : v + 1;       // previous
+      const bool has_prev = k > 0;
+      // P = coupling v -> vn, Q = coupling vp -> v, as (base, row stride,
+      // column stride) views of the stored O blocks (row-major O_u = u -> u+1).
+      const int pb = (grp == 0 ? v : vn) * MM, qb = (grp == 0 ? (k > 0 ? vp : 0) : v) * MM;
+      const int rs = grp == 0 ? M : 1, cs = grp == 0 ? 1 : M;
+      const bool fixed = act && vertex_fixed(v);
+      if (act && fixed) {
+        // Identity block: z_v = b_v (the fixed values), Z_v = 0, no Schur term.
+        if (rl) {
 #pragma unroll
-          for (int m = 0; m < M; ++m) s -= Op[m * M + j] * zp[m * D + d];
-          Rv[idx] = s;
+          for (int i = 0; i < M; ++i) zprev[i] = Bt[(v * M + i) * D + d];
         }
-        __syncthreads();
-      }
-      MTG_STAMP(100 + 2 * v);
-      // Lane -> column: 0..M-1 the coupling block (absent at v = S), then
-      // the D right-hand sides.  Each active lane factors S_v = L Delta L^T
-      // in registers (redundantly) and maps its column c to S_v^-1 c.
-      int col;
-      if (v < S)
-        col = lane < M + D ? lane : -1;
-      else
-        col = lane < D ? M + lane : -1;
-      if (col >= 0) {
-        double Lr[M][M];
-        double inv[M];
+        if (zl) {
+#pragma unroll
+          for (int i = 0; i < M; ++i) Zt[v * MM + i * M + c] = 0.0;
+        }
+      } else if (act) {
+        double Lr[M][M], inv[M], x[M], Pc[M][M], dn[M];
 #pragma unroll
         for (int i = 0; i < M; ++i)
 #pragma unroll
-          for (int j = 0; j <= i; ++j) Lr[i][j] = Sv[i * M + j];
-        const bool isW = col < M;
-        double x[M];
+          for (int j = 0; j <= i; ++j) Lr[i][j] = Dt[v * MM + i * M + j];
+        // Coupling lanes need P (next), rhs lanes Q (previous).
+        const int ob = zl ? pb : qb;
 #pragma unroll
         for (int i = 0; i < M; ++i)
-          x[i] = isW ? Ot[v * M * M + i * M + col] : Rv[i * D + (col - M)];
-        bool ok = true;
 #pragma unroll
-        for (int j = 0; j < M; ++j) {
-          // Lr[i][k] for k < j holds L[i][k] * delta_k (scaled column).
-          double dj = Lr[j][j];
-#pragma unroll
-          for (int k = 0; k < j; ++k) dj -= Lr[j][k] * (Lr[j][k] * inv[k]);
-          ok = ok && (dj > 0.0);
-          inv[j] = rcp64(dj > 0.0 ? dj : 1.0);
-#pragma unroll
-          for (int i = j + 1; i < M; ++i) {
-            double s = Lr[i][j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) s -= Lr[i][k] * (Lr[j][k] * inv[k]);
-            Lr[i][j] = s;  // = L[i][j] * delta_j
-          }
-        }
-        if (!ok) atomicOr(&flag()[0], 2);
-        // x <- L^-1 x (unit lower, L[i][k] = Lr[i][k] inv[k]) ...
+          for (int j = 0; j < M; ++j) Pc[i][j] = Ot[ob + i * rs + j * cs];
 #pragma unroll
         for (int i = 0; i < M; ++i) {
-          double s = x[i];
-#pragma unroll
-          for (int k = 0; k < i; ++k) s -= (Lr[i][k] * inv[k]) * x[k];
-          x[i] = s;
+          x[i] = zl ? Ot[pb + i * rs + c * cs] : Bt[(v * M + i) * D + d];
+          dn[i] = Dt[(vn == mid && grp == 1 ? 0 : vn * MM) + i * M + c];
         }
-        // ... then x <- L^-T Delta^-1 x.
+        // Trailing mid for the backward sweep: its term goes to Tm, not D.
+        __builtin_amdgcn_sched_barrier(0);
+        if (rl && has_prev) {
 #pragma unroll
-        for (int i = M - 1; i >= 0; --i) {
-          double s = x[i] * inv[i];
+          for (int i = 0; i < M; ++i) {
+            double s = x[i];
 #pragma unroll
-          for (int k = i + 1; k < M; ++k) s -= (Lr[k][i] * inv[i]) * x[k];
-          x[i] = s;
+            for (int m = 0; m < M; ++m) s -= Pc[m][i] * zprev[m];
+            x[i] = s;
+          }
         }
-        if (isW) {
+        ok = ldlt(Lr, inv) && ok;
+        ldlt_apply(Lr, inv, x);
+        if (rl) {
 #pragma unroll
-          for (int i = 0; i < M; ++i) Zt[v * M * M + i * M + col] = x[i];
-        } else {
+          for (int i = 0; i < M; ++i) {
+            zprev[i] = x[i];
+            Bt[(v * M + i) * D + d] = x[i];
+          }
+        }
+        if (zl) {
 #pragma unroll
-          for (int i = 0; i < M; ++i) Rv[i * D + (col - M)] = x[i];
+          for (int i = 0; i < M; ++i) Zt[v * MM + i * M + c] = x[i];
+          if (!vertex_fixed(vn)) {
+            // S_next[:, c] = D_next[:, c] - P^T Z_v[:, c]; the backward
+            // sweep's term at the middle is kept apart in Tm.
+            const bool to_tm = grp == 1 && vn == mid;
+#pragma unroll
+            for (int i = 0; i < M; ++i) {
+              double u = 0.0;
+#pragma unroll
+              for (int m = 0; m < M; ++m) u += Pc[m][i] * x[m];
+              if (to_tm)
+                Tm[i * M + c] = u;
+              else
+                Dt[vn * MM + i * M + c] = dn[i] - u;
+            }
+          }
         }
       }
       __syncthreads();
-      MTG_STAMP(101 + 2 * v);
+      MTG_STAMP(101 + 2 * k);
     }
-    MTG_STAMP(4);
-    // Back substitution x_v = z_v - Z_v x_{v+1}, lanes over (i, d).
-    for (int v = S; v >= 0; --v) {
-      if (lane < M * D) {
-        const int i = lane / D, d = lane % D;
-        if (!fixed_at(v, i)) {
-          double s = Bt[v * M * D + lane];
-          if (v < S) {
-            const double* Zv = Zt + v * M * M;
+    // Middle vertex: S_mid = D_mid (with the forward term) - Tm,
+    // r_mid = b_mid - O_{mid-1}^T z_{mid-1} - O_mid z'_{mid+1}.
+    if (!vertex_fixed(mid) && grp == 0 && (zl || rl)) {
+      double Lr[M][M], inv[M], x[M];
 #pragma unroll
-            for (int k = 0; k < M; ++k) s -= Zv[i * M + k] * dval(v + 1, k, d);
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) Lr[i][j] = Dt[mid * MM + i * M + j] - Tm[i * M + j];
+      if (rl) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          double s = Bt[(mid * M + i) * D + d];
+          if (mid > 0) {
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+              s -= Ot[(mid - 1) * MM + m * M + i] * Bt[((mid - 1) * M + m) * D + d];
           }
-          dv()[(v * M + i) * D + d] = s;
+          if (mid < S) {
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+              s -= Ot[mid * MM + i * M + m] * Bt[((mid + 1) * M + m) * D + d];
+          }
+          x[i] = s;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < M; ++i) x[i] = 0.0;
+      }
+      ok = ldlt(Lr, inv) && ok;
+      ldlt_apply(Lr, inv, x);
+      if (rl) {
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          if (!fixed_at(mid, i)) dv()[(mid * M + i) * D + d] = x[i];
+      }
+    }
+    if (!ok) atomicOr(&flag()[0], 2);
+    __syncthreads();
+    MTG_STAMP(4);
+    // Back substitution outward from the middle, lanes (i, d) per group:
+    // x_v = z_v - Z_v x_(v toward mid).
+    for (int k = 0; k < kmax; ++k) {
+      const int nst = grp == 0 ? mid : S - mid;
+      if (k < nst && gl < M * D) {
+        const int v = grp == 0 ? mid - 1 - k : mid + 1 + k;
+        const int vt = grp == 0 ? v + 1 : v - 1;
+        const int i = gl / D, dd = gl % D;
+        if (!fixed_at(v, i)) {
+          double s = Bt[(v * M + i) * D + dd];
+          const double* Zv = Zt + v * MM;
+#pragma unroll
+          for (int m = 0; m < M; ++m) s -= Zv[i * M + m] * dval(vt, m, dd);
+          dv()[(v * M + i) * D + dd] = s;
         }
       }
       __syncthreads();

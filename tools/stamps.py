@@ -32,22 +32,23 @@ def main():
         st = (ctypes.c_ulonglong * 512)()
         L.mtg_debug_stamps(st, 512)
         runs.append(np.array(st[:], dtype=np.int64))
+        L.mtg_debug_stamps_clear() if hasattr(L, 'mtg_debug_stamps_clear') else None
     st = np.median(np.array(runs), axis=0)
     t0 = st[0]
-    names = {0: "start", 1: "loaded", 2: "powers", 3: "assembled", 4: "swept", 5: "backsub",
-             6: "end"}
     print("phase cycles (workgroup 0, median of 5):")
-    prev = t0
-    for k in (1, 2, 3):
-        print(f"  {names[k]:>10}: {st[k] - prev:8.0f}")
-        prev = st[k]
-    for v in range(S + 1):
-        a, b = st[100 + 2 * v], st[101 + 2 * v]
-        print(f"  vertex {v:2d}: schur {a - prev:6.0f}  factor+solve {b - a:6.0f}")
+    print(f"  {'loaded':>22}: {st[1] - t0:8.0f}")
+    print(f"  {'powers':>22}: {st[2] - st[1]:8.0f}")
+    print(f"  {'assembled':>22}: {st[3] - st[2]:8.0f}")
+    prev = st[3]
+    k = 0
+    while st[100 + 2 * k] > 0 and 100 + 2 * k < 500:  # sweep steps (both ends at once)
+        a, b = st[100 + 2 * k], st[101 + 2 * k]
+        print(f"  {'sweep step ' + str(k):>22}: {b - prev:8.0f}")
         prev = b
-    for k in (4, 5, 6):
-        print(f"  {names[k]:>10}: {st[k] - prev:8.0f}")
-        prev = st[k]
+        k += 1
+    print(f"  {'middle vertex':>22}: {st[4] - prev:8.0f}")
+    print(f"  {'back substitution':>22}: {st[5] - st[4]:8.0f}")
+    print(f"  {'coeffs+cost+store':>22}: {st[6] - st[5]:8.0f}")
     print(f"  total: {st[6] - t0:.0f} cycles")
 
 
