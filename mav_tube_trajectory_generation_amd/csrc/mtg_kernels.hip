@@ -159,45 +159,40 @@ __device__ double objective_at(Traj<N>& t, const double* __restrict__ tab,
   return J + tot * tot * time_penalty;
 }
 
-// Central-difference gradient of the re-solved objective (grad_mode 2) or the
-// reference's getCostAndGradientTime (grad_mode 1).  T() holds the base
-// times; on exit T() is restored and dv holds the solution at the base times
-// only for grad_mode 1.  Gradient written to g (LDS, S entries).
+// The reference's getCostAndGradientTime (grad_mode 1): with d held at the
+// base solution (dv), J_d(T') differs from J_d(T) only in segment n's block
+// (nonlinear_impl:2495-2584).  No re-solve.  Gradient written to g (LDS).
 template <int N>
-__device__ void gradient_at(Traj<N>& t, const double* __restrict__ tab,
-                            const mtg_time_params& p, double* g) {
-  const int S = t.S;
+__device__ void gradient_fixed_d(Traj<N>& t, const mtg_time_params& p, double* g) {
   const double inc = p.increment;
-  if (p.grad_mode == 1) {
-    // J_d(T') with d fixed differs from J_d(T) only in segment n's block.
-    for (int n = 0; n < S; ++n) {
-      const double Tn = t.T()[n];
-      const double ts = Tn <= 0.1 ? 0.1 : Tn - inc;  // nonlinear_impl:2529-2530
-      const double tb = Tn <= 0.1 ? 0.1 : Tn + inc;
-      const double qs = t.seg_energy_at(n, ts);
-      const double qb = t.seg_energy_at(n, tb);
-      if (t.lane == 0) g[n] = p.w_d * (qb - qs) / (2.0 * inc) + p.w_t * 1.0;
-    }
-    __syncthreads();
-    return;
-  }
-  for (int n = 0; n < S; ++n) {
+  for (int n = 0; n < t.S; ++n) {
     const double Tn = t.T()[n];
-    const double ts = Tn <= 0.1 ? 0.1 : Tn - inc;
+    const double ts = Tn <= 0.1 ? 0.1 : Tn - inc;  // nonlinear_impl:2529-2530
     const double tb = Tn <= 0.1 ? 0.1 : Tn + inc;
-    __syncthreads();
-    if (t.lane == 0) t.T()[n] = ts;
-    const double Js = objective_at(t, tab, p.time_penalty);
-    if (t.lane == 0) t.T()[n] = tb;
-    const double Jb = objective_at(t, tab, p.time_penalty);
-    if (t.lane == 0) {
-      t.T()[n] = Tn;
-      g[n] = (Jb - Js) / (2.0 * inc);
-    }
+    const double qs = t.seg_energy_at(n, ts);
+    const double qb = t.seg_energy_at(n, tb);
+    if (t.lane == 0) g[n] = p.w_d * (qb - qs) / (2.0 * inc) + p.w_t * 1.0;
   }
   __syncthreads();
 }
 
+// Central-difference point of gradient step gi (0 .. 2S-1) around base
+// times Tb: segment n = gi / 2 at T_n - inc (even gi) or T_n + inc (odd),
+// both clamped to 0.1 when T_n <= 0.1 (nonlinear_impl:2529-2530).
+template <int N>
+__device__ void set_fd_point(Traj<N>& t, const double* Tb, int gi, double inc) {
+  const int n = gi >> 1;
+  if (t.lane == 0) {
+    for (int i = 0; i < t.S; ++i) t.T()[i] = Tb[i];
+    const double Tn = Tb[n];
+    t.T()[n] = Tn <= 0.1 ? 0.1 : ((gi & 1) ? Tn + inc : Tn - inc);
+  }
+  __syncthreads();
+}
+
+// Every objective evaluation of the two kernels below goes through ONE call
+// site of objective_at (a loop over evaluation points), so the solver body
+// is instantiated once per kernel and stays within the register file.
 template <int N>
 __global__ __launch_bounds__(kWave) void time_cost_kernel(
     PlanDev pl, const double* __restrict__ fixed_vals, const double* __restrict__ times,
@@ -210,14 +205,32 @@ __global__ __launch_bounds__(kWave) void time_cost_kernel(
   Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
             static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
   const int64_t b = blockIdx.x;
+  double* g = smem + lay.aux;   // gradient
+  double* Tb = g + S;           // base times
   t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times + b * S, fixed_vals + b * D * nf, nf);
-  const double J = objective_at(t, tab, p.time_penalty);
-  const int fl = t.flag()[0];
-  double* g = smem + lay.aux;
-  if (grad && p.grad_mode != 0 && !(fl & 1)) gradient_at(t, tab, p, g);
+  for (int i = t.lane; i < S; i += kWave) Tb[i] = times[b * S + i];
+  const bool fd = grad && p.grad_mode == 2;
+  const int nevals = 1 + (fd ? 2 * S : 0);
+  double J0 = 0.0, Jlo = 0.0;
+  int fl = 0;
+  for (int e = 0; e < nevals; ++e) {
+    if (e > 0) set_fd_point(t, Tb, e - 1, p.increment);
+    const double J = objective_at(t, tab, p.time_penalty);
+    if (e == 0) {
+      J0 = J;
+      fl = t.flag()[0];
+      if (fl & 1) break;
+    } else if ((e - 1) & 1) {
+      if (t.lane == 0) g[(e - 1) >> 1] = (J - Jlo) / (2.0 * p.increment);
+    } else {
+      Jlo = J;
+    }
+  }
+  __syncthreads();
+  if (grad && p.grad_mode == 1 && !(fl & 1)) gradient_fixed_d(t, p, g);
   const int fl2 = t.flag()[0];
   if (t.lane == 0) {
-    if (cost) cost[b] = (fl & 1) ? NAN : J;
+    if (cost) cost[b] = (fl & 1) ? NAN : J0;
     if (status)
       status[b] = (fl2 & 1) ? MTG_TRAJ_BAD_TIME
                             : ((fl2 & 2) ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
@@ -230,7 +243,9 @@ __global__ __launch_bounds__(kWave) void time_cost_kernel(
 // Batched segment-time optimisation (optimizeTime, nonlinear_impl:332-397):
 // bounds [0.1, 2 T0]; projected, scaled steepest descent on the grad_mode 2
 // gradient with an expand/backtrack step rule; `max_evals` objective
-// evaluations (NLopt maxeval semantics, nonlinear_impl:101).
+// evaluations (NLopt maxeval semantics, nonlinear_impl:101; gradient
+// evaluations are not counted).  Written as a state machine with one
+// objective evaluation per loop trip.
 template <int N>
 __global__ __launch_bounds__(kWave) void time_optimize_kernel(
     PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ times_io,
@@ -252,22 +267,52 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
     Tcur[i] = v;
     T0[i] = v;
   }
-  mtg_time_params pg = p;
-  pg.grad_mode = 2;
-  double f = objective_at(t, tab, p.time_penalty);
-  int evals = 1;
-  int fl = t.flag()[0];
-  if (!(fl & 1)) {
-    gradient_at(t, tab, pg, g);
-    double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
-    constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
-    while (evals < max_evals && alpha > 1e-9) {
-      // Scaled direction: -g_n T0_n, normalised so the largest relative
-      // move is alpha.
+  constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
+  enum { kBase, kGrad, kTrial, kDone };
+  int phase = kBase, gi = 0, evals = 0;
+  double f = 0.0, Jlo = 0.0;
+  double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
+  int fl = 0;
+  while (phase != kDone) {
+    const double J = objective_at(t, tab, p.time_penalty);  // at T()
+    if (phase == kBase) {
+      f = J;
+      evals = 1;
+      fl = t.flag()[0];
+      if (fl & 1) break;
+      phase = kGrad;
+      gi = 0;
+    } else if (phase == kGrad) {
+      if (gi & 1) {
+        if (t.lane == 0) g[gi >> 1] = (J - Jlo) / (2.0 * p.increment);
+      } else {
+        Jlo = J;
+      }
+      if (++gi == 2 * S) phase = kTrial;
+    } else {  // trial point
+      ++evals;
+      if (J < f) {
+        f = J;
+        if (t.lane == 0)
+          for (int i = 0; i < S; ++i) Tcur[i] = t.T()[i];
+        alpha = fmin(alpha * 1.5, 1.0);
+        phase = kGrad;
+        gi = 0;
+      } else {
+        alpha *= 0.5;
+      }
+    }
+    __syncthreads();
+    // Next evaluation point.
+    if (phase == kGrad) {
+      set_fd_point(t, Tcur, gi, p.increment);
+    } else if (phase == kTrial) {
+      if (!(evals < max_evals && alpha > 1e-9)) break;
+      // Scaled direction -g_n T0_n, normalised so the largest relative move
+      // is alpha.
       double gmax = 0.0;
       for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(g[i] * T0[i]));
       if (!(gmax > 0.0)) break;
-      __syncthreads();
       int moved = 0;
       for (int i = 0; i < S; ++i) {
         const double step = alpha * T0[i] * (g[i] * T0[i]) / gmax;
@@ -276,22 +321,8 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
         if (tn != Tcur[i]) moved = 1;
         if (t.lane == 0) t.T()[i] = tn;
       }
+      __syncthreads();
       if (!moved) break;
-      const double ft = objective_at(t, tab, p.time_penalty);
-      ++evals;
-      if (ft < f) {
-        f = ft;
-        if (t.lane == 0)
-          for (int i = 0; i < S; ++i) Tcur[i] = t.T()[i];
-        __syncthreads();
-        alpha = fmin(alpha * 1.5, 1.0);
-        gradient_at(t, tab, pg, g);
-      } else {
-        alpha *= 0.5;
-        if (t.lane == 0)
-          for (int i = 0; i < S; ++i) t.T()[i] = Tcur[i];
-        __syncthreads();
-      }
     }
   }
   fl = t.flag()[0];
