@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
     p.add_argument("--segments", type=int, default=10)
-    p.add_argument("--workload", choices=["linear", "time", "tube"], default="linear")
+    p.add_argument("--workload", choices=["linear", "time", "tube", "sample"], default="linear")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph)")
@@ -106,7 +106,7 @@ def main():
 
     N, D, r, S = 10, 3, 4, args.segments
     wl = args.workload
-    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096}[wl]
+    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "sample": 1024}[wl]
     from mav_tube_trajectory_generation_amd.shard import select_best, shard_range
     global_batch = B * world
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
@@ -141,6 +141,27 @@ def main():
         metric = "time-allocation optimisations/sec (4096 traj x 50 evals, 10-seg, N=10, 3D)"
         unit = "trajectories/s"
         units_per_step = B
+    elif wl == "sample":
+        # Sampling of solved trajectories (evaluateRange for derivatives 0..4,
+        # the [t, p, v, a, j, s] rows of printMatlabSampledTrajectory) at
+        # dt = 0.01 (nonlinear_impl:2915); coefficients resident in HBM.
+        sol = plan.solve(fixed_d, times_d, free=False)
+        dt, K = 0.01, 4
+        n_max = (int(float(times_d.sum(dim=1).max().item()) / dt) + 2 + 63) // 64 * 64
+        smp, stm, cnt = mtg.sample_trajectories(sol["coeffs"], times_d, dt, max_derivative=K,
+                                                n_max=n_max)
+        torch.cuda.synchronize(dev)
+        n_total = int(cnt.sum().item())
+
+        def step():
+            return mtg.sample_trajectories(sol["coeffs"], times_d, dt, max_derivative=K,
+                                           n_max=n_max)
+
+        # written: every sample's (K+1) D channels + its time; read: coeffs, times
+        bytes_per_traj = (n_total / B) * ((K + 1) * D + 1) * 8 + (S * D * N + S) * 8
+        metric = "trajectory samples/sec (evaluateRange, dt=0.01, derivatives 0..4, 3D)"
+        unit = "samples/s"
+        units_per_step = n_total
     else:
         radii = torch.full((B, S, 2), 0.15, dtype=torch.float64, device=dev)
         pos_d = torch.from_numpy(pos).to(dev)
@@ -159,12 +180,12 @@ def main():
         unit = "trajectories/s"
         units_per_step = B
 
-    # World 1, linear: the K timed solves are captured into one HIP graph and
+    # World 1: the K timed steps are captured into one HIP graph and
     # replayed, so launches are back to back (no host launch gaps) and the
     # per-launch duration is (end - start) / K from two HIP events on the
     # launch stream.  Otherwise (collective per step, or millisecond kernels)
     # eager launches with one event pair per launch.
-    use_graph = world == 1 and wl == "linear" and not args.no_graph
+    use_graph = world == 1 and not args.no_graph
     if use_graph:
         graphs = {}
         for name, n in (("warmup", args.warmup), ("timed", args.steps)):

@@ -227,6 +227,28 @@ int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                    int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Batched trajectory sampling: Trajectory::evaluateRange (src/trajectory.cpp:
+ * 74-134) for derivatives 0..max_derivative at once (the [t, p, v, a, j, s]
+ * rows of printMatlabSampledTrajectory, nonlinear_impl:2907-3003).
+ * Per trajectory b: samples start in the segment containing t_start, at
+ * time-in-segment t_start - (segment start) + k dt, advancing to the next
+ * segment while the time exceeds the segment time; they run while the
+ * accumulated time (segment start + k dt) is < t_end, and stop at the first
+ * sample past the last segment.  t_end < 0 means the trajectory's total time.
+ * Device pointers: coeffs B x S x D x N (as mtg_linear_solve writes them),
+ * times B x S; outputs samples B x ((max_derivative+1) * D) x n_max
+ * (channel-major: channel = derivative * D + d), sample_times B x n_max (the
+ * accumulated times, nullable), n_samples B (nullable).  Samples beyond
+ * n_max are dropped.  1 <= S <= 64.  An n_max that is a multiple of 64 keeps
+ * every channel row 512-byte aligned (full-line HBM writes).
+ */
+int mtg_sample_trajectories(int N, int D, int S, int64_t B, const double* coeffs,
+                            const double* times, double t_start, double t_end,
+                            double dt, int n_max, int max_derivative,
+                            double* samples, double* sample_times,
+                            int32_t* n_samples, void* stream);
+
+/* ------------------------------------------------------------------------
  * Host-side input generation (vertex.cpp:27-82, 228-269) for batches:
  * trajectory b uses createRandomVertices(max_derivative = M-1, S, +/-pos_bound,
  * seed = seed0 + b) and estimateSegmentTimes(v_max, a_max) (Nfabian, 6.5).

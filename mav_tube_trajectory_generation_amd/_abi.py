@@ -55,6 +55,10 @@ SIGNATURES = {
     "mtg_tube_solve": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_double,
                                       ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mtg_sample_trajectories": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int64, _vp, _vp, ctypes.c_double,
+                                               ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                               ctypes.c_int, _vp, _vp, _vp, _vp]),
     "mtg_generate_random_problems": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                     ctypes.c_int64, ctypes.c_uint64,
                                                     ctypes.c_double, ctypes.c_double,

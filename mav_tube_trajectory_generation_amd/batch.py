@@ -253,3 +253,34 @@ def tube_solve(ctx, N, r, positions, fixed_vals, times_cp, times, radii, tol=1e-
                                _ptr(coeffs), _ptr(cost), _ptr(iters), _ptr(status),
                                _stream(dev)), "mtg_tube_solve")
     return dict(x=x, coeffs=coeffs, cost=cost, iters=iters, status=status)
+
+
+def sample_trajectories(coeffs, times, dt, t_start=0.0, t_end=-1.0, max_derivative=0,
+                        n_max=None, with_times=True):
+    """Batched Trajectory::evaluateRange (trajectory.cpp:74-134) for derivatives
+    0..max_derivative (mtg_sample_trajectories).
+
+    coeffs [B, S, D, N], times [B, S] (float64, CUDA).  Returns (samples
+    [B, (max_derivative+1)*D, n_max] channel-major, sample_times [B, n_max]
+    or None, n_samples [B] int32).  n_max defaults to the longest trajectory's
+    sample count.
+    """
+    import torch
+    B, S, D, N = coeffs.shape
+    _require(coeffs, (B, S, D, N), "coeffs")
+    _require(times, (B, S), "times")
+    dev = times.device
+    if not dt > 0:
+        raise MTGError("dt must be > 0")
+    if n_max is None:
+        span = float(times.sum(dim=1).max().item()) if t_end < 0 else t_end
+        n_max = int(span / dt) + 2
+        n_max = (n_max + 63) // 64 * 64  # 512-byte aligned channel rows
+    nch = (max_derivative + 1) * D
+    samples = torch.empty((B, nch, n_max), dtype=torch.float64, device=dev)
+    stimes = torch.empty((B, n_max), dtype=torch.float64, device=dev) if with_times else None
+    count = torch.empty(B, dtype=torch.int32, device=dev)
+    check(lib().mtg_sample_trajectories(N, D, S, B, _ptr(coeffs), _ptr(times), t_start, t_end,
+                                        dt, n_max, max_derivative, _ptr(samples), _ptr(stimes),
+                                        _ptr(count), _stream(dev)), "mtg_sample_trajectories")
+    return samples, stimes, count

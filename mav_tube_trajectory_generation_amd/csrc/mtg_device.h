@@ -68,6 +68,7 @@ __device__ unsigned long long g_mtg_stamps[512];
   } while (0)
 #define MTG_TACC(slot, last) \
   do {                       \
+    (void)(last);            \
   } while (0)
 #endif
 

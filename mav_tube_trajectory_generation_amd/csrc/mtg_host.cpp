@@ -331,6 +331,21 @@ int mtg_coeffs_from_constraints(const mtg_plan* plan, int64_t B, const double* f
                                                       static_cast<hipStream_t>(stream)));
 }
 
+int mtg_sample_trajectories(int N, int D, int S, int64_t B, const double* coeffs,
+                            const double* times, double t_start, double t_end, double dt,
+                            int n_max, int max_derivative, double* samples,
+                            double* sample_times, int32_t* n_samples, void* stream) {
+  if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > mtg::kMaxSampleS || B < 0 ||
+      B > 65535 || n_max < 0 || max_derivative < 0 || max_derivative >= N || !(dt > 0.0) ||
+      !(t_start >= 0.0))
+    return MTG_ERR_INVALID_ARG;
+  if (B == 0 || n_max == 0) return MTG_OK;
+  if (!coeffs || !times || !samples) return MTG_ERR_INVALID_ARG;
+  return from_hip(mtg::launch_sample(N, D, S, B, coeffs, times, t_start, t_end, dt, n_max,
+                                     max_derivative, samples, sample_times, n_samples,
+                                     static_cast<hipStream_t>(stream)));
+}
+
 int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* times,
                          double* Q, double* A, double* Ainv, double* H, void* stream) {
   if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || n < 0 || (n && !times))

@@ -63,4 +63,11 @@ size_t tube_lds_bytes(int N, int S);
 
 constexpr int kMaxLdsBytes = 160 * 1024;
 
+// Trajectory sampling (mtg_sample.hip).
+constexpr int kMaxSampleS = 64;  // segments staged in LDS per trajectory
+hipError_t launch_sample(int N, int D, int S, int64_t B, const double* coeffs,
+                         const double* times, double t_start, double t_end, double dt,
+                         int n_max, int max_deriv, double* samples, double* sample_times,
+                         int32_t* n_samples, hipStream_t st);
+
 }  // namespace mtg

@@ -1210,6 +1210,59 @@ int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
   return 0;
 }
 
+// Polynomial::evaluate (polynomial.h:135-149): Horner with the derivative
+// row of the base table.
+static double polyEvaluate(int N, const double* c, double t, int derivative) {
+  if (derivative >= N) return 0.0;
+  const Mat& base = baseTable();
+  const int tmp = N - 1;
+  double result = base(derivative, tmp) * c[tmp];
+  for (int i = tmp - 1; i >= derivative; --i) {
+    result *= t;
+    result += base(derivative, i) * c[i];
+  }
+  return result;
+}
+
+// Trajectory::evaluateRange (trajectory.cpp:74-134), statement by statement.
+int orc_evaluate_range(int N, int D, int S, const double* coeffs, const double* times,
+                       double t_start, double t_end, double dt, int derivative,
+                       int max_out, double* out, double* times_out, int* count) {
+  if (N < 1 || D < 1 || S < 1 || !coeffs || !times || !count) return -2;
+  *count = 0;
+  double accumulated_time = 0.0;
+  int i = 0;
+  for (i = 0; i < S; ++i) {
+    accumulated_time += times[i];
+    if (accumulated_time > t_start) break;
+  }
+  if (t_start > accumulated_time) return -1;
+  if (i >= S) i = S - 1;  // (the reference indexes past the end here)
+  accumulated_time -= times[i];
+  double time_in_segment = t_start - accumulated_time;
+  int n = 0;
+  while (accumulated_time < t_end) {
+    if (time_in_segment > times[i]) {
+      time_in_segment = time_in_segment - times[i];
+      i++;
+      if (i >= S) break;
+      continue;
+    }
+    if (n < max_out) {
+      for (int d = 0; d < D; ++d)
+        out[static_cast<size_t>(n) * D + d] =
+            polyEvaluate(N, coeffs + (static_cast<size_t>(i) * D + d) * N, time_in_segment,
+                         derivative);
+      if (times_out) times_out[n] = accumulated_time;
+    }
+    ++n;
+    time_in_segment += dt;
+    accumulated_time += dt;
+  }
+  *count = n;
+  return 0;
+}
+
 int orc_control_point_map(int N, double T, double* Binv) {
   if (N < 2 || N % 2 || N > 12 || !(T > 0) || !Binv) return -1;
   Mat b = setupInverseControlPointMappingMatrix(N, T);

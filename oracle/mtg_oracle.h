@@ -94,6 +94,16 @@ int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
 // (qcqp_impl:267-319), N x N row-major.
 int orc_control_point_map(int N, double T, double* Binv);
 
+// Trajectory::evaluateRange (src/trajectory.cpp:74-134) on the trajectory
+// given by coeffs (S x D x N) and segment times, for one derivative, exactly
+// as the reference iterates (accumulated times by repeated addition).
+// out: max_out x D samples, times_out: max_out (nullable); *count = number
+// of samples the reference would produce (may exceed max_out; only the
+// first max_out are written).  Returns 0, or -1 if t_start is out of range.
+int orc_evaluate_range(int N, int D, int S, const double* coeffs, const double* times,
+                       double t_start, double t_end, double dt, int derivative,
+                       int max_out, double* out, double* times_out, int* count);
+
 // Number of inequality constraints the tube problem builds
 // (qcqp_impl:321-474): (S-1) spheres + S*(N-2) tubes + 2*S*(N-2) half-spaces.
 int orc_tube_num_constraints(int N, int S);

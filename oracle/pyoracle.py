@@ -229,3 +229,23 @@ def tube_solve(N, r, vertices, times, radii, times_cp=None, tol=1e-10, max_iter=
                                    max_iter, _d(x), _d(coeffs), _d(cost), ctypes.byref(iters))
     _check(rc, "tube_solve")
     return dict(x=x, coeffs=coeffs, cost=float(cost[0]), iters=iters.value, status=rc)
+
+
+def evaluate_range(N, coeffs, times, t_start, t_end, dt, derivative, max_out=None):
+    """Trajectory::evaluateRange (trajectory.cpp:74-134) on coeffs [S, D, N]."""
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    S, D, _ = coeffs.shape
+    if max_out is None:
+        max_out = int((t_end if t_end >= 0 else times.sum()) / dt) + 8
+    out = np.zeros((max_out, D))
+    tout = np.zeros(max_out)
+    count = ctypes.c_int()
+    L = lib()
+    L.orc_evaluate_range.argtypes = [ctypes.c_int] * 3 + [_dp, _dp] + [ctypes.c_double] * 3 + [
+        ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.POINTER(ctypes.c_int)]
+    _check(L.orc_evaluate_range(N, D, S, _d(coeffs), _d(times), t_start, t_end, dt, derivative,
+                                max_out, _d(out), _d(tout), ctypes.byref(count)),
+           "evaluate_range")
+    n = min(count.value, max_out)
+    return out[:n], tout[:n], count.value

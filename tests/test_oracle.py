@@ -156,3 +156,51 @@ def test_golden_fixtures(oracle):
         sol = oracle.linear_solve(c["N"], c["r"], oracle.Vertices(mask, vals), t)
         assert rel_err_coeffs(sol["coeffs"], np.array(c["coeffs"])) <= 1e-12, c["name"]
         assert rel_err(sol["cost"], c["cost"]) <= 1e-12, c["name"]
+
+
+def _evaluate_range_py(coeffs, times, t_start, t_end, dt, k):
+    """Independent pure-Python restatement of Trajectory::evaluateRange
+    (trajectory.cpp:74-134) with Polynomial::evaluate (polynomial.h:135-149)."""
+    S, D, N = coeffs.shape
+    acc, i = 0.0, 0
+    for i in range(S):
+        acc += times[i]
+        if acc > t_start:
+            break
+    acc -= times[i]
+    tin = t_start - acc
+    out, ts = [], []
+    while acc < t_end:
+        if tin > times[i]:
+            tin -= times[i]
+            i += 1
+            if i >= S:
+                break
+            continue
+        row = []
+        for d in range(D):
+            c = coeffs[i, d]
+            f = [numpy_ref.falling(k, j) for j in range(N)]
+            v = f[N - 1] * c[N - 1]
+            for j in range(N - 2, k - 1, -1):
+                v = v * tin + f[j] * c[j]
+            row.append(v if k < N else 0.0)
+        out.append(row)
+        ts.append(acc)
+        tin += dt
+        acc += dt
+    return np.array(out), np.array(ts)
+
+
+@pytest.mark.parametrize("k", [0, 1, 4])
+def test_evaluate_range(oracle, k):
+    """orc_evaluate_range against an independent Python loop (bit-exact:
+    same operation order, -ffp-contract=off in the oracle)."""
+    v = oracle.random_vertices(4, 4, 3, -10.0, 10.0, 123)
+    t = oracle.estimate_segment_times(v, 3.0, 5.0)
+    coeffs = oracle.linear_solve(10, 4, v, t)["coeffs"]
+    for t0, t1 in ((0.0, float(t.sum())), (float(t[0]) + 0.21, float(t.sum()) - 0.5)):
+        ref, rt = _evaluate_range_py(coeffs, t, t0, t1, 0.03, k)
+        got, gt, n = oracle.evaluate_range(10, coeffs, t, t0, t1, 0.03, k)
+        assert n == len(ref)
+        assert np.array_equal(got, ref) and np.array_equal(gt, rt)
