@@ -45,32 +45,72 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline_linear(N, D, r, S, seeds, seconds):
-    """Oracle (reference-faithful C++ port, 1 thread) on a bounded sample."""
-    import ctypes
+def _oracle_problems(N, D, S, seeds, tube=False):
+    """Dense vertex form of the bench problems (same generator and seeds as
+    the GPU batch).  tube=True: the tube pattern (positions at every vertex,
+    start/end derivatives fixed to the vertex values, qcqp_impl:48-65)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
-    L = pyoracle.lib()
     K = N // 2
     B = len(seeds)
     masks = np.zeros((B, S + 1, K), np.uint8)
     vals = np.zeros((B, S + 1, K, D))
     times = np.zeros((B, S))
     for i, sd in enumerate(seeds):
-        v = pyoracle.random_vertices(N // 2 - 1, S, D, -10.0, 10.0, int(sd))
+        v = pyoracle.random_vertices(N // 2 - 1, S, D, -10.0, 10.0, int(sd), K=K)
         masks[i], vals[i] = v.mask, v.vals
         times[i] = pyoracle.estimate_segment_times(v, 3.0, 5.0)
-    dp = ctypes.POINTER(ctypes.c_double)
-    L.orc_bench_linear.argtypes = [ctypes.c_int] * 6 + [
-        ctypes.POINTER(ctypes.c_uint8), dp, dp, ctypes.c_int, ctypes.c_double,
-        ctypes.POINTER(ctypes.c_int64), dp]
-    n, sec = ctypes.c_int64(), ctypes.c_double()
-    rc = L.orc_bench_linear(N, D, r, S, K, B, masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
-                            vals.ctypes.data_as(dp), times.ctypes.data_as(dp), 1, seconds,
-                            ctypes.byref(n), ctypes.byref(sec))
-    if rc != 0:
-        raise RuntimeError(f"oracle baseline failed ({rc})")
-    return n.value / sec.value, n.value, B
+    if tube:
+        masks[:] = 0
+        masks[:, :, 0] = 1
+        masks[:, 0, :] = 1
+        masks[:, S, :] = 1
+        pos = vals[:, :, 0, :].copy()
+        vals[:] = 0.0
+        vals[:, :, 0, :] = pos
+    return pyoracle, masks, vals, times
+
+
+def cpu_baseline(wl, N, D, r, S, seconds, sample_args=None):
+    """Oracle (reference-faithful C++ port, 1 thread) on a bounded sample of
+    the same workload.  Returns (rate, units, description)."""
+    import ctypes
+    seeds = range(105, 105 + (256 if wl in ("linear", "sample") else 64))
+    pyoracle, masks, vals, times = _oracle_problems(N, D, S, seeds, tube=(wl == "tube"))
+    K = N // 2
+    B = len(seeds)
+    if wl == "linear":
+        L = pyoracle.lib()
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.orc_bench_linear.argtypes = [ctypes.c_int] * 6 + [
+            ctypes.POINTER(ctypes.c_uint8), dp, dp, ctypes.c_int, ctypes.c_double,
+            ctypes.POINTER(ctypes.c_int64), dp]
+        n, sec = ctypes.c_int64(), ctypes.c_double()
+        rc = L.orc_bench_linear(N, D, r, S, K, B,
+                                masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                vals.ctypes.data_as(dp), times.ctypes.data_as(dp), 1, seconds,
+                                ctypes.byref(n), ctypes.byref(sec))
+        if rc != 0:
+            raise RuntimeError(f"oracle baseline failed ({rc})")
+        units, sec = n.value, sec.value
+        what = "solves (setupFromVertices + solveLinear + computeCost)"
+    elif wl == "time":
+        units, sec = pyoracle.bench_workload(1, N, D, r, S, K, masks, vals, times,
+                                             param_i=50, seconds=seconds)
+        what = "50-evaluation time optimisations (orc_time_optimize)"
+    elif wl == "tube":
+        radii = np.full((B, S, 2), 0.15)
+        units, sec = pyoracle.bench_workload(2, N, D, r, S, K, masks, vals, times, radii=radii,
+                                             seconds=seconds)
+        what = "tube QCQP solves (oracle primal-dual IPM, tol 1e-10)"
+    else:
+        dt, kmax = sample_args
+        units, sec = pyoracle.bench_workload(3, N, D, r, S, K, masks, vals, times, param_i=kmax,
+                                             param_d=dt, seconds=seconds)
+        what = f"samples (evaluateRange, derivatives 0..{kmax}, dt={dt})"
+    desc = (f"{units} {what} cycling over {B} of the same {S}-seg problems "
+            f"(seeds 105..{104 + B}), oracle C++ port, 1 thread, ~{seconds:.0f} s")
+    return units / sec, units, desc
 
 
 def load_pmc_traffic(workload, config_key):
@@ -240,13 +280,10 @@ def main():
 
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1 and wl == "linear":
-            rate, nsolves, sample = cpu_baseline_linear(N, D, r, S, range(105, 105 + 256),
-                                                        args.cpu_seconds)
-            cpu = {"value": rate, "unit": unit, "cores": 1, "kind": "port",
-                   "sample": f"{nsolves} solves cycling over 256 of the same 10-seg problems "
-                             f"(seeds 105..360), oracle C++ port, 1 thread, "
-                             f"~{args.cpu_seconds:.0f} s"}
+        if not args.no_cpu_baseline and world == 1:
+            rate, _, desc = cpu_baseline(wl, N, D, r, S, args.cpu_seconds,
+                                         sample_args=(0.01, 4) if wl == "sample" else None)
+            cpu = {"value": rate, "unit": unit, "cores": 1, "kind": "port", "sample": desc}
         line = {
             "metric": metric,
             "value": value,

@@ -1343,6 +1343,146 @@ int orc_tube_qcqp_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
   return status;
 }
 
+int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                      const double* vals, double* times_io, double time_penalty,
+                      double increment, int max_evals, double* cost, int* evals) {
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times_io, &lp);
+  if (rc) return rc;
+  auto objective = [&](const std::vector<double>& t) {
+    lp.updateSegmentTimes(t);
+    lp.solveLinear();
+    double total = 0.0;
+    for (double v : t) total += v;
+    return lp.computeCost() + total * total * time_penalty;
+  };
+  auto gradient = [&](const std::vector<double>& t, std::vector<double>* g) {
+    for (int n = 0; n < S; ++n) {  // grad_mode 2 of orc_time_cost
+      std::vector<double> ts = t, tb = t;
+      ts[n] = ts[n] <= 0.1 ? 0.1 : ts[n] - increment;
+      tb[n] = tb[n] <= 0.1 ? 0.1 : tb[n] + increment;
+      const double Js = objective(ts);
+      const double Jb = objective(tb);
+      (*g)[n] = (Jb - Js) / (2.0 * increment);
+    }
+  };
+  const std::vector<double> T0(times_io, times_io + S);
+  std::vector<double> T = T0, g(S), trial(S);
+  double f = objective(T);
+  gradient(T, &g);
+  int n_eval = 1;
+  double alpha = 0.1;
+  while (n_eval < max_evals && alpha > 1e-9) {
+    double gmax = 0.0;
+    for (int n = 0; n < S; ++n) gmax = std::max(gmax, std::fabs(g[n] * T0[n]));
+    if (!(gmax > 0.0)) break;
+    bool same = true;
+    for (int n = 0; n < S; ++n) {
+      const double x = T[n] - alpha * T0[n] * (g[n] * T0[n]) / gmax;
+      trial[n] = std::min(std::max(x, 0.1), 2.0 * T0[n]);
+      same = same && trial[n] == T[n];
+    }
+    if (same) break;
+    const double ft = objective(trial);
+    ++n_eval;
+    if (ft < f) {
+      T = trial;
+      f = ft;
+      alpha = std::min(alpha * 1.5, 1.0);
+      gradient(T, &g);
+    } else {
+      alpha *= 0.5;
+    }
+  }
+  std::memcpy(times_io, T.data(), sizeof(double) * S);
+  if (cost) *cost = f;
+  if (evals) *evals = n_eval;
+  return 0;
+}
+
+int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
+                       const uint8_t* masks, const double* vals, const double* times,
+                       const double* radii, int param_i, double param_d, int threads,
+                       double min_seconds, int64_t* units, double* seconds) {
+  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 3) return -1;
+  if (kind == 2 && !radii) return -1;
+  if (kind == 3 && !(param_d > 0.0)) return -1;
+  const size_t mstride = static_cast<size_t>(S + 1) * K;
+  // kind 3: coefficients solved before the clock starts.
+  std::vector<std::vector<double>> coeffs;
+  if (kind == 3) {
+    coeffs.resize(B);
+    for (int b = 0; b < B; ++b) {
+      LinearProblem lp;
+      int rc = setupLinear(N, D, r, S, K, masks + b * mstride, vals + b * mstride * D,
+                           times + static_cast<size_t>(b) * S, &lp);
+      if (!rc) rc = lp.solveLinear();
+      if (rc) return -2;
+      coeffs[b] = lp.coeffs;
+    }
+  }
+  std::atomic<int64_t> total(0);
+  std::atomic<int> failed(0);
+  volatile double sink = 0.0;
+  auto t0 = std::chrono::steady_clock::now();
+  auto worker = [&](int tid) {
+    int64_t n = 0, iters = 0;
+    double acc = 0.0;
+    std::vector<double> out, tout;
+    for (int64_t it = tid;; it += threads) {
+      const int b = static_cast<int>(it % B);
+      const uint8_t* mk = masks + b * mstride;
+      const double* vl = vals + b * mstride * D;
+      const double* tb = times + static_cast<size_t>(b) * S;
+      if (kind == 1) {
+        std::vector<double> t(tb, tb + S);
+        double c = 0.0;
+        int ev = 0;
+        if (orc_time_optimize(N, D, r, S, K, mk, vl, t.data(), 500.0, 0.1, param_i, &c, &ev))
+          failed = 1;
+        acc += c;
+        ++n;
+      } else if (kind == 2) {
+        double c = 0.0;
+        int itn = 0;
+        const int rc = orc_tube_qcqp_solve(N, D, r, S, K, mk, vl, tb, tb,
+                                           radii + static_cast<size_t>(b) * S * 2, 1e-10, 100,
+                                           nullptr, nullptr, &c, &itn);
+        if (rc < 0 && rc != -22) failed = 1;
+        acc += c;
+        ++n;
+      } else {
+        double total_t = 0.0;
+        for (int i = 0; i < S; ++i) total_t += tb[i];
+        const int max_out = static_cast<int>(total_t / param_d) + 8;
+        out.resize(static_cast<size_t>(max_out) * D);
+        tout.resize(max_out);
+        int cnt = 0;
+        for (int dv = 0; dv <= param_i; ++dv) {
+          if (orc_evaluate_range(N, D, S, coeffs[b].data(), tb, 0.0, total_t, param_d, dv,
+                                 max_out, out.data(), tout.data(), &cnt))
+            failed = 1;
+          acc += out[0];
+        }
+        n += cnt;
+      }
+      if ((++iters & 3) == 0) {
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el >= min_seconds) break;
+      }
+    }
+    total += n;
+    sink = sink + acc;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t) pool.emplace_back(worker, t);
+  for (auto& th : pool) th.join();
+  const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (units) *units = total.load();
+  if (seconds) *seconds = el;
+  return failed.load() ? -2 : 0;
+}
+
 int orc_bench_linear(int N, int D, int r, int S, int K, int B, const uint8_t* masks,
                      const double* vals, const double* times, int threads,
                      double min_seconds, int64_t* solves, double* seconds) {

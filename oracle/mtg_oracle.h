@@ -153,6 +153,28 @@ int orc_bench_linear(int N, int D, int r, int S, int K, int B, const uint8_t* ma
                      const double* vals, const double* times, int threads,
                      double min_seconds, int64_t* solves, double* seconds);
 
+// The batched optimiser of mtg_time_optimize (time_optimize_kernel),
+// restated on the oracle objective (objectiveFunctionTime,
+// nonlinear_impl:877-945, with central-difference gradients, grad_mode 2):
+// projected scaled steepest descent in [0.1, 2 T0] (nonlinear_impl:350-378),
+// step x1.5 on success / x0.5 on failure, at most max_evals objective
+// evaluations.  times_io: S (in: T0, out: optimised times).
+int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                      const double* vals, double* times_io, double time_penalty,
+                      double increment, int max_evals, double* cost, int* evals);
+
+// CPU baseline for the other bench workloads, same cycling/threads/timing
+// rules as orc_bench_linear.  kind 1: orc_time_optimize with max_evals =
+// param_i; kind 2: tube QCQP solve (radii: B x S x 2, tol 1e-10, 100
+// iterations); kind 3: evaluateRange for derivatives 0..param_i at
+// dt = param_d over the whole trajectory, on coefficients solved once before
+// the clock starts.  *units = optimisations (1), solves (2), or samples
+// (3, one sample = all derivatives of all dimensions at one time).
+int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
+                       const uint8_t* masks, const double* vals, const double* times,
+                       const double* radii, int param_i, double param_d, int threads,
+                       double min_seconds, int64_t* units, double* seconds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -171,6 +171,44 @@ def time_cost(N, r, vertices, times, time_penalty=500.0, grad_mode=0, increment=
     return float(cost[0]), (grad if grad_mode else None)
 
 
+
+def time_optimize(N, r, vertices, times, max_evals, time_penalty=500.0, increment=0.1):
+    """orc_time_optimize: the mtg_time_optimize algorithm on the oracle
+    objective.  Returns (times, cost, evals)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    t = np.array(times, dtype=np.float64)
+    cost = np.zeros(1)
+    evals = ctypes.c_int()
+    L = lib()
+    L.orc_time_optimize.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, ctypes.c_double,
+                                                         ctypes.c_double, ctypes.c_int, _dp, _ip]
+    _check(L.orc_time_optimize(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                               _d(vertices.vals), _d(t), time_penalty, increment, max_evals,
+                               _d(cost), ctypes.byref(evals)), "time_optimize")
+    return t, float(cost[0]), evals.value
+
+
+def bench_workload(kind, N, D, r, S, K, masks, vals, times, radii=None, param_i=0,
+                   param_d=0.0, threads=1, seconds=10.0):
+    """orc_bench_workload (kind 1 time optimisation, 2 tube, 3 sampling).
+    Returns (units, seconds)."""
+    L = lib()
+    L.orc_bench_workload.argtypes = [ctypes.c_int] * 7 + [_u8p, _dp, _dp, _dp, ctypes.c_int,
+                                                          ctypes.c_double, ctypes.c_int,
+                                                          ctypes.c_double,
+                                                          ctypes.POINTER(ctypes.c_int64), _dp]
+    masks = np.ascontiguousarray(masks, dtype=np.uint8)
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    rad = None if radii is None else np.ascontiguousarray(radii, dtype=np.float64)
+    units = ctypes.c_int64()
+    sec = np.zeros(1)
+    _check(L.orc_bench_workload(kind, N, D, r, S, K, masks.shape[0],
+                                masks.ctypes.data_as(_u8p), _d(vals), _d(times),
+                                _d(rad) if rad is not None else None, param_i, param_d, threads,
+                                seconds, ctypes.byref(units), _d(sec)), "bench_workload")
+    return units.value, float(sec[0])
+
 def control_point_map(N, T):
     B = np.zeros((N, N))
     _check(lib().orc_control_point_map(N, T, _d(B)), "control_point_map")

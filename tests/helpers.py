@@ -99,3 +99,30 @@ def cost_numeric(coeffs, times, r, dt=1e-3):
             vals = (c[r:] * f)[None, :] * ts[:, None] ** (k - r)[None, :]
             total += np.sum(vals.sum(axis=1) ** 2) * dt
     return total
+
+
+def optimize_reference(oracle, N, R, v, t0, max_evals, time_penalty=500.0, inc=0.1):
+    """The optimiser of time_optimize_kernel restated on the oracle objective:
+    projected scaled steepest descent, expand x1.5 / backtrack x0.5."""
+    T0 = np.array(t0, float)
+    T = T0.copy()
+    f, _ = oracle.time_cost(N, R, v, T, time_penalty=time_penalty)
+    _, g = oracle.time_cost(N, R, v, T, time_penalty=time_penalty, grad_mode=2, increment=inc)
+    evals, alpha = 1, 0.1
+    while evals < max_evals and alpha > 1e-9:
+        gmax = np.max(np.abs(g * T0))
+        if not gmax > 0:
+            break
+        trial = np.clip(T - alpha * T0 * (g * T0) / gmax, 0.1, 2.0 * T0)
+        if np.array_equal(trial, T):
+            break
+        ft, _ = oracle.time_cost(N, R, v, trial, time_penalty=time_penalty)
+        evals += 1
+        if ft < f:
+            T, f = trial, ft
+            alpha = min(alpha * 1.5, 1.0)
+            _, g = oracle.time_cost(N, R, v, T, time_penalty=time_penalty, grad_mode=2,
+                                    increment=inc)
+        else:
+            alpha *= 0.5
+    return T, f, evals

@@ -204,3 +204,48 @@ def test_evaluate_range(oracle, k):
         got, gt, n = oracle.evaluate_range(10, coeffs, t, t0, t1, 0.03, k)
         assert n == len(ref)
         assert np.array_equal(got, ref) and np.array_equal(gt, rt)
+
+
+@pytest.mark.parametrize("seed", [900, 901, 902])
+def test_time_optimize_port_matches_driver(oracle, seed):
+    """orc_time_optimize (the C++ port timed as bench's time-workload CPU
+    baseline) takes the same steps as the Python driver of the GPU
+    optimiser, on the same oracle objective."""
+    from helpers import optimize_reference
+    N, R, S = 10, 4, 6
+    v = standard_vertices(N, S, 3, seed)
+    t0 = oracle.estimate_segment_times(v, 3.0, 5.0)
+    Tr, fr, er = optimize_reference(oracle, N, R, v, t0, 20)
+    Tc, fc, ec = oracle.time_optimize(N, R, v, t0, 20)
+    assert ec == er
+    assert np.max(np.abs(Tc - Tr) / Tr) <= 1e-12
+    assert abs(fc - fr) <= 1e-12 * abs(fr)
+
+
+def test_bench_workload_baselines(oracle):
+    """The three CPU-baseline legs run and count units (tiny budgets)."""
+    N, R, S, D = 10, 4, 4, 3
+    K = N // 2
+    B = 2
+    masks = np.zeros((B, S + 1, K), np.uint8)
+    vals = np.zeros((B, S + 1, K, D))
+    times = np.zeros((B, S))
+    for b in range(B):
+        v = standard_vertices(N, S, D, 105 + b)
+        masks[b], vals[b] = v.mask, v.vals
+        times[b] = oracle.estimate_segment_times(v, 3.0, 5.0)
+    n, sec = oracle.bench_workload(1, N, D, R, S, K, masks, vals, times, param_i=5, seconds=0.01)
+    assert n >= 1 and sec > 0
+    tm = masks.copy()
+    tm[:, :, :] = 0
+    tm[:, :, 0] = 1
+    tm[:, 0, :] = 1
+    tm[:, S, :] = 1
+    tv = np.zeros_like(vals)
+    tv[:, :, 0, :] = vals[:, :, 0, :]
+    radii = np.full((B, S, 2), 0.15)
+    n, sec = oracle.bench_workload(2, N, D, R, S, K, tm, tv, times, radii=radii, seconds=0.01)
+    assert n >= 1
+    n, sec = oracle.bench_workload(3, N, D, R, S, K, masks, vals, times, param_i=4, param_d=0.01,
+                                   seconds=0.01)
+    assert n >= int(times[0].sum() / 0.01)
