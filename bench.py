@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
     p.add_argument("--segments", type=int, default=10)
-    p.add_argument("--workload", choices=["linear", "time", "tube", "sample"], default="linear")
+    p.add_argument("--workload", choices=["linear", "time", "tube", "sample", "extrema"], default="linear")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph)")
@@ -75,7 +75,7 @@ def cpu_baseline(wl, N, D, r, S, seconds, sample_args=None):
     """Oracle (reference-faithful C++ port, 1 thread) on a bounded sample of
     the same workload.  Returns (rate, units, description)."""
     import ctypes
-    seeds = range(105, 105 + (256 if wl in ("linear", "sample") else 64))
+    seeds = range(105, 105 + (256 if wl in ("linear", "sample", "extrema") else 64))
     pyoracle, masks, vals, times = _oracle_problems(N, D, S, seeds, tube=(wl == "tube"))
     K = N // 2
     B = len(seeds)
@@ -103,6 +103,11 @@ def cpu_baseline(wl, N, D, r, S, seconds, sample_args=None):
         units, sec = pyoracle.bench_workload(2, N, D, r, S, K, masks, vals, times, radii=radii,
                                              seconds=seconds)
         what = "tube QCQP solves (oracle primal-dual IPM, tol 1e-10)"
+    elif wl == "extrema":
+        units, sec = pyoracle.bench_workload(4, N, D, r, S, K, masks, vals, times,
+                                             seconds=seconds)
+        what = ("soft-constraint evaluations (two computeMaximumOfMagnitude searches, "
+                "companion-matrix roots)")
     else:
         dt, kmax = sample_args
         units, sec = pyoracle.bench_workload(3, N, D, r, S, K, masks, vals, times, param_i=kmax,
@@ -146,7 +151,8 @@ def main():
 
     N, D, r, S = 10, 3, 4, args.segments
     wl = args.workload
-    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "sample": 1024}[wl]
+    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "sample": 1024,
+                       "extrema": 1024}[wl]
     from mav_tube_trajectory_generation_amd.shard import select_best, shard_range
     global_batch = B * world
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
@@ -202,6 +208,23 @@ def main():
         metric = "trajectory samples/sec (evaluateRange, dt=0.01, derivatives 0..4, 3D)"
         unit = "samples/s"
         units_per_step = n_total
+    elif wl == "extrema":
+        # Soft-constraint cost of max |v| <= 3, max |a| <= 5 (v_max, a_max of
+        # estimateSegmentTimes) on solved trajectories: two batched
+        # computeMaximumOfMagnitude searches + the exp cost
+        # (evaluateMaximumMagnitudeAsSoftConstraint, nonlinear_impl:2735-2766).
+        sol = plan.solve(fixed_d, times_d, free=False)
+        ext_out = mtg.soft_constraint_cost(sol["coeffs"], times_d, [1, 2], [3.0, 5.0])
+
+        def step():
+            return mtg.soft_constraint_cost(sol["coeffs"], times_d, [1, 2], [3.0, 5.0],
+                                            out=ext_out)
+
+        # per search: read coeffs + times, write one maximum; + cost pass
+        bytes_per_traj = 2 * ((S * D * N + S) * 8 + 8) + (2 * 8 + 8)
+        metric = "soft-constraint evaluations/sec (max |v|, |a| extremum search, 10-seg, N=10, 3D)"
+        unit = "trajectories/s"
+        units_per_step = B
     else:
         radii = torch.full((B, S, 2), 0.15, dtype=torch.float64, device=dev)
         pos_d = torch.from_numpy(pos).to(dev)

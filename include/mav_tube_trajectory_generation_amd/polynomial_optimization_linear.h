@@ -27,9 +27,11 @@
 //     (linear_impl:287-292, 370) are not reproduced;
 //   * setupFromPositons (header :79) is declared but never defined in the
 //     reference and is not provided;
-//   * the extremum search (computeSegmentMaximumMagnitudeCandidates,
-//     computeMaximumOfMagnitude, :139-176) is SURVEY.md §8(f) rank 1 and
-//     not part of this build yet.
+//   * computeMaximumOfMagnitude (linear_impl:449-487) runs on the device
+//     (mtg_max_magnitude) and does not produce the optional candidate list
+//     (candidates must be null); the per-segment candidate helpers
+//     computeSegmentMaximumMagnitudeCandidates(BySampling) (:395-447) are
+//     not provided.
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_LINEAR_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_LINEAR_H_
 
@@ -41,6 +43,7 @@
 #include <vector>
 
 #include "mav_tube_trajectory_generation_amd/device.h"
+#include "mav_tube_trajectory_generation_amd/extremum.h"
 #include "mav_tube_trajectory_generation_amd/polynomial.h"
 #include "mav_tube_trajectory_generation_amd/segment.h"
 #include "mav_tube_trajectory_generation_amd/trajectory.h"
@@ -269,6 +272,44 @@ class PolynomialOptimization {
     cost_ = cost;
     cost_valid_ = true;
     return st == MTG_TRAJ_OK;
+  }
+
+  // linear_impl:449-487: the maximum of |p^(Derivative)| over all segments,
+  // by the device extremum search (mtg_max_magnitude).
+  template <int Derivative>
+  Extremum computeMaximumOfMagnitude(std::vector<Extremum>* candidates) const {
+    return computeMaximumOfMagnitude(Derivative, candidates);
+  }
+  Extremum computeMaximumOfMagnitude(int derivative, std::vector<Extremum>* candidates) const {
+    MTG_CHECK(candidates == nullptr,
+              "computeMaximumOfMagnitude: the candidate list is not produced by this build");
+    MTG_CHECK(N - derivative - 1 > 0, "N-Derivative-1 has to be greater 0");
+    const int D = static_cast<int>(dimension_);
+    const int S = static_cast<int>(n_segments_);
+    std::vector<double> coeffs(static_cast<size_t>(S) * D * N);
+    std::vector<double> times(S);
+    for (int s = 0; s < S; ++s) {
+      times[s] = segments_[s].getTime();
+      for (int d = 0; d < D; ++d) {
+        const VectorXd c = segments_[s][d].getCoefficients(0);
+        for (int k = 0; k < N; ++k) coeffs[(static_cast<size_t>(s) * D + d) * N + k] = c[k];
+      }
+    }
+    internal::DeviceBuffer<double> d_c, d_t, d_time(1), d_value(1);
+    internal::DeviceBuffer<int32_t> d_seg(1);
+    d_c.upload(coeffs);
+    d_t.upload(times);
+    internal::checkStatus(mtg_max_magnitude(N, D, S, 1, d_c.get(), d_t.get(), derivative,
+                                            d_time.get(), d_value.get(), d_seg.get(), nullptr),
+                          "mtg_max_magnitude");
+    internal::synchronize();
+    Extremum e;
+    int32_t seg = 0;
+    d_time.download(&e.time, 1);
+    d_value.download(&e.value, 1);
+    d_seg.download(&seg, 1);
+    e.segment_idx = seg;
+    return e;
   }
 
   void getTrajectory(Trajectory* trajectory) const {

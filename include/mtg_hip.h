@@ -249,6 +249,38 @@ int mtg_sample_trajectories(int N, int D, int S, int64_t B, const double* coeffs
                             int32_t* n_samples, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Batched magnitude extrema: PolynomialOptimization::computeMaximumOfMagnitude
+ * (polynomial_optimization_linear_impl.h:455-487, with
+ * Segment::computeMinMaxMagnitudeCandidateTimes, src/segment.cpp:82-133, and
+ * the candidate rules of Polynomial::selectMinMaxCandidatesFromRoots,
+ * src/polynomial.cpp:32-63).  For each trajectory b: the maximum over all
+ * segments s and t in [0, T_s] of |p_s^(derivative)(t)| (Euclidean norm over
+ * the D dimensions), attained at t = 0, T_s or a real root of
+ * d/dt |p^(derivative)|^2.  Outputs (device, each nullable): max_time B
+ * (time relative to the segment start, Extremum::time), max_value B,
+ * max_segment B.  Ties keep the first candidate in the reference's order
+ * (segment ascending).  0 <= derivative <= 4 (POSITION..SNAP) and
+ * derivative <= N - 2 (linear_impl:400); 1 <= S <= 256.  The reference's
+ * optional candidate list is not produced.
+ */
+int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
+                      const double* times, int derivative, double* max_time,
+                      double* max_value, int32_t* max_segment, void* stream);
+
+/* Soft-constraint cost of PolynomialOptimizationNonLinear
+ * (evaluateMaximumMagnitudeAsSoftConstraint, nonlinear_impl:2735-2766; the
+ * constraints of addMaximumMagnitudeConstraint, :847-875):
+ *   cost_b = sum_c min(maximum_cost, exp((max_bc - limit_c) / limit_c * weight)).
+ * derivatives and limits are HOST arrays of n_constraints (1..8) entries;
+ * maxima (device, B x n_constraints) receives max_bc; cost (device, B).
+ * Reference defaults: weight = soft_constraint_weight = 100
+ * (polynomial_optimization_nonlinear.h:64), maximum_cost = 1e12 (:576). */
+int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeffs,
+                             const double* times, int n_constraints, const int* derivatives,
+                             const double* limits, double weight, double maximum_cost,
+                             double* maxima, double* cost, void* stream);
+
+/* ------------------------------------------------------------------------
  * Host-side input generation (vertex.cpp:27-82, 228-269) for batches:
  * trajectory b uses createRandomVertices(max_derivative = M-1, S, +/-pos_bound,
  * seed = seed0 + b) and estimateSegmentTimes(v_max, a_max) (Nfabian, 6.5).

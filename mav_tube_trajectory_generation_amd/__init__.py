@@ -7,8 +7,10 @@ the C++ host API in include/mav_tube_trajectory_generation_amd/.  This Python
 package is the batched front end used by tests and bench.py.
 """
 from ._abi import LIB_PATH, MTGError, lib  # noqa: F401
-from .batch import (Context, LinearPlan, generate_random_problems, sample_trajectories,  # noqa: F401,E501
-                    segment_matrices, tube_num_constraints, tube_residuals, tube_solve)
+from .batch import (Context, LinearPlan, generate_random_problems, max_magnitude,  # noqa: F401
+                    sample_trajectories, segment_matrices, soft_constraint_cost,
+                    tube_num_constraints, tube_residuals, tube_solve)
 
-__all__ = ["Context", "LinearPlan", "MTGError", "generate_random_problems", "segment_matrices",
+__all__ = ["Context", "LinearPlan", "MTGError", "generate_random_problems", "max_magnitude",
+           "sample_trajectories", "segment_matrices", "soft_constraint_cost",
            "tube_num_constraints", "tube_residuals", "tube_solve", "lib", "LIB_PATH"]

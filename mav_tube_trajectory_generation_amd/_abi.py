@@ -59,6 +59,13 @@ SIGNATURES = {
                                                ctypes.c_int64, _vp, _vp, ctypes.c_double,
                                                ctypes.c_double, ctypes.c_double, ctypes.c_int,
                                                ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "mtg_max_magnitude": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                         _vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "mtg_soft_constraint_cost": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int64, _vp, _vp, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_int), _dp,
+                                                ctypes.c_double, ctypes.c_double, _vp, _vp,
+                                                _vp]),
     "mtg_generate_random_problems": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                     ctypes.c_int64, ctypes.c_uint64,
                                                     ctypes.c_double, ctypes.c_double,

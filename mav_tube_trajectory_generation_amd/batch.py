@@ -284,3 +284,56 @@ def sample_trajectories(coeffs, times, dt, t_start=0.0, t_end=-1.0, max_derivati
                                         dt, n_max, max_derivative, _ptr(samples), _ptr(stimes),
                                         _ptr(count), _stream(dev)), "mtg_sample_trajectories")
     return samples, stimes, count
+
+
+def max_magnitude(coeffs, times, derivative, out=None):
+    """Batched PolynomialOptimization::computeMaximumOfMagnitude
+    (linear_impl:455-487; mtg_max_magnitude).
+
+    coeffs [B, S, D, N], times [B, S] (float64, CUDA).  Returns a dict of
+    time [B] (relative to the segment start), value [B], segment [B] int32:
+    the Extremum of |p^(derivative)| over the trajectory.
+    """
+    import torch
+    B, S, D, N = coeffs.shape
+    _require(coeffs, (B, S, D, N), "coeffs")
+    _require(times, (B, S), "times")
+    dev = times.device
+    if out is None:
+        out = {"time": torch.empty(B, dtype=torch.float64, device=dev),
+               "value": torch.empty(B, dtype=torch.float64, device=dev),
+               "segment": torch.empty(B, dtype=torch.int32, device=dev)}
+    check(lib().mtg_max_magnitude(N, D, S, B, _ptr(coeffs), _ptr(times), derivative,
+                                  _ptr(out["time"]), _ptr(out["value"]), _ptr(out["segment"]),
+                                  _stream(dev)), "mtg_max_magnitude")
+    return out
+
+
+def soft_constraint_cost(coeffs, times, derivatives, limits, weight=100.0, maximum_cost=1.0e12,
+                         out=None):
+    """Batched evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:
+    2735-2766; mtg_soft_constraint_cost) for the constraints
+    (derivatives[c], limits[c]) of addMaximumMagnitudeConstraint.
+
+    Returns a dict of cost [B] and maxima [B, n_constraints].
+    """
+    import ctypes
+
+    import torch
+    B, S, D, N = coeffs.shape
+    _require(coeffs, (B, S, D, N), "coeffs")
+    _require(times, (B, S), "times")
+    nc = len(derivatives)
+    if len(limits) != nc:
+        raise MTGError("derivatives and limits differ in length")
+    dev = times.device
+    if out is None:
+        out = {"cost": torch.empty(B, dtype=torch.float64, device=dev),
+               "maxima": torch.empty((B, nc), dtype=torch.float64, device=dev)}
+    der = (ctypes.c_int * max(nc, 1))(*[int(d) for d in derivatives])
+    lim = (ctypes.c_double * max(nc, 1))(*[float(v) for v in limits])
+    check(lib().mtg_soft_constraint_cost(N, D, S, B, _ptr(coeffs), _ptr(times), nc, der, lim,
+                                         float(weight), float(maximum_cost), _ptr(out["maxima"]),
+                                         _ptr(out["cost"]), _stream(dev)),
+          "mtg_soft_constraint_cost")
+    return out

@@ -346,6 +346,51 @@ int mtg_sample_trajectories(int N, int D, int S, int64_t B, const double* coeffs
                                      static_cast<hipStream_t>(stream)));
 }
 
+int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
+                      const double* times, int derivative, double* max_time,
+                      double* max_value, int32_t* max_segment, void* stream) {
+  if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > 256 || B < 0 || derivative < 0 ||
+      derivative > mtg::kMaxExtremaDerivative || N - derivative - 1 <= 0)
+    return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  if (!coeffs || !times) return MTG_ERR_INVALID_ARG;
+  const mtg::SoftCostArgs none{};
+  return from_hip(mtg::launch_max_magnitude(N, D, S, B, derivative, coeffs, times, max_time,
+                                            max_value, max_segment, 1, 0, none,
+                                            static_cast<hipStream_t>(stream)));
+}
+
+int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeffs,
+                             const double* times, int n_constraints, const int* derivatives,
+                             const double* limits, double weight, double maximum_cost,
+                             double* maxima, double* cost, void* stream) {
+  if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > 256 || B < 0 ||
+      n_constraints < 1 || n_constraints > mtg::kMaxSoftConstraints || !derivatives ||
+      !limits)
+    return MTG_ERR_INVALID_ARG;
+  mtg::SoftLimits lim{};
+  lim.n = n_constraints;
+  for (int c = 0; c < n_constraints; ++c) {
+    // addMaximumMagnitudeConstraint: CHECK_GE(derivative, 0), CHECK_GE(value, 0)
+    if (derivatives[c] < 0 || derivatives[c] > mtg::kMaxExtremaDerivative ||
+        N - derivatives[c] - 1 <= 0 || !(limits[c] >= 0.0))
+      return MTG_ERR_INVALID_ARG;
+    lim.value[c] = limits[c];
+  }
+  if (B == 0) return MTG_OK;
+  if (!coeffs || !times || !maxima || !cost) return MTG_ERR_INVALID_ARG;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const mtg::SoftCostArgs none{};
+  const mtg::SoftCostArgs last{cost, lim, weight, maximum_cost};
+  for (int c = 0; c < n_constraints; ++c) {
+    const int rc = from_hip(mtg::launch_max_magnitude(
+        N, D, S, B, derivatives[c], coeffs, times, nullptr, maxima, nullptr, n_constraints, c,
+        c == n_constraints - 1 ? last : none, st));
+    if (rc) return rc;
+  }
+  return MTG_OK;
+}
+
 int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* times,
                          double* Q, double* A, double* Ainv, double* H, void* stream) {
   if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || n < 0 || (n && !times))

@@ -70,4 +70,23 @@ hipError_t launch_sample(int N, int D, int S, int64_t B, const double* coeffs,
                          int n_max, int max_deriv, double* samples, double* sample_times,
                          int32_t* n_samples, hipStream_t st);
 
+// Magnitude extrema and soft constraints (mtg_extrema.hip).
+constexpr int kMaxExtremaDerivative = 4;  // POSITION..SNAP (nonlinear_impl:2697-2724)
+constexpr int kMaxSoftConstraints = 8;
+struct SoftLimits {
+  int n;
+  double value[kMaxSoftConstraints];
+};
+// Soft-constraint cost formed by the last constraint's launch:
+// cost_b = sum_c min(maximum_cost, exp((max_bc - lim_c) / lim_c * weight)).
+struct SoftCostArgs {
+  double* cost;  // null: plain maximum search
+  SoftLimits lim;
+  double weight, maximum_cost;
+};
+hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
+                                const double* coeffs, const double* times, double* max_time,
+                                double* max_value, int32_t* max_segment, int value_stride,
+                                int value_offset, const SoftCostArgs& soft, hipStream_t st);
+
 }  // namespace mtg

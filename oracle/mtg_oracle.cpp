@@ -1263,6 +1263,359 @@ int orc_evaluate_range(int N, int D, int S, const double* coeffs, const double* 
   return 0;
 }
 
+// ----------------------------------------------------------------------------
+// Magnitude extrema.
+//
+// The reference finds all complex roots with Jenkins-Traub
+// (findRootsJenkinsTraub, src/rpoly/rpoly_ak1.cpp:70-117; the TOMS-493
+// translation needs Eigen and cannot be built here).  The
+// oracle computes the same roots as the eigenvalues of the companion matrix
+// (balancing + Francis double-shift QR on the Hessenberg form, as
+// numpy.roots / LAPACK dgeev do); real roots come out with an imaginary part
+// of exactly 0 in both, which is what selectMinMaxCandidatesFromRoots
+// (polynomial.cpp:32-63) filters on.
+
+// Balancing of a general matrix (radix 2; Parlett-Reinsch), in place.
+static void balanceMatrix(std::vector<double>& a, int n) {
+  const double radix = 2.0, sqrdx = radix * radix;
+  bool done = false;
+  while (!done) {
+    done = true;
+    for (int i = 0; i < n; ++i) {
+      double r = 0.0, c = 0.0;
+      for (int j = 0; j < n; ++j)
+        if (j != i) {
+          c += std::fabs(a[j * n + i]);
+          r += std::fabs(a[i * n + j]);
+        }
+      if (c != 0.0 && r != 0.0) {
+        double g = r / radix, f = 1.0;
+        const double s0 = c + r;
+        while (c < g) {
+          f *= radix;
+          c *= sqrdx;
+        }
+        g = r * radix;
+        while (c > g) {
+          f /= radix;
+          c /= sqrdx;
+        }
+        if ((c + r) / f < 0.95 * s0) {
+          done = false;
+          g = 1.0 / f;
+          for (int j = 0; j < n; ++j) a[i * n + j] *= g;
+          for (int j = 0; j < n; ++j) a[j * n + i] *= f;
+        }
+      }
+    }
+  }
+}
+
+// Eigenvalues of an upper Hessenberg matrix by the Francis double-shift QR
+// iteration (EISPACK hqr).  Returns false if an eigenvalue did not converge
+// in 60 iterations.
+static bool hessenbergEigenvalues(std::vector<double>& A, int n, std::vector<double>* wr,
+                                  std::vector<double>* wi) {
+  auto a = [&](int i, int j) -> double& { return A[i * n + j]; };
+  wr->assign(n, 0.0);
+  wi->assign(n, 0.0);
+  double anorm = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int j = std::max(i - 1, 0); j < n; ++j) anorm += std::fabs(a(i, j));
+  int nn = n - 1;
+  double t = 0.0;
+  double p = 0.0, q = 0.0, r = 0.0, s = 0.0, w = 0.0, x = 0.0, y = 0.0, z = 0.0;
+  while (nn >= 0) {
+    int its = 0, l = 0;
+    do {
+      for (l = nn; l >= 1; --l) {
+        s = std::fabs(a(l - 1, l - 1)) + std::fabs(a(l, l));
+        if (s == 0.0) s = anorm;
+        if (std::fabs(a(l, l - 1)) + s == s) {
+          a(l, l - 1) = 0.0;
+          break;
+        }
+      }
+      x = a(nn, nn);
+      if (l == nn) {  // one root
+        (*wr)[nn] = x + t;
+        (*wi)[nn] = 0.0;
+        --nn;
+      } else {
+        y = a(nn - 1, nn - 1);
+        w = a(nn, nn - 1) * a(nn - 1, nn);
+        if (l == nn - 1) {  // two roots
+          p = 0.5 * (y - x);
+          q = p * p + w;
+          z = std::sqrt(std::fabs(q));
+          x += t;
+          if (q >= 0.0) {
+            z = p + (p >= 0.0 ? std::fabs(z) : -std::fabs(z));
+            (*wr)[nn - 1] = (*wr)[nn] = x + z;
+            if (z != 0.0) (*wr)[nn] = x - w / z;
+            (*wi)[nn - 1] = (*wi)[nn] = 0.0;
+          } else {
+            (*wr)[nn - 1] = (*wr)[nn] = x + p;
+            (*wi)[nn - 1] = -z;
+            (*wi)[nn] = z;
+          }
+          nn -= 2;
+        } else {
+          if (its == 60) return false;
+          if (its == 10 || its == 20) {  // exceptional shift
+            t += x;
+            for (int i = 0; i <= nn; ++i) a(i, i) -= x;
+            s = std::fabs(a(nn, nn - 1)) + std::fabs(a(nn - 1, nn - 2));
+            y = x = 0.75 * s;
+            w = -0.4375 * s * s;
+          }
+          ++its;
+          int m = nn - 2;
+          for (; m >= l; --m) {
+            z = a(m, m);
+            r = x - z;
+            s = y - z;
+            p = (r * s - w) / a(m + 1, m) + a(m, m + 1);
+            q = a(m + 1, m + 1) - z - r - s;
+            r = a(m + 2, m + 1);
+            s = std::fabs(p) + std::fabs(q) + std::fabs(r);
+            p /= s;
+            q /= s;
+            r /= s;
+            if (m == l) break;
+            const double u = std::fabs(a(m, m - 1)) * (std::fabs(q) + std::fabs(r));
+            const double v =
+                std::fabs(p) * (std::fabs(a(m - 1, m - 1)) + std::fabs(z) + std::fabs(a(m + 1, m + 1)));
+            if (u + v == v) break;
+          }
+          for (int i = m + 2; i <= nn; ++i) {
+            a(i, i - 2) = 0.0;
+            if (i != m + 2) a(i, i - 3) = 0.0;
+          }
+          for (int k = m; k <= nn - 1; ++k) {
+            if (k != m) {
+              p = a(k, k - 1);
+              q = a(k + 1, k - 1);
+              r = 0.0;
+              if (k != nn - 1) r = a(k + 2, k - 1);
+              if ((x = std::fabs(p) + std::fabs(q) + std::fabs(r)) != 0.0) {
+                p /= x;
+                q /= x;
+                r /= x;
+              }
+            }
+            const double nrm = std::sqrt(p * p + q * q + r * r);
+            if ((s = (p >= 0.0 ? nrm : -nrm)) != 0.0) {
+              if (k == m) {
+                if (l != m) a(k, k - 1) = -a(k, k - 1);
+              } else {
+                a(k, k - 1) = -s * x;
+              }
+              p += s;
+              x = p / s;
+              y = q / s;
+              z = r / s;
+              q /= p;
+              r /= p;
+              for (int j = k; j <= nn; ++j) {
+                p = a(k, j) + q * a(k + 1, j);
+                if (k != nn - 1) {
+                  p += r * a(k + 2, j);
+                  a(k + 2, j) -= p * z;
+                }
+                a(k + 1, j) -= p * y;
+                a(k, j) -= p * x;
+              }
+              const int mmin = nn < k + 3 ? nn : k + 3;
+              for (int i = l; i <= mmin; ++i) {
+                p = x * a(i, k) + y * a(i, k + 1);
+                if (k != nn - 1) {
+                  p += z * a(i, k + 2);
+                  a(i, k + 2) -= p * r;
+                }
+                a(i, k + 1) -= p * q;
+                a(i, k) -= p;
+              }
+            }
+          }
+        }
+      }
+    } while (nn >= 0 && l < nn - 1);
+  }
+  return true;
+}
+
+// findRootsJenkinsTraub's contract (rpoly_ak1.cpp:70-117): coefficients in
+// increasing order; trailing (highest-order) coefficients below DBL_MIN are
+// dropped; constant or zero polynomials have no roots.  Roots at the origin
+// are split off exactly, as rpoly does.
+static bool findRoots(const std::vector<double>& inc, std::vector<double>* re,
+                      std::vector<double>* im) {
+  re->clear();
+  im->clear();
+  int last = -1;
+  for (int i = static_cast<int>(inc.size()) - 1; i >= 0; --i)
+    if (std::fabs(inc[i]) >= std::numeric_limits<double>::min()) {
+      last = i;
+      break;
+    }
+  if (last < 1) return last == 0 ? false : true;
+  int lo = 0;
+  while (inc[lo] == 0.0) {  // zero roots
+    re->push_back(0.0);
+    im->push_back(0.0);
+    ++lo;
+  }
+  const int n = last - lo;
+  if (n == 0) return true;
+  std::vector<double> C(static_cast<size_t>(n) * n, 0.0);
+  for (int j = 0; j < n; ++j) C[j] = -inc[last - 1 - j] / inc[last];  // first row
+  for (int i = 1; i < n; ++i) C[i * n + i - 1] = 1.0;
+  balanceMatrix(C, n);
+  std::vector<double> wr, wi;
+  if (!hessenbergEigenvalues(C, n, &wr, &wi)) return false;
+  for (int i = 0; i < n; ++i) {
+    re->push_back(wr[i]);
+    im->push_back(wi[i]);
+  }
+  return true;
+}
+
+// Polynomial::getCoefficients(derivative) (polynomial.h:113-127): the
+// derivative's coefficients, index 0 = t^0, zero-padded to N.
+static std::vector<double> derivCoefficients(int N, const double* c, int derivative) {
+  const Mat& base = baseTable();
+  std::vector<double> out(N, 0.0);
+  for (int i = derivative; i < N; ++i) out[i - derivative] = base(derivative, i) * c[i];
+  return out;
+}
+
+// Polynomial::convolve (polynomial.cpp:163-181).
+static std::vector<double> convolveCoefficients(const std::vector<double>& data,
+                                                const std::vector<double>& kernel) {
+  const int nd = static_cast<int>(data.size()), nk = static_cast<int>(kernel.size());
+  std::vector<double> out(nd + nk - 1, 0.0);
+  for (int i = 0; i < nd + nk - 1; ++i) {
+    const int data_idx = i - nk + 1;
+    const int lower = std::max(0, -data_idx), upper = std::min(nk, nd - data_idx);
+    for (int k = lower; k < upper; ++k) out[i] += kernel[nk - 1 - k] * data[data_idx + k];
+  }
+  return out;
+}
+
+// Segment::computeMinMaxMagnitudeCandidateTimes (segment.cpp:82-133) +
+// Polynomial::computeMinMaxCandidates (polynomial.cpp:65-81) for all D
+// dimensions (linear_impl:395-409).  Appends to *cand.
+static void magnitudeCandidateTimes(int N, int D, const double* seg, int derivative,
+                                    double t_start, double t_end, std::vector<double>* cand) {
+  std::vector<double> f;
+  if (D > 1) {
+    const int n_d = N - derivative, n_dd = n_d - 1;
+    f.assign(n_d + n_dd - 1, 0.0);
+    for (int d = 0; d < D; ++d) {
+      std::vector<double> dv = derivCoefficients(N, seg + d * N, derivative);
+      std::vector<double> ddv = derivCoefficients(N, seg + d * N, derivative + 1);
+      dv.resize(n_d);
+      ddv.resize(n_dd);
+      const std::vector<double> c = convolveCoefficients(dv, ddv);
+      for (size_t i = 0; i < f.size(); ++i) f[i] += c[i];
+    }
+  } else {
+    f = derivCoefficients(N, seg, derivative + 1);
+  }
+  std::vector<double> re, im;
+  findRoots(f, &re, &im);
+  cand->push_back(t_start);  // selectMinMaxCandidatesFromRoots :44-45
+  cand->push_back(t_end);
+  for (size_t i = 0; i < re.size(); ++i) {
+    if (std::fabs(im[i]) > std::numeric_limits<double>::epsilon()) continue;
+    if (re[i] < t_start || re[i] > t_end) continue;
+    cand->push_back(re[i]);
+  }
+}
+
+static double magnitudeAt(int N, int D, const double* seg, double t, int derivative) {
+  double sq = 0.0;
+  for (int d = 0; d < D; ++d) {
+    const double v = polyEvaluate(N, seg + d * N, t, derivative);
+    sq += v * v;
+  }
+  return std::sqrt(sq);
+}
+
+// PolynomialOptimization::computeMaximumOfMagnitude (linear_impl:455-487) on
+// a trajectory's coefficients (S x D x N).  n_candidates (optional) receives
+// the number of candidates the reference would list.
+int orc_max_magnitude(int N, int D, int S, const double* coeffs, const double* times,
+                      int derivative, double* time, double* value, int* segment,
+                      int* n_candidates) {
+  if (N < 2 || D < 1 || S < 1 || !coeffs || !times) return -2;
+  if (N - derivative - 1 <= 0 || derivative < 0) return -3;  // linear_impl:400
+  double best_t = 0.0, best_v = 0.0;  // Extremum() = {0, 0, 0}
+  int best_s = 0, count = 0;
+  for (int s = 0; s < S; ++s) {
+    const double* seg = coeffs + static_cast<size_t>(s) * D * N;
+    std::vector<double> ts;
+    ts.push_back(0.0);
+    magnitudeCandidateTimes(N, D, seg, derivative, 0.0, times[s], &ts);
+    for (double t : ts) {
+      const double v = magnitudeAt(N, D, seg, t, derivative);
+      if (best_v < v) {
+        best_t = t;
+        best_v = v;
+        best_s = s;
+      }
+      ++count;
+    }
+  }
+  const double* last = coeffs + static_cast<size_t>(S - 1) * D * N;
+  const double v = magnitudeAt(N, D, last, times[S - 1], derivative);
+  if (best_v < v) {
+    best_t = times[S - 1];
+    best_v = v;
+    best_s = S - 1;
+  }
+  ++count;
+  if (time) *time = best_t;
+  if (value) *value = best_v;
+  if (segment) *segment = best_s;
+  if (n_candidates) *n_candidates = count;
+  return 0;
+}
+
+// Real roots of a polynomial (increasing coefficients) by the oracle's root
+// finder; re/im hold up to n-1 entries.  Returns the number of roots.
+int orc_poly_roots(int n, const double* inc, double* re, double* im) {
+  std::vector<double> c(inc, inc + n), r, i;
+  if (!findRoots(c, &r, &i)) return -1;
+  for (size_t k = 0; k < r.size(); ++k) {
+    re[k] = r[k];
+    im[k] = i[k];
+  }
+  return static_cast<int>(r.size());
+}
+
+// evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:2735-2766):
+// sum over constraints of min(maximum_cost, exp((max - limit) / limit * w)).
+int orc_soft_constraint_cost(int N, int D, int S, const double* coeffs, const double* times,
+                             int n_constraints, const int* derivatives, const double* limits,
+                             double weight, double maximum_cost, double* maxima,
+                             double* cost) {
+  double total = 0.0;
+  for (int c = 0; c < n_constraints; ++c) {
+    double value = 0.0;
+    int rc = orc_max_magnitude(N, D, S, coeffs, times, derivatives[c], nullptr, &value, nullptr,
+                               nullptr);
+    if (rc) return rc;
+    if (maxima) maxima[c] = value;
+    const double abs_violation = value - limits[c];
+    const double relative_violation = abs_violation / limits[c];
+    total += std::min(maximum_cost, std::exp(relative_violation * weight));
+  }
+  if (cost) *cost = total;
+  return 0;
+}
+
 int orc_control_point_map(int N, double T, double* Binv) {
   if (N < 2 || N % 2 || N > 12 || !(T > 0) || !Binv) return -1;
   Mat b = setupInverseControlPointMappingMatrix(N, T);
@@ -1404,13 +1757,13 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                        const uint8_t* masks, const double* vals, const double* times,
                        const double* radii, int param_i, double param_d, int threads,
                        double min_seconds, int64_t* units, double* seconds) {
-  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 3) return -1;
+  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 4) return -1;
   if (kind == 2 && !radii) return -1;
   if (kind == 3 && !(param_d > 0.0)) return -1;
   const size_t mstride = static_cast<size_t>(S + 1) * K;
-  // kind 3: coefficients solved before the clock starts.
+  // kinds 3, 4: coefficients solved before the clock starts.
   std::vector<std::vector<double>> coeffs;
-  if (kind == 3) {
+  if (kind >= 3) {
     coeffs.resize(B);
     for (int b = 0; b < B; ++b) {
       LinearProblem lp;
@@ -1449,6 +1802,15 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                                            radii + static_cast<size_t>(b) * S * 2, 1e-10, 100,
                                            nullptr, nullptr, &c, &itn);
         if (rc < 0 && rc != -22) failed = 1;
+        acc += c;
+        ++n;
+      } else if (kind == 4) {
+        const int ders[2] = {1, 2};
+        const double lims[2] = {3.0, 5.0};
+        double c = 0.0;
+        if (orc_soft_constraint_cost(N, D, S, coeffs[b].data(), tb, 2, ders, lims, 100.0, 1.0e12,
+                                     nullptr, &c))
+          failed = 1;
         acc += c;
         ++n;
       } else {

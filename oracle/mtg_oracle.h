@@ -89,6 +89,21 @@ int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
                   int grad_mode, double increment, double w_d, double w_t,
                   double* cost, double* grad);
 
+// PolynomialOptimization::computeMaximumOfMagnitude (linear_impl:455-487)
+// on one trajectory (coeffs S x D x N, times S): the Extremum {time relative
+// to its segment, value, segment}.  Roots by companion-matrix eigenvalues in
+// place of Jenkins-Traub (see mtg_oracle.cpp).  -3 if N - derivative - 1 <= 0.
+int orc_max_magnitude(int N, int D, int S, const double* coeffs, const double* times,
+                      int derivative, double* time, double* value, int* segment,
+                      int* n_candidates);
+// All complex roots of the polynomial with increasing coefficients inc[0..n).
+int orc_poly_roots(int n, const double* inc, double* re, double* im);
+// evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:2735-2766).
+int orc_soft_constraint_cost(int N, int D, int S, const double* coeffs, const double* times,
+                             int n_constraints, const int* derivatives, const double* limits,
+                             double weight, double maximum_cost, double* maxima,
+                             double* cost);
+
 // ---------------- tube QCQP (qcqp_impl) ----------------
 // Inverse Bezier control-point map B^-1(T) with the 1e-5 zero-snap
 // (qcqp_impl:267-319), N x N row-major.
@@ -168,8 +183,11 @@ int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
 // param_i; kind 2: tube QCQP solve (radii: B x S x 2, tol 1e-10, 100
 // iterations); kind 3: evaluateRange for derivatives 0..param_i at
 // dt = param_d over the whole trajectory, on coefficients solved once before
-// the clock starts.  *units = optimisations (1), solves (2), or samples
-// (3, one sample = all derivatives of all dimensions at one time).
+// the clock starts; kind 4: the soft-constraint cost of max |v| <= 3,
+// max |a| <= 5 (two computeMaximumOfMagnitude searches) on coefficients
+// solved before the clock starts.  *units = optimisations (1), solves (2),
+// samples (3, one sample = all derivatives of all dimensions at one time)
+// or trajectories (4).
 int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                        const uint8_t* masks, const double* vals, const double* times,
                        const double* radii, int param_i, double param_d, int threads,

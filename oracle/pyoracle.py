@@ -287,3 +287,50 @@ def evaluate_range(N, coeffs, times, t_start, t_end, dt, derivative, max_out=Non
            "evaluate_range")
     n = min(count.value, max_out)
     return out[:n], tout[:n], count.value
+
+
+def max_magnitude(N, coeffs, times, derivative):
+    """orc_max_magnitude: computeMaximumOfMagnitude (linear_impl:455-487) on
+    coeffs [S, D, N].  Returns dict(time, value, segment, n_candidates)."""
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    S, D, _ = coeffs.shape
+    t, v = np.zeros(1), np.zeros(1)
+    seg, nc = ctypes.c_int(), ctypes.c_int()
+    L = lib()
+    L.orc_max_magnitude.argtypes = [ctypes.c_int] * 3 + [_dp, _dp, ctypes.c_int, _dp, _dp, _ip, _ip]
+    _check(L.orc_max_magnitude(N, D, S, _d(coeffs), _d(times), derivative, _d(t), _d(v),
+                               ctypes.byref(seg), ctypes.byref(nc)), "max_magnitude")
+    return dict(time=float(t[0]), value=float(v[0]), segment=seg.value, n_candidates=nc.value)
+
+
+def poly_roots(inc):
+    """orc_poly_roots: all complex roots (companion-matrix eigenvalues)."""
+    inc = np.ascontiguousarray(inc, dtype=np.float64)
+    re, im = np.zeros(len(inc)), np.zeros(len(inc))
+    L = lib()
+    L.orc_poly_roots.argtypes = [ctypes.c_int, _dp, _dp, _dp]
+    n = L.orc_poly_roots(len(inc), _d(inc), _d(re), _d(im))
+    _check(0 if n >= 0 else n, "poly_roots")
+    return re[:n] + 1j * im[:n]
+
+
+def soft_constraint_cost(N, coeffs, times, derivatives, limits, weight=100.0,
+                         maximum_cost=1.0e12):
+    """orc_soft_constraint_cost (nonlinear_impl:2735-2766).  Returns
+    (cost, maxima)."""
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    S, D, _ = coeffs.shape
+    der = np.ascontiguousarray(derivatives, dtype=np.int32)
+    lim = np.ascontiguousarray(limits, dtype=np.float64)
+    maxima = np.zeros(len(der))
+    cost = np.zeros(1)
+    L = lib()
+    L.orc_soft_constraint_cost.argtypes = [ctypes.c_int] * 3 + [_dp, _dp, ctypes.c_int, _ip, _dp,
+                                                                ctypes.c_double, ctypes.c_double,
+                                                                _dp, _dp]
+    _check(L.orc_soft_constraint_cost(N, D, S, _d(coeffs), _d(times), len(der),
+                                      der.ctypes.data_as(_ip), _d(lim), weight, maximum_cost,
+                                      _d(maxima), _d(cost)), "soft_constraint_cost")
+    return float(cost[0]), maxima

@@ -243,7 +243,10 @@ TEST(host, RandomVerticesBitIdentical) {
 }
 
 TEST(host, SolveFailsLoudlyWithoutDevice) {
-  // No CPU fallback: the plan cannot be created without a HIP device.
+  // No CPU fallback: the plan cannot be created without a HIP device.  (On a
+  // GPU host there is a device, and the gpu group covers the solve.)
+  int n_dev = 0;
+  if (hipGetDeviceCount(&n_dev) == hipSuccess && n_dev > 0) return;
   const Vertex::Vector vs = fixtureVertices(kSeg10Dim3, 10);
   PolynomialOptimization<10> opt(3);
   EXPECT_THROW(opt.setupFromVertices(vs, estimateSegmentTimes(vs, 3.0, 5.0), 4));
@@ -549,6 +552,49 @@ TEST(gpu, OptimizeTimeLowersObjective) {
   Segment::Vector segs;
   traj.getSegments(&segs);
   checkPath(vs, segs, 10);
+}
+
+// Extrema test of the reference (test_polynomial_optimization.cpp:370-400):
+// the analytic maximum of |v| and |a| agrees with dense sampling within 0.01
+// (getMaximumMagnitude, test_utils.h) and with the oracle's
+// computeMaximumOfMagnitude restatement.
+TEST(gpu, MaximumOfMagnitude) {
+  for (const Fixture& f : kFixtures) {
+    const Vertex::Vector vs = fixtureVertices(f, 10);
+    const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+    PolynomialOptimization<10> opt(f.D);
+    opt.setupFromVertices(vs, times, f.r);
+    EXPECT_TRUE(opt.solveLinear());
+    Segment::Vector segs;
+    opt.getSegments(&segs);
+    const std::vector<double> c = coeffsOf(segs, 10);
+    for (int k = derivative_order::VELOCITY; k <= derivative_order::ACCELERATION; ++k) {
+      const Extremum e = k == derivative_order::VELOCITY
+                             ? opt.computeMaximumOfMagnitude<derivative_order::VELOCITY>(nullptr)
+                             : opt.computeMaximumOfMagnitude(k, nullptr);
+      double ot = 0.0, ov = 0.0;
+      int os = 0;
+      EXPECT_TRUE(orc_max_magnitude(10, f.D, f.S, c.data(), times.data(), k, &ot, &ov, &os,
+                                    nullptr) == 0);
+      EXPECT_LE(relErr(e.value, ov), 1e-10);
+      double sampled = 0.0;  // getMaximumMagnitude: dt = 0.01
+      for (const Segment& s : segs)
+        for (double t = 0.0; t < s.getTime(); t += 0.01) {
+          const VectorXd v = s.evaluate(t, k);
+          double n2 = 0.0;
+          for (int d = 0; d < f.D; ++d) n2 += v[d] * v[d];
+          sampled = std::max(sampled, std::sqrt(n2));
+        }
+      EXPECT_LE(std::fabs(sampled - e.value), 0.01);
+      EXPECT_TRUE(e.value >= sampled - 1e-12);
+      // The reported time lies in its segment and attains the value.
+      EXPECT_TRUE(e.segment_idx >= 0 && e.segment_idx < f.S);
+      const VectorXd v = segs[e.segment_idx].evaluate(e.time, k);
+      double n2 = 0.0;
+      for (int d = 0; d < f.D; ++d) n2 += v[d] * v[d];
+      EXPECT_LE(relErr(std::sqrt(n2), e.value), 1e-12);
+    }
+  }
 }
 
 }  // namespace

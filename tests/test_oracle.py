@@ -249,3 +249,82 @@ def test_bench_workload_baselines(oracle):
     n, sec = oracle.bench_workload(3, N, D, R, S, K, masks, vals, times, param_i=4, param_d=0.01,
                                    seconds=0.01)
     assert n >= int(times[0].sum() / 0.01)
+
+
+def test_poly_roots_match_numpy(oracle):
+    """The oracle's root finder (companion eigenvalues, standing in for
+    findRootsJenkinsTraub, rpoly_ak1.cpp:70-117) against numpy.roots,
+    including zero roots and dropped highest-order zeros."""
+    rng = np.random.default_rng(3)
+    for it in range(300):
+        n = int(rng.integers(2, 19))
+        c = rng.standard_normal(n)
+        if it % 5 == 0:
+            c[0] = 0.0
+        if it % 7 == 0:
+            c[-1] = 0.0
+        got = np.sort_complex(oracle.poly_roots(c))
+        if not np.any(c):
+            assert len(got) == 0
+            continue
+        last = np.nonzero(c)[0].max()
+        ref = np.sort_complex(np.roots(c[:last + 1][::-1])) if last > 0 else np.array([])
+        assert len(got) == len(ref)
+        if len(ref):
+            assert np.max(np.abs(got - ref) / np.maximum(1, np.abs(ref))) <= 1e-10
+
+
+def _max_magnitude_numpy(N, coeffs, times, k):
+    """computeMaximumOfMagnitude (linear_impl:455-487) restated with numpy:
+    convolution of segment.cpp:101-116, numpy.roots, the candidate filter of
+    polynomial.cpp:32-63."""
+    from numpy.polynomial import polynomial as P
+    S, D, _ = coeffs.shape
+    best = (0.0, 0.0, 0)
+    for s in range(S):
+        f = np.zeros(2 * (N - k) - 2)
+        for d in range(D):
+            dv = P.polyder(coeffs[s, d], k) if k else coeffs[s, d]
+            ddv = P.polyder(coeffs[s, d], k + 1)
+            dv = np.pad(dv, (0, N - k - len(dv)))[:N - k]
+            ddv = np.pad(ddv, (0, N - k - 1 - len(ddv)))[:N - k - 1]
+            f += np.convolve(dv, ddv)
+        nz = np.nonzero(np.abs(f) >= np.finfo(float).tiny)[0]
+        roots = np.roots(f[:nz.max() + 1][::-1]) if len(nz) and nz.max() > 0 else []
+        cands = [0.0, 0.0, times[s]] + [r.real for r in roots
+                                        if abs(r.imag) <= np.finfo(float).eps
+                                        and 0.0 <= r.real <= times[s]]
+        for t in cands:
+            v = np.sqrt(sum(P.polyval(t, P.polyder(coeffs[s, d], k) if k else coeffs[s, d]) ** 2
+                            for d in range(D)))
+            if v > best[0]:
+                best = (v, t, s)
+    return best
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 4])
+def test_max_magnitude_matches_numpy_restatement(oracle, k):
+    N, S, D = 10, 10, 3
+    for seed in (105, 106, 111):
+        v = standard_vertices(N, S, D, seed)
+        t = oracle.estimate_segment_times(v, 3.0, 5.0)
+        c = oracle.linear_solve(N, 4, v, t)["coeffs"]
+        got = oracle.max_magnitude(N, c, t, k)
+        val, tm, seg = _max_magnitude_numpy(N, c, t, k)
+        assert abs(got["value"] - val) <= 1e-12 * val
+        assert got["segment"] == seg and abs(got["time"] - tm) <= 1e-9 * t[seg]
+        # candidates: 0, 0, T and the real roots in [0, T] per segment, + the end
+        assert got["n_candidates"] >= 3 * S + 1
+
+
+def test_soft_constraint_cost_formula(oracle):
+    N, S, D = 10, 6, 3
+    v = standard_vertices(N, S, D, 140)
+    t = oracle.estimate_segment_times(v, 3.0, 5.0)
+    c = oracle.linear_solve(N, 4, v, t)["coeffs"]
+    cost, maxima = oracle.soft_constraint_cost(N, c, t, [1, 2], [2.0, 1.0], 100.0)
+    vm = oracle.max_magnitude(N, c, t, 1)["value"]
+    am = oracle.max_magnitude(N, c, t, 2)["value"]
+    assert np.allclose(maxima, [vm, am], rtol=0, atol=0)
+    ref = min(1e12, np.exp((vm - 2.0) / 2.0 * 100.0)) + min(1e12, np.exp((am - 1.0) / 1.0 * 100.0))
+    assert abs(cost - ref) <= 1e-12 * ref
