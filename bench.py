@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph)")
+    p.add_argument("--soft", action="store_true",
+                   help="time workload: soft constraints max|v| <= 3, max|a| <= 5 in the objective")
     return p.parse_args()
 
 
@@ -180,11 +182,15 @@ def main():
     elif wl == "time":
         max_evals = 50
 
+        soft = [(1, 3.0), (2, 5.0)] if args.soft else None
+
         def step():
-            return plan.time_optimize(fixed_d, times_d, max_evals=max_evals)
+            return plan.time_optimize(fixed_d, times_d, max_evals=max_evals, soft=soft)
 
         bytes_per_traj = (D * nf + S) * 8 + (S + 2) * 8
         metric = "time-allocation optimisations/sec (4096 traj x 50 evals, 10-seg, N=10, 3D)"
+        if args.soft:
+            metric += " + soft max|v|<=3, max|a|<=5"
         unit = "trajectories/s"
         units_per_step = B
     elif wl == "sample":

@@ -5,8 +5,8 @@
 // restricted to the objective on the hot path:
 // kOptimizeTime with the time-only cost callback
 //   J(T) = computeCost() + time_penalty * (sum_i T_i)^2
-// (objectiveFunctionTime, nonlinear_impl:877-945, w_c = 0, no soft
-// constraints).  Both the callback (evaluateTimeCost -> mtg_time_cost) and
+// (objectiveFunctionTime, nonlinear_impl:877-945, w_c = 0, optional soft
+// magnitude constraints).  Both the callback (evaluateTimeCost -> mtg_time_cost) and
 // the whole optimisation loop (optimize -> mtg_time_optimize) run on the
 // device.
 //
@@ -24,12 +24,18 @@
 //   * the collision cost (w_c > 0) needs the supereight octree (out of scope,
 //     SURVEY.md §8f rank 4; the reference dereferences a null octree there,
 //     §8a T6): it is ignored with a warning;
-//   * addMaximumMagnitudeConstraint / soft constraints need the extremum
-//     search (§8f rank 1) and return false.
+//   * addMaximumMagnitudeConstraint with use_soft_constraints (the default)
+//     adds the soft cost of evaluateMaximumMagnitudeAsSoftConstraint
+//     (:2735-2766) to the objective, evaluated on the device after every
+//     inner solve (extremum search of mtg_max_magnitude); at most 8
+//     constraints, derivatives POSITION..SNAP.  The NLopt hard inequality
+//     constraints used when use_soft_constraints is false (:861-872) have no
+//     counterpart in the device optimiser: that call returns false.
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
 
 #include <chrono>
+#include <map>
 #include <ostream>
 #include <utility>
 #include <vector>
@@ -111,6 +117,7 @@ class OptimizationInfo {
   double cost_time = 0;
   double cost_soft_constraints = 0;
   double optimization_time = 0;
+  std::map<int, Extremum> maxima;  // per constrained derivative, after optimize()
 };
 
 template <int _N = 10>
@@ -137,11 +144,23 @@ class PolynomialOptimizationNonLinear {
     return ret;
   }
 
-  bool addMaximumMagnitudeConstraint(int /*derivative_order*/, double /*maximum_value*/) {
-    internal::warn(
-        "addMaximumMagnitudeConstraint: the extremum search is not part of this build "
-        "(SURVEY.md 8f rank 1); constraint ignored");
-    return false;
+  // nonlinear_impl:847-875.
+  bool addMaximumMagnitudeConstraint(int derivative_order, double maximum_value) {
+    MTG_CHECK(derivative_order >= 0, "derivative must be >= 0");
+    MTG_CHECK(maximum_value >= 0.0, "maximum_value must be >= 0");
+    if (!params_.use_soft_constraints) {
+      internal::warn(
+          "addMaximumMagnitudeConstraint: hard (NLopt) inequality constraints are not "
+          "available in the device optimiser; set use_soft_constraints");
+      return false;
+    }
+    if (soft_.size() >= 8 || derivative_order > derivative_order::SNAP ||
+        N - derivative_order - 1 <= 0) {
+      internal::warn("addMaximumMagnitudeConstraint: unsupported constraint ignored");
+      return false;
+    }
+    soft_.push_back(std::make_pair(derivative_order, maximum_value));
+    return true;
   }
 
   int solveQCQP() { return poly_opt_.solveQCQP(); }
@@ -205,6 +224,14 @@ class PolynomialOptimizationNonLinear {
     optimization_info_.n_iterations = evals;
     optimization_info_.cost_trajectory = linear_.computeCost();
     optimization_info_.cost_time = tot * tot * params_.time_penalty;
+    double J = 0.0;
+    d_cost.download(&J, 1);
+    optimization_info_.cost_soft_constraints =
+        soft_.empty() ? 0.0
+                      : J - optimization_info_.cost_trajectory - optimization_info_.cost_time;
+    for (const auto& c : soft_)
+      optimization_info_.maxima[c.first] =
+          linear_.computeMaximumOfMagnitude(c.first, nullptr);
     optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
     optimization_info_.optimization_time =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -243,6 +270,13 @@ class PolynomialOptimizationNonLinear {
     p.w_d = params_.weights.w_d;
     p.w_t = params_.weights.w_t;
     p.grad_mode = grad_mode;
+    p.n_soft = params_.use_soft_constraints ? static_cast<int>(soft_.size()) : 0;
+    for (int c = 0; c < 8; ++c) {
+      p.soft_derivative[c] = c < p.n_soft ? soft_[c].first : 0;
+      p.soft_limit[c] = c < p.n_soft ? soft_[c].second : 1.0;
+    }
+    p.soft_weight = params_.soft_constraint_weight;
+    p.soft_maximum_cost = 1.0e12;  // evaluateMaximumMagnitudeAsSoftConstraint default
     return p;
   }
   void warnCollision() const {
@@ -266,6 +300,7 @@ class PolynomialOptimizationNonLinear {
   Vertex::Vector vertices_;
   Trajectory trajectory_initial_;
   OptimizationInfo optimization_info_;
+  std::vector<std::pair<int, double>> soft_;  // (derivative, maximum_value)
 };
 
 }  // namespace mav_trajectory_generation

@@ -142,9 +142,15 @@ int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n,
 /* ------------------------------------------------------------------------
  * Time-allocation cost callback, batched.  Replaces
  * PolynomialOptimizationNonLinear<N>::objectiveFunctionTime
- * (nonlinear_impl:877-945) with w_c = 0 and no soft constraints (SURVEY.md
- * §8a T6) and a linear inner solve (upstream semantics):
- *   J(T) = computeCost() + time_penalty * (sum_i T_i)^2
+ * (nonlinear_impl:877-945) with w_c = 0 and a linear
+ * inner solve (upstream semantics):
+ *   J(T) = computeCost() + time_penalty * (sum_i T_i)^2 [+ soft]
+ * soft (n_soft > 0, use_soft_constraints, :907-913) is
+ * evaluateMaximumMagnitudeAsSoftConstraint (:2735-2766) over the
+ * addMaximumMagnitudeConstraint list (:847-875): sum_c min(soft_maximum_cost,
+ * exp((max_t |p^(soft_derivative[c])| - soft_limit[c]) / soft_limit[c] *
+ * soft_weight)), with the maxima from the device extremum search of
+ * mtg_max_magnitude.
  * grad_mode (grad may be NULL when 0):
  *   0  no gradient (objectiveFunctionTime is gradient-free, :881-882)
  *   1  getCostAndGradientTime (nonlinear_impl:2495-2584):
@@ -162,6 +168,11 @@ typedef struct mtg_time_params {
   double w_d;          /* ::weights.w_d (0.1) */
   double w_t;          /* ::weights.w_t (1.0) */
   int grad_mode;       /* see above */
+  int n_soft;          /* soft magnitude constraints, 0..8 (0: none) */
+  int soft_derivative[8];   /* derivative order of constraint c, 0..4 */
+  double soft_limit[8];     /* maximum_value of constraint c, > 0 */
+  double soft_weight;       /* ::soft_constraint_weight (100) */
+  double soft_maximum_cost; /* maximum_cost (1e12, header :576) */
 } mtg_time_params;
 
 int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,

@@ -19,9 +19,29 @@ _vp = ctypes.c_void_p
 
 
 class TimeParams(ctypes.Structure):
+    """mtg_time_params (include/mtg_hip.h)."""
     _fields_ = [("time_penalty", ctypes.c_double), ("increment", ctypes.c_double),
                 ("w_d", ctypes.c_double), ("w_t", ctypes.c_double),
-                ("grad_mode", ctypes.c_int)]
+                ("grad_mode", ctypes.c_int), ("n_soft", ctypes.c_int),
+                ("soft_derivative", ctypes.c_int * 8), ("soft_limit", ctypes.c_double * 8),
+                ("soft_weight", ctypes.c_double), ("soft_maximum_cost", ctypes.c_double)]
+
+
+def make_time_params(time_penalty=500.0, increment=0.1, w_d=0.1, w_t=1.0, grad_mode=0,
+                     soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """soft: list of (derivative, maximum_value) magnitude constraints
+    (addMaximumMagnitudeConstraint), evaluated as soft costs."""
+    p = TimeParams(time_penalty, increment, w_d, w_t, grad_mode)
+    soft = list(soft or [])
+    if len(soft) > 8:
+        raise MTGError("at most 8 soft constraints")
+    p.n_soft = len(soft)
+    for i, (d, v) in enumerate(soft):
+        p.soft_derivative[i] = int(d)
+        p.soft_limit[i] = float(v)
+    p.soft_weight = soft_weight
+    p.soft_maximum_cost = soft_maximum_cost
+    return p
 
 
 # Symbol -> (restype, argtypes).  Must match include/mtg_hip.h exactly; the

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import MTGError, TimeParams, check, lib
+from ._abi import MTGError, check, lib, make_time_params
 
 
 def _ptr(t):
@@ -133,7 +133,9 @@ class LinearPlan:
         return coeffs, cost, status
 
     def time_cost(self, fixed_vals, times, time_penalty=500.0, grad_mode=0, increment=0.1,
-                  w_d=0.1, w_t=1.0):
+                  w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0):
+        """objectiveFunctionTime per trajectory (mtg_time_cost); soft: list of
+        (derivative, maximum_value) soft magnitude constraints."""
         import torch
         B = times.shape[0]
         _require(times, (B, self.S), "times")
@@ -142,14 +144,14 @@ class LinearPlan:
         cost = torch.empty(B, dtype=torch.float64, device=dev)
         grad = torch.empty((B, self.S), dtype=torch.float64, device=dev) if grad_mode else None
         status = torch.empty(B, dtype=torch.int32, device=dev)
-        p = TimeParams(time_penalty, increment, w_d, w_t, grad_mode)
+        p = make_time_params(time_penalty, increment, w_d, w_t, grad_mode, soft, soft_weight)
         check(lib().mtg_time_cost(self._h, B, _ptr(fixed_vals), _ptr(times), ctypes.byref(p),
                                   _ptr(cost), _ptr(grad), _ptr(status), _stream(dev)),
               "mtg_time_cost")
         return dict(cost=cost, grad=grad, status=status)
 
     def time_optimize(self, fixed_vals, times, max_evals=50, time_penalty=500.0, increment=0.1,
-                      w_d=0.1, w_t=1.0):
+                      w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0):
         """Optimise segment times in place on a copy; returns dict(times, cost, evals)."""
         import torch
         B = times.shape[0]
@@ -160,7 +162,7 @@ class LinearPlan:
         cost = torch.empty(B, dtype=torch.float64, device=dev)
         evals = torch.empty(B, dtype=torch.int32, device=dev)
         status = torch.empty(B, dtype=torch.int32, device=dev)
-        p = TimeParams(time_penalty, increment, w_d, w_t, 2)
+        p = make_time_params(time_penalty, increment, w_d, w_t, 2, soft, soft_weight)
         check(lib().mtg_time_optimize(self._h, B, _ptr(fixed_vals), _ptr(t), ctypes.byref(p),
                                       max_evals, _ptr(cost), _ptr(evals), _ptr(status),
                                       _stream(dev)), "mtg_time_optimize")

@@ -91,7 +91,7 @@ struct Layout {
   int ndouble;
   int slot;        // (S+1)*M int slots (after the doubles)
   int nint;
-  size_t bytes() const { return sizeof(double) * ndouble + sizeof(int) * nint; }
+  __host__ __device__ size_t bytes() const { return sizeof(double) * ndouble + sizeof(int) * nint; }
 };
 
 __host__ __device__ inline Layout make_layout(int N, int S, int D) {

@@ -31,43 +31,11 @@
 
 #include <cmath>
 
-#include "mtg_internal.h"
+#include "mtg_extrema_device.h"
 
 namespace mtg {
 
 constexpr int kExtBlock = 256;
-constexpr int kExtParts = 8;       // dyadic parts per segment (power of 2)
-constexpr int kExtMaxLevel = 30;   // node width 2^-30 of the segment: cluster
-constexpr int kExtRefineIters = 80;
-
-__host__ __device__ constexpr double ext_falling(int k, int i) {
-  double p = 1.0;
-  for (int m = 0; m < k; ++m) p *= static_cast<double>(i - m);
-  return p;
-}
-
-__host__ __device__ constexpr double ext_binom(int n, int k) {
-  double r = 1.0;
-  for (int i = 1; i <= k; ++i) r = r * static_cast<double>(n - k + i) / static_cast<double>(i);
-  return r;
-}
-
-// |p^(K)(t)|^2 over the D dimensions of one segment (Polynomial::evaluate,
-// polynomial.h:135-149: Horner over base(K, i) c_i).
-template <int N, int K>
-__device__ inline double ext_mag2(const double* c, int D, double t) {
-  double sq = 0.0;
-#pragma unroll
-  for (int d = 0; d < kMaxD; ++d) {
-    if (d >= D) break;
-    const double* cd = c + d * N;
-    double v = ext_falling(K, N - 1) * cd[N - 1];
-#pragma unroll
-    for (int i = N - 2; i >= K; --i) v = fma(v, t, ext_falling(K, i) * cd[i]);
-    sq = fma(v, v, sq);
-  }
-  return sq;
-}
 
 template <int N, int K>
 __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
@@ -75,9 +43,6 @@ __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
     const double* __restrict__ times, double* __restrict__ max_time,
     double* __restrict__ max_value, int32_t* __restrict__ max_segment, int value_stride,
     int value_offset, SoftCostArgs soft) {
-  constexpr int ND = N - K;       // terms of p^(K)
-  constexpr int NDD = ND - 1;     // terms of p^(K+1)
-  constexpr int M = ND + NDD - 2; // degree of f
   __shared__ double val_s[kExtBlock];
   __shared__ double time_s[kExtBlock];
   // The block's trajectories (coefficients, then segment times), staged
@@ -107,164 +72,7 @@ __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
   if (active) {
     const double T = traj_s[traj_per_block * S * D * N + bl * S + s];
     const double* c = traj_s + (bl * S + s) * D * N;
-    // Endpoint candidates first (the reference lists 0, 0, T, roots).
-    if (part == 0) {
-      best_v = ext_mag2<N, K>(c, D, 0.0);
-      best_t = 0.0;
-    }
-    if (part == parts - 1) {
-      const double v = ext_mag2<N, K>(c, D, T);
-      if (v > best_v) {
-        best_v = v;
-        best_t = T;
-      }
-    }
-    // f(t) = sum_d conv(p_d^(K), p_d^(K+1)), then q(u) = f(T u) on [0, 1].
-    double q[M + 1];
-#pragma unroll
-    for (int j = 0; j <= M; ++j) q[j] = 0.0;
-#pragma unroll
-    for (int d = 0; d < kMaxD; ++d) {
-      if (d >= D) break;
-      const double* cd = c + d * N;
-      double dv[ND], ddv[NDD];
-#pragma unroll
-      for (int j = 0; j < ND; ++j) dv[j] = ext_falling(K, j + K) * cd[j + K];
-#pragma unroll
-      for (int j = 0; j < NDD; ++j) ddv[j] = ext_falling(K + 1, j + K + 1) * cd[j + K + 1];
-#pragma unroll
-      for (int a = 0; a < ND; ++a)
-#pragma unroll
-        for (int e = 0; e < NDD; ++e) q[a + e] = fma(dv[a], ddv[e], q[a + e]);
-    }
-    {
-      double tp = T;
-#pragma unroll
-      for (int j = 1; j <= M; ++j) {
-        q[j] *= tp;
-        tp *= T;
-      }
-    }
-    // Bernstein coefficients on [0, 1]: beta_i = sum_{j<=i} C(i,j)/C(M,j) q_j,
-    // normalised to max |beta| = 1.
-    double beta[M + 1];
-    double mx = 0.0;
-#pragma unroll
-    for (int i = 0; i <= M; ++i) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j <= i; ++j) acc = fma(ext_binom(i, j) / ext_binom(M, j), q[j], acc);
-      beta[i] = acc;
-      mx = fmax(mx, fabs(acc));
-    }
-    if (mx > 0.0) {
-      const double inv = 1.0 / mx;
-#pragma unroll
-      for (int i = 0; i <= M; ++i) {
-        beta[i] *= inv;
-        q[i] *= inv;
-      }
-      // Depth-first walk of the dyadic tree under node (log2parts, part).
-      int level = log2parts, idx = part;
-      for (;;) {
-        const double w = ldexp(1.0, -level);
-        const double a = idx * w;
-        const double e = a + w;
-        // Node coefficients: left part of a split at e, then the right part
-        // of that at a / e.
-        double bb[M + 1];
-#pragma unroll
-        for (int i = 0; i <= M; ++i) bb[i] = beta[i];
-        if (e < 1.0) {
-#pragma unroll
-          for (int r = 1; r <= M; ++r)
-#pragma unroll
-            for (int i = M; i >= r; --i) bb[i] = fma(e, bb[i] - bb[i - 1], bb[i - 1]);
-        }
-        if (a > 0.0) {
-          const double u = a / e;
-#pragma unroll
-          for (int r = 1; r <= M; ++r)
-#pragma unroll
-            for (int i = 0; i <= M - r; ++i) bb[i] = fma(u, bb[i + 1] - bb[i], bb[i]);
-        }
-        // Sign variations (zeros skipped), first / last nonzero signs.
-        int var = 0;
-        double first = 0.0, last = 0.0;
-#pragma unroll
-        for (int i = 0; i <= M; ++i) {
-          const double x = bb[i];
-          const bool nz = x != 0.0;
-          var += (nz && last != 0.0 && ((x > 0.0) != (last > 0.0))) ? 1 : 0;
-          first = (first == 0.0) ? x : first;
-          last = nz ? x : last;
-        }
-        double root = -1.0;
-        if (bb[0] == 0.0 && a > 0.0) {  // root exactly at the node's left end
-          const double v = ext_mag2<N, K>(c, D, a * T);
-          if (v > best_v) {
-            best_v = v;
-            best_t = a * T;
-          }
-        }
-        bool descend = false;
-        if (var == 1) {
-          // Laguerre's method safeguarded by the bracket (bisection when a
-          // step leaves it); lo keeps the sign of q just right of a.  Laguerre
-          // models the other roots as one cluster, which is what the
-          // high-multiplicity roots at rest-to-rest vertices look like, so it
-          // converges in a few steps where Newton crawls.  Stops at the
-          // rounding floor of the Horner evaluation.
-          double lo = a, hi = e, x = 0.5 * (a + e);
-          const bool pos_lo = first > 0.0;
-          for (int it = 0; it < kExtRefineIters; ++it) {
-            double fx = q[M], d1 = 0.0, d2 = 0.0, ab = fabs(q[M]);
-#pragma unroll
-            for (int j = M - 1; j >= 0; --j) {
-              d2 = fma(d2, x, d1);
-              d1 = fma(d1, x, fx);
-              fx = fma(fx, x, q[j]);
-              ab = fma(ab, x, fabs(q[j]));
-            }
-            if (fabs(fx) <= 32.0 * 2.220446049250313e-16 * ab) break;
-            if ((fx > 0.0) == pos_lo) lo = x; else hi = x;
-            const double G = d1 / fx;
-            const double H = G * G - 2.0 * d2 / fx;
-            const double rad = fmax((M - 1) * (M * H - G * G), 0.0);
-            const double sq = sqrt(rad);
-            const double den = G >= 0.0 ? G + sq : G - sq;
-            double xn = den != 0.0 ? x - M / den : 0.5 * (lo + hi);
-            if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
-            const bool done = fabs(xn - x) <= 1.0e-12 || hi - lo <= 1.0e-12;
-            x = xn;
-            if (done) break;
-          }
-          root = x;
-        } else if (var > 1) {
-          if (level >= kExtMaxLevel) root = 0.5 * (a + e);  // unresolved cluster
-          else descend = true;
-        }
-        if (root >= 0.0) {
-          const double t = root * T;
-          const double v = ext_mag2<N, K>(c, D, t);
-          if (v > best_v) {
-            best_v = v;
-            best_t = t;
-          }
-        }
-        if (descend) {
-          ++level;
-          idx *= 2;
-          continue;
-        }
-        while (level > log2parts && (idx & 1)) {
-          idx >>= 1;
-          --level;
-        }
-        if (level == log2parts) break;
-        ++idx;
-      }
-    }
+    ext_segment_search<N, K>(c, D, T, part, parts, log2parts, best_v, best_t);
   }
   val_s[tid] = best_v;
   time_s[tid] = best_t;

@@ -403,12 +403,28 @@ int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* ti
                                                static_cast<hipStream_t>(stream)));
 }
 
+// Soft constraints of mtg_time_params: addMaximumMagnitudeConstraint's
+// CHECK_GE(derivative, 0), CHECK_GE(maximum_value, 0) (nonlinear_impl:849-850),
+// the POSITION..SNAP switch (:2697-2724), N - derivative - 1 > 0
+// (linear_impl:400) and a nonzero limit (the cost divides by it, :2754).
+static bool valid_soft(const mtg_plan* plan, const mtg_time_params* p) {
+  if (p->n_soft < 0 || p->n_soft > mtg::kMaxSoftConstraints) return false;
+  if (p->n_soft > 0 && plan->dev.S > 256) return false;
+  for (int c = 0; c < p->n_soft; ++c) {
+    const int k = p->soft_derivative[c];
+    if (k < 0 || k > mtg::kMaxExtremaDerivative || plan->dev.N - k - 1 <= 0) return false;
+    if (!(p->soft_limit[c] > 0.0)) return false;
+  }
+  return true;
+}
+
 int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                   const double* times, const mtg_time_params* params, double* cost,
                   double* grad, int32_t* status, void* stream) {
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times) return MTG_ERR_INVALID_ARG;
   if (params->grad_mode < 0 || params->grad_mode > 2) return MTG_ERR_INVALID_ARG;
   if (params->grad_mode && !(params->increment > 0)) return MTG_ERR_INVALID_ARG;
+  if (!valid_soft(plan, params)) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   return from_hip(mtg::launch_time_cost(plan->dev, B, fixed_vals, times, *params, cost, grad,
                                         status, static_cast<hipStream_t>(stream)));
@@ -420,6 +436,7 @@ int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
+  if (!valid_soft(plan, params)) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   return from_hip(mtg::launch_time_optimize(plan->dev, B, fixed_vals, times_io, *params,
                                             max_evals, cost, evals, status,

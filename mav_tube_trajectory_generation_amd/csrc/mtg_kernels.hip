@@ -6,6 +6,7 @@
 #include <cmath>
 
 #include "mtg_device.h"
+#include "mtg_extrema_device.h"
 #include "mtg_internal.h"
 
 namespace mtg {
@@ -142,9 +143,9 @@ __global__ void segment_matrices_kernel(int N, int r, int64_t n,
 // ---------------------------------------------------------------------------
 // Time-allocation objective J(T) = computeCost() + time_penalty (sum T)^2
 // (objectiveFunctionTime, nonlinear_impl:877-945) with optional gradient.
-template <int N>
+template <int N, bool kSoft>
 __device__ double objective_at(Traj<N>& t, const double* __restrict__ tab,
-                               double time_penalty) {
+                               const mtg_time_params& p, double* cbuf) {
   // Assumes T() holds the times; recomputes powers and re-solves.
   __syncthreads();
   t.compute_powers();
@@ -152,11 +153,42 @@ __device__ double objective_at(Traj<N>& t, const double* __restrict__ tab,
   t.clear_free();
   __syncthreads();
   t.solve();
-  const double J = t.cost(tab);
+  double J;
+  if constexpr (kSoft) {
+    J = t.template coeffs_and_cost<true>(tab, cbuf);  // coefficients into LDS
+  } else {
+    J = t.cost(tab);
+  }
   double tot = 0.0;
   for (int i = 0; i < t.S; ++i) tot += t.T()[i];  // nonlinear_impl:2768-2774
+  J += tot * tot * p.time_penalty;
+  if constexpr (kSoft) {
+    // evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:2735-2766):
+    // one extremum search per constraint over the wave, from one call site.
+    __syncthreads();
+    double soft = 0.0;
+    for (int c = 0; c < p.n_soft; ++c) {
+      int K = 0;
+      double lim = 1.0;
+#pragma unroll
+      for (int cc = 0; cc < kMaxSoftConstraints; ++cc)  // compile-time indices
+        if (cc == c) {
+          K = p.soft_derivative[cc];
+          lim = p.soft_limit[cc];
+        }
+      const double m = ext_trajectory_max_wave_k<N>(K, cbuf, t.T(), t.S, t.D, t.lane);
+      const double relative_violation = (m - lim) / lim;
+      soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
+    }
+    J += soft;
+  }
   __syncthreads();
-  return J + tot * tot * time_penalty;
+  return J;
+}
+
+// LDS for the soft-constraint objective's coefficients, after the layout.
+__host__ __device__ inline size_t soft_cbuf_offset(const Layout& lay) {
+  return (lay.bytes() + 15) / 16 * 16;
 }
 
 // The reference's getCostAndGradientTime (grad_mode 1): with d held at the
@@ -193,7 +225,7 @@ __device__ void set_fd_point(Traj<N>& t, const double* Tb, int gi, double inc) {
 // Every objective evaluation of the two kernels below goes through ONE call
 // site of objective_at (a loop over evaluation points), so the solver body
 // is instantiated once per kernel and stays within the register file.
-template <int N>
+template <int N, bool kSoft>
 __global__ __launch_bounds__(kWave) void time_cost_kernel(
     PlanDev pl, const double* __restrict__ fixed_vals, const double* __restrict__ times,
     mtg_time_params p, double* __restrict__ cost, double* __restrict__ grad,
@@ -205,6 +237,7 @@ __global__ __launch_bounds__(kWave) void time_cost_kernel(
   Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
             static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
   const int64_t b = blockIdx.x;
+  double* cbuf = reinterpret_cast<double*>(reinterpret_cast<char*>(smem) + soft_cbuf_offset(lay));
   double* g = smem + lay.aux;   // gradient
   double* Tb = g + S;           // base times
   t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times + b * S, fixed_vals + b * D * nf, nf);
@@ -215,7 +248,7 @@ __global__ __launch_bounds__(kWave) void time_cost_kernel(
   int fl = 0;
   for (int e = 0; e < nevals; ++e) {
     if (e > 0) set_fd_point(t, Tb, e - 1, p.increment);
-    const double J = objective_at(t, tab, p.time_penalty);
+    const double J = objective_at<N, kSoft>(t, tab, p, cbuf);
     if (e == 0) {
       J0 = J;
       fl = t.flag()[0];
@@ -246,7 +279,7 @@ __global__ __launch_bounds__(kWave) void time_cost_kernel(
 // evaluations (NLopt maxeval semantics, nonlinear_impl:101; gradient
 // evaluations are not counted).  Written as a state machine with one
 // objective evaluation per loop trip.
-template <int N>
+template <int N, bool kSoft>
 __global__ __launch_bounds__(kWave) void time_optimize_kernel(
     PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ times_io,
     mtg_time_params p, int max_evals, double* __restrict__ cost,
@@ -258,6 +291,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
             static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
   const int64_t b = blockIdx.x;
+  double* cbuf = reinterpret_cast<double*>(reinterpret_cast<char*>(smem) + soft_cbuf_offset(lay));
   double* Tcur = smem + lay.aux;   // accepted times
   double* T0 = Tcur + S;           // initial times (bounds)
   double* g = T0 + S;              // gradient at Tcur
@@ -274,7 +308,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   int fl = 0;
   while (phase != kDone) {
-    const double J = objective_at(t, tab, p.time_penalty);  // at T()
+    const double J = objective_at<N, kSoft>(t, tab, p, cbuf);  // at T()
     if (phase == kBase) {
       f = J;
       evals = 1;
@@ -379,11 +413,20 @@ static hipError_t launch_time_cost_n(const PlanDev& pl, int64_t B, const double*
                                      const double* times, const mtg_time_params& p,
                                      double* cost, double* grad, int32_t* status,
                                      hipStream_t st) {
-  const size_t bytes = make_layout(N, pl.S, pl.D).bytes();
-  hipError_t e = prepare_lds(time_cost_kernel<N>, bytes);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(time_cost_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
-                     bytes, st, pl, df, times, p, cost, grad, status);
+  const Layout lay = make_layout(N, pl.S, pl.D);
+  if (p.n_soft > 0) {
+    const size_t bytes = soft_cbuf_offset(lay) + sizeof(double) * pl.S * pl.D * N;
+    hipError_t e = prepare_lds(time_cost_kernel<N, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_cost_kernel<N, true>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, times, p, cost, grad, status);
+  } else {
+    const size_t bytes = lay.bytes();
+    hipError_t e = prepare_lds(time_cost_kernel<N, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_cost_kernel<N, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, times, p, cost, grad, status);
+  }
   return hipGetLastError();
 }
 
@@ -392,11 +435,20 @@ static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* 
                                     double* times, const mtg_time_params& p,
                                     int max_evals, double* cost, int32_t* evals,
                                     int32_t* status, hipStream_t st) {
-  const size_t bytes = make_layout(N, pl.S, pl.D).bytes();
-  hipError_t e = prepare_lds(time_optimize_kernel<N>, bytes);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(time_optimize_kernel<N>, dim3(static_cast<unsigned>(B)), dim3(kWave),
-                     bytes, st, pl, df, times, p, max_evals, cost, evals, status);
+  const Layout lay = make_layout(N, pl.S, pl.D);
+  if (p.n_soft > 0) {
+    const size_t bytes = soft_cbuf_offset(lay) + sizeof(double) * pl.S * pl.D * N;
+    hipError_t e = prepare_lds(time_optimize_kernel<N, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_optimize_kernel<N, true>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, status);
+  } else {
+    const size_t bytes = lay.bytes();
+    hipError_t e = prepare_lds(time_optimize_kernel<N, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_optimize_kernel<N, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, status);
+  }
   return hipGetLastError();
 }
 

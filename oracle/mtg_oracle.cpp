@@ -1164,10 +1164,18 @@ int orc_linear_matrices(int N, int D, int r, int S, int K, const uint8_t* mask,
   return 0;
 }
 
-int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
-                  const double* vals, const double* times, double time_penalty,
-                  int grad_mode, double increment, double w_d, double w_t,
-                  double* cost, double* grad) {
+// Soft-constraint part of objectiveFunctionTime (nonlinear_impl:907-913).
+struct SoftSpec {
+  int n;
+  const int* derivatives;
+  const double* limits;
+  double weight, maximum_cost;
+};
+
+static int timeCostImpl(int N, int D, int r, int S, int K, const uint8_t* mask,
+                        const double* vals, const double* times, double time_penalty,
+                        int grad_mode, double increment, double w_d, double w_t,
+                        const SoftSpec* soft, double* cost, double* grad) {
   LinearProblem lp;
   int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
   if (rc) return rc;
@@ -1176,8 +1184,16 @@ int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
     p.solveLinear();
     double total = 0.0;
     for (double v : t) total += v;  // nonlinear_impl:2768-2774
-    return p.computeCost() + total * total * time_penalty;
+    double J = p.computeCost() + total * total * time_penalty;
+    if (soft && soft->n > 0) {
+      double c = 0.0;
+      orc_soft_constraint_cost(N, D, S, p.coeffs.data(), t.data(), soft->n, soft->derivatives,
+                               soft->limits, soft->weight, soft->maximum_cost, nullptr, &c);
+      J += c;
+    }
+    return J;
   };
+
   std::vector<double> t(times, times + S);
   const double J = objective(lp, t);
   if (cost) *cost = J;
@@ -1208,6 +1224,25 @@ int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
     grad[n] = (Jb - Js) / (2.0 * increment);
   }
   return 0;
+}
+
+int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                  const double* vals, const double* times, double time_penalty,
+                  int grad_mode, double increment, double w_d, double w_t,
+                  double* cost, double* grad) {
+  return timeCostImpl(N, D, r, S, K, mask, vals, times, time_penalty, grad_mode, increment,
+                      w_d, w_t, nullptr, cost, grad);
+}
+
+int orc_time_cost_soft(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times, double time_penalty,
+                       int grad_mode, double increment, double w_d, double w_t, int n_soft,
+                       const int* soft_derivatives, const double* soft_limits,
+                       double soft_weight, double soft_maximum_cost, double* cost,
+                       double* grad) {
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  return timeCostImpl(N, D, r, S, K, mask, vals, times, time_penalty, grad_mode, increment,
+                      w_d, w_t, &soft, cost, grad);
 }
 
 // Polynomial::evaluate (polynomial.h:135-149): Horner with the derivative
@@ -1696,9 +1731,10 @@ int orc_tube_qcqp_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
   return status;
 }
 
-int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
-                      const double* vals, double* times_io, double time_penalty,
-                      double increment, int max_evals, double* cost, int* evals) {
+static int timeOptimizeImpl(int N, int D, int r, int S, int K, const uint8_t* mask,
+                            const double* vals, double* times_io, double time_penalty,
+                            double increment, int max_evals, const SoftSpec* soft,
+                            double* cost, int* evals) {
   LinearProblem lp;
   int rc = setupLinear(N, D, r, S, K, mask, vals, times_io, &lp);
   if (rc) return rc;
@@ -1707,8 +1743,16 @@ int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
     lp.solveLinear();
     double total = 0.0;
     for (double v : t) total += v;
-    return lp.computeCost() + total * total * time_penalty;
+    double J = lp.computeCost() + total * total * time_penalty;
+    if (soft && soft->n > 0) {
+      double c = 0.0;
+      orc_soft_constraint_cost(N, D, S, lp.coeffs.data(), t.data(), soft->n, soft->derivatives,
+                               soft->limits, soft->weight, soft->maximum_cost, nullptr, &c);
+      J += c;
+    }
+    return J;
   };
+
   auto gradient = [&](const std::vector<double>& t, std::vector<double>* g) {
     for (int n = 0; n < S; ++n) {  // grad_mode 2 of orc_time_cost
       std::vector<double> ts = t, tb = t;
@@ -1751,6 +1795,24 @@ int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
   if (cost) *cost = f;
   if (evals) *evals = n_eval;
   return 0;
+}
+
+int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                      const double* vals, double* times_io, double time_penalty,
+                      double increment, int max_evals, double* cost, int* evals) {
+  return timeOptimizeImpl(N, D, r, S, K, mask, vals, times_io, time_penalty, increment,
+                          max_evals, nullptr, cost, evals);
+}
+
+int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, double* times_io, double time_penalty,
+                           double increment, int max_evals, int n_soft,
+                           const int* soft_derivatives, const double* soft_limits,
+                           double soft_weight, double soft_maximum_cost, double* cost,
+                           int* evals) {
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  return timeOptimizeImpl(N, D, r, S, K, mask, vals, times_io, time_penalty, increment,
+                          max_evals, &soft, cost, evals);
 }
 
 int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,

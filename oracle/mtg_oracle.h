@@ -178,6 +178,22 @@ int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
                       const double* vals, double* times_io, double time_penalty,
                       double increment, int max_evals, double* cost, int* evals);
 
+// objectiveFunctionTime / the optimiser with soft magnitude constraints
+// (use_soft_constraints, nonlinear_impl:907-913, 2735-2766): the objective
+// adds orc_soft_constraint_cost on the solved coefficients.
+int orc_time_cost_soft(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times, double time_penalty,
+                       int grad_mode, double increment, double w_d, double w_t, int n_soft,
+                       const int* soft_derivatives, const double* soft_limits,
+                       double soft_weight, double soft_maximum_cost, double* cost,
+                       double* grad);
+int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, double* times_io, double time_penalty,
+                           double increment, int max_evals, int n_soft,
+                           const int* soft_derivatives, const double* soft_limits,
+                           double soft_weight, double soft_maximum_cost, double* cost,
+                           int* evals);
+
 // CPU baseline for the other bench workloads, same cycling/threads/timing
 // rules as orc_bench_linear.  kind 1: orc_time_optimize with max_evals =
 // param_i; kind 2: tube QCQP solve (radii: B x S x 2, tol 1e-10, 100

@@ -160,31 +160,59 @@ def linear_matrices(N, r, vertices, times):
 
 
 def time_cost(N, r, vertices, times, time_penalty=500.0, grad_mode=0, increment=0.1,
-              w_d=0.1, w_t=1.0):
+              w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """objectiveFunctionTime (orc_time_cost / orc_time_cost_soft); soft: list
+    of (derivative, maximum_value) soft magnitude constraints."""
     S, D, K = vertices.S, vertices.D, vertices.K
     times = np.ascontiguousarray(times, dtype=np.float64)
     cost = np.zeros(1)
     grad = np.zeros(S)
-    _check(lib().orc_time_cost(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p), _d(vertices.vals),
-                               _d(times), time_penalty, grad_mode, increment, w_d, w_t, _d(cost),
-                               _d(grad)), "time_cost")
+    L = lib()
+    if soft:
+        der = np.ascontiguousarray([d for d, _ in soft], dtype=np.int32)
+        lim = np.ascontiguousarray([v for _, v in soft], dtype=np.float64)
+        L.orc_time_cost_soft.argtypes = [ctypes.c_int] * 5 + [
+            _u8p, _dp, _dp, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+            ctypes.c_double, ctypes.c_int, _ip, _dp, ctypes.c_double, ctypes.c_double, _dp, _dp]
+        _check(L.orc_time_cost_soft(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                    _d(vertices.vals), _d(times), time_penalty, grad_mode,
+                                    increment, w_d, w_t, len(der), der.ctypes.data_as(_ip),
+                                    _d(lim), soft_weight, soft_maximum_cost, _d(cost), _d(grad)),
+               "time_cost_soft")
+    else:
+        _check(L.orc_time_cost(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                               _d(vertices.vals), _d(times), time_penalty, grad_mode, increment,
+                               w_d, w_t, _d(cost), _d(grad)), "time_cost")
     return float(cost[0]), (grad if grad_mode else None)
 
 
-
-def time_optimize(N, r, vertices, times, max_evals, time_penalty=500.0, increment=0.1):
-    """orc_time_optimize: the mtg_time_optimize algorithm on the oracle
+def time_optimize(N, r, vertices, times, max_evals, time_penalty=500.0, increment=0.1,
+                  soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """orc_time_optimize(_soft): the mtg_time_optimize algorithm on the oracle
     objective.  Returns (times, cost, evals)."""
     S, D, K = vertices.S, vertices.D, vertices.K
     t = np.array(times, dtype=np.float64)
     cost = np.zeros(1)
     evals = ctypes.c_int()
     L = lib()
-    L.orc_time_optimize.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, ctypes.c_double,
-                                                         ctypes.c_double, ctypes.c_int, _dp, _ip]
-    _check(L.orc_time_optimize(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
-                               _d(vertices.vals), _d(t), time_penalty, increment, max_evals,
-                               _d(cost), ctypes.byref(evals)), "time_optimize")
+    if soft:
+        der = np.ascontiguousarray([d for d, _ in soft], dtype=np.int32)
+        lim = np.ascontiguousarray([v for _, v in soft], dtype=np.float64)
+        L.orc_time_optimize_soft.argtypes = [ctypes.c_int] * 5 + [
+            _u8p, _dp, _dp, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int, _ip,
+            _dp, ctypes.c_double, ctypes.c_double, _dp, _ip]
+        _check(L.orc_time_optimize_soft(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                        _d(vertices.vals), _d(t), time_penalty, increment,
+                                        max_evals, len(der), der.ctypes.data_as(_ip), _d(lim),
+                                        soft_weight, soft_maximum_cost, _d(cost),
+                                        ctypes.byref(evals)), "time_optimize_soft")
+    else:
+        L.orc_time_optimize.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, ctypes.c_double,
+                                                             ctypes.c_double, ctypes.c_int, _dp,
+                                                             _ip]
+        _check(L.orc_time_optimize(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                   _d(vertices.vals), _d(t), time_penalty, increment, max_evals,
+                                   _d(cost), ctypes.byref(evals)), "time_optimize")
     return t, float(cost[0]), evals.value
 
 

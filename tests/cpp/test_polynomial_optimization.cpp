@@ -597,6 +597,54 @@ TEST(gpu, MaximumOfMagnitude) {
   }
 }
 
+// Soft magnitude constraints on the callback (addMaximumMagnitudeConstraint
+// + use_soft_constraints, nonlinear_impl:847-875, 907-913, 2735-2766).
+TEST(gpu, SoftConstraintTimeCost) {
+  const Fixture f = kSeg10Dim3;
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.weights.w_c = 0.0;
+  p.max_iterations = 30;
+  PolynomialOptimizationNonLinear<10> opt(f.D, p);
+  opt.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}),
+                        f.r);
+  EXPECT_TRUE(opt.addMaximumMagnitudeConstraint(derivative_order::VELOCITY, 3.2));
+  EXPECT_TRUE(opt.addMaximumMagnitudeConstraint(derivative_order::ACCELERATION, 1.4));
+  const Dense d = toDense(vs, 5);
+  const int ders[2] = {1, 2};
+  const double lims[2] = {3.2, 1.4};
+  for (int mode = 0; mode <= 2; mode += 2) {
+    std::vector<double> g, og(f.S);
+    const double J = opt.evaluateTimeCost(times, mode, mode ? &g : nullptr);
+    double oJ = 0.0;
+    EXPECT_TRUE(orc_time_cost_soft(10, f.D, f.r, f.S, 5, d.mask.data(), d.vals.data(),
+                                   times.data(), p.time_penalty, mode, p.increment_time,
+                                   p.weights.w_d, p.weights.w_t, 2, ders, lims,
+                                   p.soft_constraint_weight, 1.0e12, &oJ, og.data()) == 0);
+    EXPECT_LE(relErr(J, oJ), 1e-9);
+    if (mode) EXPECT_LE(relErr(g, og), 1e-5);
+  }
+  // The optimiser sees the soft cost: the result's objective (with soft
+  // terms) is no larger than the start's, and the info splits it.
+  const double J0 = opt.evaluateTimeCost(times);
+  EXPECT_TRUE(opt.optimize() > 0);
+  std::vector<double> t1;
+  opt.getPolynomialOptimizationRef().getSegmentTimes(&t1);
+  const double J1 = opt.evaluateTimeCost(t1);
+  EXPECT_LE(J1, J0);
+  const OptimizationInfo info = opt.getOptimizationInfo();
+  EXPECT_LE(relErr(J1, info.cost_trajectory + info.cost_time + info.cost_soft_constraints),
+            1e-9);
+  EXPECT_TRUE(info.maxima.count(derivative_order::VELOCITY) == 1);
+  // Hard constraints are not available.
+  NonlinearOptimizationParameters hard = p;
+  hard.use_soft_constraints = false;
+  PolynomialOptimizationNonLinear<10> opt2(f.D, hard);
+  EXPECT_TRUE(!opt2.addMaximumMagnitudeConstraint(derivative_order::VELOCITY, 3.0));
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {

@@ -128,3 +128,72 @@ def test_time_optimize_properties(ctx, dev, oracle):
     # The reported cost is the objective at the returned times.
     chk = plan.time_cost(fd, out["times"])["cost"].cpu().numpy()
     assert np.allclose(chk, c1, rtol=1e-12)
+
+
+def _soft_limits(oracle, v, t):
+    """Limits 3% above the start trajectory's max |v| and |a|: the soft cost
+    is in its exponential regime (exp(100 * -0.03) ~ 0.05) and grows fast
+    when the optimiser shortens the segments."""
+    c = oracle.linear_solve(N, R, v, t)["coeffs"]
+    return [(1, 1.03 * oracle.max_magnitude(N, c, t, 1)["value"]),
+            (2, 1.03 * oracle.max_magnitude(N, c, t, 2)["value"])]
+
+
+@pytest.mark.parametrize("grad_mode", [0, 2])
+def test_time_cost_soft_constraints_vs_oracle(ctx, dev, oracle, grad_mode):
+    """objectiveFunctionTime with use_soft_constraints (nonlinear_impl:907-913):
+    J + sum_c min(1e12, exp((max_c - lim_c) / lim_c * 100))."""
+    import mav_tube_trajectory_generation_amd as mtg
+    S, B = 8, 8
+    mask, fixed, times, _ = _batch(S, B, 540)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    for b in range(B):
+        v = standard_vertices(N, S, D, 540 + b)
+        soft = _soft_limits(oracle, v, times[b])
+        out = plan.time_cost(fd[b:b + 1], td[b:b + 1], grad_mode=grad_mode, soft=soft)
+        J, g = oracle.time_cost(N, R, v, times[b], grad_mode=grad_mode, soft=soft)
+        J0, _ = oracle.time_cost(N, R, v, times[b])
+        assert J > J0  # the soft term is present
+        assert rel_err(float(out["cost"][0]), J) <= 1e-9, b
+        if grad_mode:
+            gg = out["grad"].cpu().numpy()[0]
+            assert np.max(np.abs(gg - g)) <= 1e-6 * np.max(np.abs(g)) + 1e-9, (b, gg, g)
+
+
+def test_time_optimize_soft_constraints_vs_oracle(ctx, dev, oracle):
+    """The device optimiser on the soft-constrained objective takes the same
+    steps as the oracle port (orc_time_optimize_soft)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    S, B, E = 6, 6, 20
+    mask, fixed, times, _ = _batch(S, B, 940)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    agree = 0
+    for b in range(B):
+        v = standard_vertices(N, S, D, 940 + b)
+        soft = _soft_limits(oracle, v, times[b])
+        out = plan.time_optimize(fd[b:b + 1], td[b:b + 1], max_evals=E, soft=soft)
+        T = out["times"].cpu().numpy()[0]
+        Tc, fc, ec = oracle.time_optimize(N, R, v, times[b], E, soft=soft)
+        # the reported cost is the soft objective at the returned times
+        chk = plan.time_cost(fd[b:b + 1], out["times"], soft=soft)["cost"].cpu().numpy()[0]
+        assert rel_err(float(out["cost"][0]), chk) <= 1e-12
+        if int(out["evals"][0]) == ec and np.max(np.abs(T - Tc) / Tc) <= 1e-6:
+            assert rel_err(float(out["cost"][0]), fc) <= 1e-6
+            agree += 1
+    # accept/reject decisions compare objectives whose soft terms amplify
+    # rounding by the weight (100); allow one divergent path in six
+    assert agree >= B - 1
+
+
+def test_time_soft_rejects_bad_constraints(ctx, dev):
+    import mav_tube_trajectory_generation_amd as mtg
+    from mav_tube_trajectory_generation_amd._abi import MTGError
+    S = 4
+    mask, fixed, times, _ = _batch(S, 1, 5)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    for soft in ([(5, 1.0)], [(1, 0.0)], [(-1, 1.0)], [(1, 1.0)] * 9):
+        with pytest.raises(MTGError):
+            plan.time_cost(fd, td, soft=soft)
