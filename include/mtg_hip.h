@@ -86,6 +86,18 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S,
                     const uint8_t* fixed_mask /* host (S+1)*M */,
                     mtg_plan** out);
 int mtg_plan_destroy(mtg_plan* plan);
+/* Kernel selection for mtg_linear_solve.  AUTO (default) runs the
+ * standard-pattern kernel when the pattern is the reference's standard one
+ * (start and end vertex fully fixed, intermediate vertices position only:
+ * createRandomVertices / makeStartOrEnd, vertex.cpp:27-82, 147-153) and
+ * 2 <= S <= 64, else the generic kernel.  GENERIC forces the generic kernel
+ * (parity cross-checks); STANDARD fails with MTG_ERR_UNSUPPORTED on other
+ * patterns.  mtg_plan_kernel returns the kernel a solve will run
+ * (GENERIC or STANDARD). */
+enum { MTG_KERNEL_AUTO = 0, MTG_KERNEL_GENERIC = 1, MTG_KERNEL_STANDARD = 2 };
+int mtg_plan_set_kernel(mtg_plan* plan, int kernel);
+int mtg_plan_kernel(const mtg_plan* plan);
+
 /* n_fixed / n_free per dimension (getNumberFixedConstraints /
  * getNumberFreeConstraints, polynomial_optimization_linear.h:224-226). */
 int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free);

@@ -56,6 +56,8 @@ SIGNATURES = {
                                        ctypes.c_int, _u8p, ctypes.POINTER(_vp)]),
     "mtg_plan_destroy": (ctypes.c_int, [_vp]),
     "mtg_plan_counts": (ctypes.c_int, [_vp, _ip, _ip]),
+    "mtg_plan_set_kernel": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "mtg_plan_kernel": (ctypes.c_int, [_vp]),
     "mtg_linear_solve": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mtg_linear_solve_host": (ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, _dp, _dp,
                                              _i32p]),

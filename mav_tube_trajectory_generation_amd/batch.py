@@ -75,6 +75,21 @@ class LinearPlan:
         check(lib().mtg_plan_counts(self._h, ctypes.byref(nf), ctypes.byref(np_)), "counts")
         self.n_fixed, self.n_free = nf.value, np_.value
 
+    KERNELS = {"auto": 0, "generic": 1, "standard": 2}
+
+    def set_kernel(self, which):
+        """Select the linear-solve kernel: "auto" (default), "generic", or
+        "standard" (the standard-pattern kernel; MTGError on other patterns)."""
+        check(lib().mtg_plan_set_kernel(self._h, self.KERNELS[which]), "mtg_plan_set_kernel")
+        return self
+
+    @property
+    def kernel(self):
+        """Kernel a solve runs: "generic" or "standard"."""
+        k = lib().mtg_plan_kernel(self._h)
+        check(min(k, 0), "mtg_plan_kernel")
+        return {1: "generic", 2: "standard"}[k]
+
     def close(self):
         if self._h:
             lib().mtg_plan_destroy(self._h)

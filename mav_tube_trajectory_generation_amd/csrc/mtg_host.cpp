@@ -249,8 +249,16 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fix
     (void)hipFree(p->d_fixed_map);
     return MTG_ERR_HIP;
   }
+  // Standard pattern (createRandomVertices / makeStartOrEnd, vertex.cpp:
+  // 27-82, 147-153): start and end fully fixed, intermediate positions only.
+  bool std_pattern = S >= 2 && S <= mtg::kMaxStdS;
+  for (int v = 0; v <= S && std_pattern; ++v)
+    for (int k = 0; k < M; ++k) {
+      const bool want = (v == 0 || v == S) ? true : (k == 0);
+      if ((fixed_mask[v * M + k] != 0) != want) std_pattern = false;
+    }
   p->dev = PlanDev{N, D, r, S, nf, np, tab, p->d_slots, p->d_free_map, p->d_fixed_map,
-                   fmask, use_mask ? 1 : 0};
+                   fmask, use_mask ? 1 : 0, std_pattern ? 1 : 0, MTG_KERNEL_AUTO};
   *out = p.release();
   return MTG_OK;
 }
@@ -262,6 +270,19 @@ int mtg_plan_destroy(mtg_plan* plan) {
   (void)hipFree(plan->d_fixed_map);
   delete plan;
   return MTG_OK;
+}
+
+int mtg_plan_set_kernel(mtg_plan* plan, int kernel) {
+  if (!plan || kernel < MTG_KERNEL_AUTO || kernel > MTG_KERNEL_STANDARD)
+    return MTG_ERR_INVALID_ARG;
+  if (kernel == MTG_KERNEL_STANDARD && !plan->dev.std_pattern) return MTG_ERR_UNSUPPORTED;
+  plan->dev.kernel = kernel;
+  return MTG_OK;
+}
+
+int mtg_plan_kernel(const mtg_plan* plan) {
+  if (!plan) return MTG_ERR_INVALID_ARG;
+  return mtg::use_std_kernel(plan->dev) ? MTG_KERNEL_STANDARD : MTG_KERNEL_GENERIC;
 }
 
 int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free) {

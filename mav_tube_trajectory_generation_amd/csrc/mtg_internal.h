@@ -21,7 +21,20 @@ struct PlanDev {
   const int* fixed_map;    // nf: fixed index f -> v*M + k
   uint64_t fmask;          // bit v*M+k set iff fixed, valid when use_mask
   int use_mask;            // (S+1)*M <= 64
+  int std_pattern;         // 1: standard pattern (start/end fully fixed,
+                           // intermediate positions only), 2 <= S <= kMaxStdS
+  int kernel;              // MTG_KERNEL_* choice (mtg_plan_set_kernel)
 };
+
+// Standard-pattern linear solve (mtg_linear_std.hip).
+constexpr int kMaxStdS = 64;
+hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
+                                   const double* times, double* coeffs, double* cost,
+                                   double* free_vals, int32_t* status, hipStream_t st);
+size_t linear_std_lds_bytes(int N, int S, int D);
+inline bool use_std_kernel(const PlanDev& pl) {
+  return pl.std_pattern && pl.kernel != MTG_KERNEL_GENERIC;
+}
 
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,

@@ -465,6 +465,8 @@ static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* 
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,
                                double* free_vals, int32_t* status, hipStream_t st) {
+  if (use_std_kernel(pl))
+    return launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st);
 #define CALL(n) launch_linear_n<n>(pl, B, df, times, coeffs, cost, free_vals, status, st)
   MTG_DISPATCH_N(pl.N, CALL)
 #undef CALL

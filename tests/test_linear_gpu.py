@@ -15,11 +15,19 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _solve_gpu(ctx, dev, N, r, mask, df_batch, times_batch):
+@pytest.fixture(params=["auto", "generic"])
+def kernel(request):
+    """Every parity case runs twice: with the kernel AUTO selects (the
+    standard-pattern kernel wherever the pattern allows it) and with the
+    generic kernel forced."""
+    return request.param
+
+
+def _solve_gpu(ctx, dev, N, r, mask, df_batch, times_batch, kernel="auto"):
     import mav_tube_trajectory_generation_amd as mtg
     S = times_batch.shape[1]
     D = df_batch.shape[1]
-    plan = mtg.LinearPlan(ctx, N, D, r, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, r, S, mask).set_kernel(kernel)
     out = plan.solve(torch.from_numpy(np.ascontiguousarray(df_batch)).to(dev),
                      torch.from_numpy(np.ascontiguousarray(times_batch)).to(dev), free=True)
     torch.cuda.synchronize()
@@ -53,13 +61,13 @@ REF_PARAMS = [
 
 
 @pytest.mark.parametrize("D,r,S,seed,vmax,amax", REF_PARAMS)
-def test_reference_fixture_parity(ctx, dev, oracle, D, r, S, seed, vmax, amax):
+def test_reference_fixture_parity(ctx, dev, oracle, D, r, S, seed, vmax, amax, kernel):
     N = 10
     v = standard_vertices(N, S, D, seed)
     times = oracle.estimate_segment_times(v, vmax, amax)
     ref = oracle.linear_solve(N, r, v, times)
     mask, df = compact_fixed(v, N)
-    _, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None])
+    _, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None], kernel)
     assert out["status"][0] == 0
     assert rel_err_coeffs(out["coeffs"][0], ref["coeffs"]) <= REL_TOL
     assert rel_err(out["cost"][0], ref["cost"]) <= REL_TOL
@@ -82,7 +90,7 @@ def _exact_cases():
 
 
 @pytest.mark.parametrize("case", _exact_cases(), ids=lambda c: f"N{c['N']}_r{c['r']}")
-def test_orders_vs_exact(ctx, dev, oracle, case):
+def test_orders_vs_exact(ctx, dev, oracle, case, kernel):
     """Every supported N (4..12) and derivative order against the exact
     rational solution (tests/golden/make_exact.py).  Where the
     reference-faithful oracle is itself accurate (< 1e-7 from the truth) the
@@ -93,7 +101,7 @@ def test_orders_vs_exact(ctx, dev, oracle, case):
     times = np.array(case["times"])
     exact = np.array(case["exact"])
     mask, df = compact_fixed(v, N)
-    _, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None])
+    _, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None], kernel)
     assert out["status"][0] == 0
     gpu_err = rel_err_coeffs(out["coeffs"][0], exact)
     assert gpu_err <= max(REL_TOL, 2.0 * case["oracle_err"]), gpu_err
@@ -104,7 +112,7 @@ def test_orders_vs_exact(ctx, dev, oracle, case):
 
 
 @pytest.mark.parametrize("N", [4, 6, 8, 12])
-def test_other_orders_3d(ctx, dev, oracle, N):
+def test_other_orders_3d(ctx, dev, oracle, N, kernel):
     """3-D problems at the orders where FP64 resolves the solution."""
     D, S = 3, 6
     for r in range(max(0, N // 2 - 3), N // 2):
@@ -112,7 +120,7 @@ def test_other_orders_3d(ctx, dev, oracle, N):
         times = oracle.estimate_segment_times(v, 3.0, 5.0)
         ref = oracle.linear_solve(N, r, v, times)
         mask, df = compact_fixed(v, N)
-        _, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None])
+        _, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None], kernel)
         assert out["status"][0] == 0, (N, r)
         tol = 1e-5 if (N == 12 and r == 3) else REL_TOL
         assert rel_err_coeffs(out["coeffs"][0], ref["coeffs"]) <= tol, (N, r)
@@ -134,7 +142,8 @@ def test_irregular_patterns(ctx, dev, oracle):
         times = rng.uniform(0.5, 6.0, size=S)
         ref = oracle.linear_solve(N, r, v, times)
         mask, df = compact_fixed(v, N)
-        _, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None])
+        plan, out = _solve_gpu(ctx, dev, N, r, mask, df[None], times[None])
+        assert plan.kernel == "generic"
         assert out["status"][0] == 0
         assert rel_err_coeffs(out["coeffs"][0], ref["coeffs"]) <= REL_TOL, D
         assert rel_err(out["cost"][0], ref["cost"]) <= REL_TOL, D
@@ -154,12 +163,12 @@ def test_fully_constrained(ctx, dev, oracle):
     assert rel_err_coeffs(out["coeffs"][0], ref["coeffs"]) <= REL_TOL
 
 
-def test_config2_batch(ctx, dev, oracle):
+def test_config2_batch(ctx, dev, oracle, kernel):
     """BASELINE config 2: 1024 x 10-segment N=10 3-D minimum snap."""
     import mav_tube_trajectory_generation_amd as mtg
     N, D, S, B = 10, 3, 10, 1024
     mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=105)
-    _, out = _solve_gpu(ctx, dev, N, 4, mask, fixed, times)
+    _, out = _solve_gpu(ctx, dev, N, 4, mask, fixed, times, kernel)
     assert (out["status"] == 0).all()
     for b in list(range(0, B, 37)) + [B - 1]:
         v = standard_vertices(N, S, D, 105 + b)
@@ -182,13 +191,13 @@ def test_config2_batch(ctx, dev, oracle):
     assert np.allclose(c[:, 0, :, 0], fixed[:, :, 0], atol=1e-12)
 
 
-def test_bad_time_status(ctx, dev):
+def test_bad_time_status(ctx, dev, kernel):
     import mav_tube_trajectory_generation_amd as mtg
     N, D, S, B = 10, 3, 4, 3
     mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=1)
     times[1, 2] = 0.0
     times[2, 0] = -1.0
-    _, out = _solve_gpu(ctx, dev, N, 4, mask, fixed, times)
+    _, out = _solve_gpu(ctx, dev, N, 4, mask, fixed, times, kernel)
     assert list(out["status"]) == [0, 1, 1]
     assert np.isnan(out["cost"][1]) and np.isfinite(out["cost"][0])
 
@@ -260,7 +269,10 @@ def test_coefficients_from_constraints(ctx, dev, oracle):
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
     assert rel_err_coeffs(c.cpu().numpy(), out["coeffs"]) <= 1e-12
-    assert np.max(np.abs(cost.cpu().numpy() - out["cost"]) / out["cost"]) <= 1e-12
+    # The solve (standard-pattern kernel) and the recovery (generic
+    # formulation) sum the quadratic form in different orders; the form
+    # cancels, so the round trip is held to 1e-9, not the rounding floor.
+    assert np.max(np.abs(cost.cpu().numpy() - out["cost"]) / out["cost"]) <= 1e-9
     rng = np.random.default_rng(3)
     dp = out["free"] + rng.normal(0.0, 0.3, out["free"].shape)
     c2, cost2, _ = plan.coefficients(T(fixed), T(dp), T(times))
@@ -275,3 +287,57 @@ def test_coefficients_from_constraints(ctx, dev, oracle):
             want = (m["Ainv"] @ m["M"] @ dall).reshape(S, N)
             assert rel_err_coeffs(c2[b, :, d], want) <= 1e-9, (b, d)
         assert nf == m["M"].shape[1] - dp.shape[2]
+
+
+@pytest.mark.parametrize("N,D,S", [(10, 3, 2), (10, 3, 3), (10, 3, 4), (10, 3, 9), (10, 3, 10),
+                                   (10, 3, 17), (10, 3, 18), (10, 3, 33), (10, 3, 64),
+                                   (10, 1, 10), (10, 2, 7), (10, 4, 10), (8, 3, 10),
+                                   (6, 3, 12), (12, 3, 10), (4, 3, 10)])
+def test_standard_kernel_matches_generic(ctx, dev, oracle, N, D, S):
+    """The standard-pattern kernel against the generic kernel (and spot
+    checks against the oracle) on a random batch: every S parity of the
+    twisted sweep, S*D beyond one wave, every N and D.  Same inputs, same
+    algorithm family: agreement to 1e-9 normwise."""
+    import mav_tube_trajectory_generation_amd as mtg
+    B = 64
+    r = N // 2 - 1
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=1000 + S)
+    plan_s, out_s = _solve_gpu(ctx, dev, N, r, mask, fixed, times, "standard")
+    plan_g, out_g = _solve_gpu(ctx, dev, N, r, mask, fixed, times, "generic")
+    assert plan_s.kernel == "standard" and plan_g.kernel == "generic"
+    assert (out_s["status"] == 0).all() and (out_g["status"] == 0).all()
+    tol = 1e-9 if N <= 10 else 1e-6
+    worse = []
+    for b in range(B):
+        assert rel_err_coeffs(out_s["coeffs"][b], out_g["coeffs"][b]) <= tol, b
+        assert rel_err_coeffs(out_s["free"][b], out_g["free"][b]) <= tol, b
+        # The cost is a cancelling quadratic form summed in a different order
+        # by the two kernels (symmetric half vs full rows).
+        assert rel_err(out_s["cost"][b], out_g["cost"][b]) <= 100 * tol, b
+        v = standard_vertices(N, S, D, 1000 + S + b)
+        ref = oracle.linear_solve(N, r, v, times[b])
+        assert rel_err_coeffs(out_s["coeffs"][b], ref["coeffs"]) <= REL_TOL, b
+        assert rel_err(out_s["cost"][b], ref["cost"]) <= REL_TOL, b
+        worse.append(rel_err(out_s["cost"][b], ref["cost"]) /
+                     max(rel_err(out_g["cost"][b], ref["cost"]), 1e-15))
+    # No systematic accuracy loss against the oracle.
+    assert np.median(worse) <= 10.0, np.median(worse)
+
+
+def test_kernel_selection(ctx):
+    """AUTO picks the standard-pattern kernel exactly on the standard
+    pattern; STANDARD is refused elsewhere."""
+    import mav_tube_trajectory_generation_amd as mtg
+    N, D, S = 10, 3, 10
+    mask = np.zeros((S + 1, 5), np.uint8)
+    mask[0, :] = mask[S, :] = 1
+    mask[1:S, 0] = 1
+    assert mtg.LinearPlan(ctx, N, D, 4, S, mask).kernel == "standard"
+    assert mtg.LinearPlan(ctx, N, D, 4, S, mask).set_kernel("generic").kernel == "generic"
+    odd = mask.copy()
+    odd[3, 0] = 0
+    p = mtg.LinearPlan(ctx, N, D, 4, S, odd)
+    assert p.kernel == "generic"
+    with pytest.raises(mtg.MTGError):
+        p.set_kernel("standard")
+    assert mtg.LinearPlan(ctx, N, D, 4, 1, np.ones((2, 5), np.uint8)).kernel == "generic"
