@@ -1,0 +1,58 @@
+"""Phase timing of workgroup 0 of the standard-pattern linear kernel from the
+diagnostic build (make STAMPS=1 STAMPS_OUT=...):
+
+MTG_LIB_PATH=mav_tube_trajectory_generation_amd/libmtg_hip_stamps.so \
+    python tools/stamps_std.py [B]
+Slots (mtg_linear_std.hip): 0 start, 1 inputs+powers, 2 assembly,
+100+2k sweep step k start, 3 sweep end, 4 middle vertex, 5 back
+substitution, 6 coefficients/cost/stores.
+"""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    import numpy as np
+    import torch
+    import mav_tube_trajectory_generation_amd as mtg
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    N, D, r, S = 10, 3, 4, 10
+    dev = torch.device("cuda", 0)
+    ctx = mtg.Context(0)
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=105)
+    plan = mtg.LinearPlan(ctx, N, D, r, S, mask)
+    assert plan.kernel == "standard"
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    out = plan.solve(fd, td)
+    L = mtg.lib()
+    L.mtg_debug_stamps_std.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    runs = []
+    for _ in range(7):
+        plan.solve(fd, td, out=out)
+        torch.cuda.synchronize()
+        st = (ctypes.c_ulonglong * 512)()
+        L.mtg_debug_stamps_std(st, 512)
+        runs.append(np.array(st[:], dtype=np.int64))
+    st = np.median(np.array(runs), axis=0)
+    order = [(0, "start"), (7, "inputs arrived, fixed stored"), (1, "powers"),
+             (2, "assembly")]
+    k = 0
+    while st[100 + 2 * k] > 0:
+        order.append((100 + 2 * k, f"(sweep step {k} start)"))
+        k += 1
+    order += [(3, "sweep end"), (4, "middle vertex solve"), (5, "back substitution"),
+              (6, "coeffs + cost + stores")]
+    print(f"phase cycles (workgroup 0, median of 7, B={B}):")
+    prev = st[0]
+    for slot, name in order[1:]:
+        print(f"  {name:>24}: {st[slot] - prev:8.0f}")
+        prev = st[slot]
+    print(f"  total: {st[6] - st[0]:.0f} cycles")
+
+
+if __name__ == "__main__":
+    main()
