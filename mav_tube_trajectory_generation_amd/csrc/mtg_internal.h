@@ -32,6 +32,16 @@ hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* d
                                    const double* times, double* coeffs, double* cost,
                                    double* free_vals, int32_t* status, hipStream_t st);
 size_t linear_std_lds_bytes(int N, int S, int D);
+// Standard-pattern time kernels (mtg_time_std.hip): N = 10, r = 2..4, D = 1..3.
+bool has_time_std(const PlanDev& pl);
+hipError_t launch_time_cost_std(const PlanDev& pl, int64_t B, const double* df,
+                                const double* times, const mtg_time_params& p, double* cost,
+                                double* grad, int32_t* status, hipStream_t st);
+hipError_t launch_time_optimize_std(const PlanDev& pl, int64_t B, const double* df,
+                                    double* times, const mtg_time_params& p, int max_evals,
+                                    double* cost, int32_t* evals, int32_t* status,
+                                    hipStream_t st);
+size_t time_std_lds_bytes(int N, int S, int D, bool soft);
 inline bool use_std_kernel(const PlanDev& pl) {
   return pl.std_pattern && pl.kernel != MTG_KERNEL_GENERIC;
 }

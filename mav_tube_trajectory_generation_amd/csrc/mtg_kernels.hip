@@ -485,6 +485,7 @@ hipError_t launch_time_cost(const PlanDev& pl, int64_t B, const double* df,
                             const double* times, const mtg_time_params& p,
                             double* cost, double* grad, int32_t* status,
                             hipStream_t st) {
+  if (has_time_std(pl)) return launch_time_cost_std(pl, B, df, times, p, cost, grad, status, st);
 #define CALL(n) launch_time_cost_n<n>(pl, B, df, times, p, cost, grad, status, st)
   MTG_DISPATCH_N(pl.N, CALL)
 #undef CALL
@@ -494,6 +495,8 @@ hipError_t launch_time_optimize(const PlanDev& pl, int64_t B, const double* df,
                                 double* times, const mtg_time_params& p, int max_evals,
                                 double* cost, int32_t* evals, int32_t* status,
                                 hipStream_t st) {
+  if (has_time_std(pl))
+    return launch_time_optimize_std(pl, B, df, times, p, max_evals, cost, evals, status, st);
 #define CALL(n) launch_time_opt_n<n>(pl, B, df, times, p, max_evals, cost, evals, status, st)
   MTG_DISPATCH_N(pl.N, CALL)
 #undef CALL

@@ -1,0 +1,326 @@
+// mtg_time_std.hip — the time-allocation objective and the batched
+// segment-time optimiser (objectiveFunctionTime / getCostAndGradientTime /
+// optimizeTime, nonlinear_impl:877-945, 2495-2584, 332-397) for the standard
+// vertex pattern, on the standard-pattern solver (stdp::Solver,
+// mtg_std_device.h).  Same objective, gradient modes and optimiser state
+// machine as the generic kernels (mtg_kernels.hip: time_cost_kernel,
+// time_optimize_kernel); instantiated for N = 10, r = 2..4, D = 1..3 (other
+// combinations run the generic kernels).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "mtg_extrema_device.h"
+#include "mtg_std_device.h"
+
+namespace mtg {
+
+namespace {
+
+template <int N, int R, int D>
+using StdSv = stdp::Solver<N, R, D>;
+
+// J(T) = computeCost() + time_penalty (sum T)^2 [+ soft constraints] at the
+// times T (LDS, S values).  Every lane calls it; returns the wave-uniform J
+// (NaN and *bad set when a time is invalid).  kSoft: the coefficients go to
+// cbuf (LDS) and evaluateMaximumMagnitudeAsSoftConstraint
+// (nonlinear_impl:2735-2766) runs one extremum search per constraint.
+template <int N, int R, int D, bool kSoft>
+__device__ double std_objective(StdSv<N, R, D>& sv, const double* __restrict__ tab,
+                                const double* T, const mtg_time_params& p, double* cbuf,
+                                bool* bad, bool* not_spd) {
+  __syncthreads();
+  const bool b = sv.powers_from(T);
+  __syncthreads();
+  if (b) {
+    *bad = true;
+    return NAN;
+  }
+  sv.assemble(tab);
+  __syncthreads();
+  *not_spd = sv.solve() || *not_spd;
+  double J = sv.coeff_cost(kSoft ? cbuf : nullptr);
+  double tot = 0.0;
+  for (int i = 0; i < sv.S; ++i) tot += T[i];  // nonlinear_impl:2768-2774
+  J += tot * tot * p.time_penalty;
+  if constexpr (kSoft) {
+    __syncthreads();
+    double soft = 0.0;
+    for (int c = 0; c < p.n_soft; ++c) {
+      int K = 0;
+      double lim = 1.0;
+#pragma unroll
+      for (int cc = 0; cc < kMaxSoftConstraints; ++cc)  // compile-time indices
+        if (cc == c) {
+          K = p.soft_derivative[cc];
+          lim = p.soft_limit[cc];
+        }
+      const double m = ext_trajectory_max_wave_k<N>(K, cbuf, T, sv.S, D, sv.lane);
+      const double relative_violation = (m - lim) / lim;
+      soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
+    }
+    J += soft;
+  }
+  return J;
+}
+
+// Loads d_f into the solver (all lanes).
+template <int N, int R, int D>
+__device__ void std_load_fixed(StdSv<N, R, D>& sv, const double* __restrict__ fb) {
+  const int nf = sv.nf;
+  for (int i = sv.lane; i < D * nf; i += kWave) sv.put_fixed(i, fb[i]);
+}
+
+// Central-difference point gi (0 .. 2S-1) around base times Tb: segment
+// n = gi / 2 at T_n - inc (even gi) or T_n + inc (odd), both clamped to 0.1
+// when T_n <= 0.1 (nonlinear_impl:2529-2530).
+__device__ inline void std_set_fd_point(double* T, const double* Tb, int S, int gi, double inc,
+                                        int lane) {
+  const int n = gi >> 1;
+  for (int i = lane; i < S; i += kWave) {
+    const double Tn = Tb[i];
+    T[i] = i != n ? Tn : (Tn <= 0.1 ? 0.1 : ((gi & 1) ? Tn + inc : Tn - inc));
+  }
+}
+
+}  // namespace
+
+size_t time_std_lds_bytes(int N, int S, int D, bool soft) {
+  const size_t base = sizeof(double) * static_cast<size_t>(stdp::layout(N, S, D).n);
+  return soft ? (base + 15) / 16 * 16 + sizeof(double) * S * D * N : base;
+}
+
+template <int N, int R, int D, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_cost_std_kernel(
+    int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    const double* __restrict__ times, mtg_time_params p, double* __restrict__ cost,
+    double* __restrict__ grad, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int64_t b = blockIdx.x;
+  StdSv<N, R, D> sv;
+  sv.init(S, smem, tab);
+  const int lane = sv.lane;
+  double* cbuf = smem + (sv.L.n + 1) / 2 * 2;
+  double* T = sv.aux();  // evaluation point
+  double* Tb = T + S;    // base times
+  double* g = Tb + S;    // gradient
+  double* E = g + S;     // 2S segment energies (grad_mode 1)
+  std_load_fixed(sv, fixed_vals + b * D * sv.nf);
+  for (int i = lane; i < S; i += kWave) T[i] = Tb[i] = times[b * S + i];
+  const bool fd = grad && p.grad_mode == 2;
+  const int nevals = 1 + (fd ? 2 * S : 0);
+  double J0 = 0.0, Jlo = 0.0;
+  bool bad = false, not_spd = false;
+  for (int e = 0; e < nevals; ++e) {
+    if (e > 0) std_set_fd_point(T, Tb, S, e - 1, p.increment, lane);
+    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd);
+    if (e == 0) {
+      J0 = J;
+      if (bad) break;
+    } else if ((e - 1) & 1) {
+      if (lane == 0) g[(e - 1) >> 1] = (J - Jlo) / (2.0 * p.increment);
+    } else {
+      Jlo = J;
+    }
+  }
+  __syncthreads();
+  if (grad && p.grad_mode == 1 && !bad) {
+    // getCostAndGradientTime (nonlinear_impl:2495-2584): d held at the base
+    // solution, only segment n's block of J_d = d^T R d changes.
+    const double inc = p.increment;
+    for (int i = lane; i < 2 * S; i += kWave) {
+      const int n = i >> 1;
+      const double Tn = Tb[n];
+      const double tau = Tn <= 0.1 ? 0.1 : ((i & 1) ? Tn + inc : Tn - inc);
+      E[i] = sv.seg_energy(n, tau);
+    }
+    __syncthreads();
+    for (int n = lane; n < S; n += kWave)
+      g[n] = p.w_d * (E[2 * n + 1] - E[2 * n]) / (2.0 * inc) + p.w_t * 1.0;
+    __syncthreads();
+  }
+  if (lane == 0) {
+    if (cost) cost[b] = bad ? NAN : J0;
+    if (status)
+      status[b] = bad ? MTG_TRAJ_BAD_TIME : (not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
+  }
+  if (grad && p.grad_mode != 0)
+    for (int i = lane; i < S; i += kWave) grad[b * S + i] = bad ? NAN : g[i];
+}
+
+// Batched segment-time optimisation (optimizeTime, nonlinear_impl:332-397):
+// bounds [0.1, 2 T0]; projected, scaled steepest descent on the grad_mode 2
+// gradient with an expand/backtrack step rule; `max_evals` objective
+// evaluations (NLopt maxeval semantics, nonlinear_impl:101; gradient
+// evaluations are not counted).  A state machine with one objective call
+// site, as time_optimize_kernel.
+template <int N, int R, int D, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
+    int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    double* __restrict__ times_io, mtg_time_params p, int max_evals,
+    double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int64_t b = blockIdx.x;
+  StdSv<N, R, D> sv;
+  sv.init(S, smem, tab);
+  const int lane = sv.lane;
+  double* cbuf = smem + (sv.L.n + 1) / 2 * 2;
+  double* T = sv.aux();   // evaluation point
+  double* Tcur = T + S;   // accepted times
+  double* T0 = Tcur + S;  // initial times (bounds)
+  double* g = T0 + S;     // gradient at Tcur
+  std_load_fixed(sv, fixed_vals + b * D * sv.nf);
+  for (int i = lane; i < S; i += kWave) T[i] = Tcur[i] = T0[i] = times_io[b * S + i];
+  constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
+  enum { kBase, kGrad, kTrial, kDone };
+  int phase = kBase, gi = 0, evals = 0;
+  double f = 0.0, Jlo = 0.0;
+  double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
+  bool bad = false, not_spd = false;
+  while (phase != kDone) {
+    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd);
+    if (phase == kBase) {
+      f = J;
+      evals = 1;
+      if (bad) break;
+      phase = kGrad;
+      gi = 0;
+    } else if (phase == kGrad) {
+      if (gi & 1) {
+        if (lane == 0) g[gi >> 1] = (J - Jlo) / (2.0 * p.increment);
+      } else {
+        Jlo = J;
+      }
+      if (++gi == 2 * S) phase = kTrial;
+    } else {  // trial point
+      ++evals;
+      if (J < f) {
+        f = J;
+        for (int i = lane; i < S; i += kWave) Tcur[i] = T[i];
+        alpha = fmin(alpha * 1.5, 1.0);
+        phase = kGrad;
+        gi = 0;
+      } else {
+        alpha *= 0.5;
+      }
+    }
+    __syncthreads();
+    // Next evaluation point.
+    if (phase == kGrad) {
+      std_set_fd_point(T, Tcur, S, gi, p.increment, lane);
+    } else if (phase == kTrial) {
+      if (!(evals < max_evals && alpha > 1e-9)) break;
+      // Scaled direction -g_n T0_n, normalised so the largest relative move
+      // is alpha.
+      double gmax = 0.0;
+      for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(g[i] * T0[i]));
+      if (!(gmax > 0.0)) break;
+      int moved = 0;
+      for (int i = 0; i < S; ++i) {
+        const double step = alpha * T0[i] * (g[i] * T0[i]) / gmax;
+        double tn = Tcur[i] - step;
+        tn = fmin(fmax(tn, kLower), 2.0 * T0[i]);
+        if (tn != Tcur[i]) moved = 1;
+        if (lane == 0) T[i] = tn;
+      }
+      __syncthreads();
+      if (!moved) break;
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < S; i += kWave) times_io[b * S + i] = Tcur[i];
+  if (lane == 0) {
+    if (cost) cost[b] = bad ? NAN : f;
+    if (evals_out) evals_out[b] = evals;
+    if (status)
+      status[b] = bad ? MTG_TRAJ_BAD_TIME : (not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
+  }
+}
+
+namespace {
+template <typename K>
+hipError_t prepare_lds_std(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(bytes));
+  return hipSuccess;
+}
+
+template <int N, int R, int D>
+hipError_t time_cost_nrd(const PlanDev& pl, int64_t B, const double* df, const double* times,
+                         const mtg_time_params& p, double* cost, double* grad, int32_t* status,
+                         hipStream_t st) {
+  const bool soft = p.n_soft > 0;
+  const size_t bytes = time_std_lds_bytes(N, pl.S, D, soft);
+  if (soft) {
+    hipError_t e = prepare_lds_std(time_cost_std_kernel<N, R, D, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_cost_std_kernel<N, R, D, true>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl.S, pl.tab, df, times, p, cost, grad, status);
+  } else {
+    hipError_t e = prepare_lds_std(time_cost_std_kernel<N, R, D, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_cost_std_kernel<N, R, D, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl.S, pl.tab, df, times, p, cost, grad, status);
+  }
+  return hipGetLastError();
+}
+
+template <int N, int R, int D>
+hipError_t time_opt_nrd(const PlanDev& pl, int64_t B, const double* df, double* times,
+                        const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
+                        int32_t* status, hipStream_t st) {
+  const bool soft = p.n_soft > 0;
+  const size_t bytes = time_std_lds_bytes(N, pl.S, D, soft);
+  if (soft) {
+    hipError_t e = prepare_lds_std(time_optimize_std_kernel<N, R, D, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_optimize_std_kernel<N, R, D, true>),
+                       dim3(static_cast<unsigned>(B)), dim3(kWave), bytes, st, pl.S, pl.tab,
+                       df, times, p, max_evals, cost, evals, status);
+  } else {
+    hipError_t e = prepare_lds_std(time_optimize_std_kernel<N, R, D, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_optimize_std_kernel<N, R, D, false>),
+                       dim3(static_cast<unsigned>(B)), dim3(kWave), bytes, st, pl.S, pl.tab,
+                       df, times, p, max_evals, cost, evals, status);
+  }
+  return hipGetLastError();
+}
+}  // namespace
+
+bool has_time_std(const PlanDev& pl) {
+  return use_std_kernel(pl) && pl.N == 10 && pl.r >= 2 && pl.r <= 4 && pl.D >= 1 && pl.D <= 3;
+}
+
+#define MTG_TIME_STD_DISPATCH(FN, ...)                          \
+  switch (pl.r * 4 + pl.D) {                                    \
+    case 2 * 4 + 1: return FN<10, 2, 1>(__VA_ARGS__);           \
+    case 2 * 4 + 2: return FN<10, 2, 2>(__VA_ARGS__);           \
+    case 2 * 4 + 3: return FN<10, 2, 3>(__VA_ARGS__);           \
+    case 3 * 4 + 1: return FN<10, 3, 1>(__VA_ARGS__);           \
+    case 3 * 4 + 2: return FN<10, 3, 2>(__VA_ARGS__);           \
+    case 3 * 4 + 3: return FN<10, 3, 3>(__VA_ARGS__);           \
+    case 4 * 4 + 1: return FN<10, 4, 1>(__VA_ARGS__);           \
+    case 4 * 4 + 2: return FN<10, 4, 2>(__VA_ARGS__);           \
+    case 4 * 4 + 3: return FN<10, 4, 3>(__VA_ARGS__);           \
+    default: return hipErrorInvalidValue;                       \
+  }
+
+hipError_t launch_time_cost_std(const PlanDev& pl, int64_t B, const double* df,
+                                const double* times, const mtg_time_params& p, double* cost,
+                                double* grad, int32_t* status, hipStream_t st) {
+  if (!has_time_std(pl)) return hipErrorInvalidValue;
+  MTG_TIME_STD_DISPATCH(time_cost_nrd, pl, B, df, times, p, cost, grad, status, st)
+}
+
+hipError_t launch_time_optimize_std(const PlanDev& pl, int64_t B, const double* df,
+                                    double* times, const mtg_time_params& p, int max_evals,
+                                    double* cost, int32_t* evals, int32_t* status,
+                                    hipStream_t st) {
+  if (!has_time_std(pl)) return hipErrorInvalidValue;
+  MTG_TIME_STD_DISPATCH(time_opt_nrd, pl, B, df, times, p, max_evals, cost, evals, status, st)
+}
+
+}  // namespace mtg
