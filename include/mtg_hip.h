@@ -207,6 +207,45 @@ int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Free-derivative objectives of PolynomialOptimizationNonLinear (the NLopt
+ * callbacks of kOptimizeFreeConstraints / kOptimizeFreeConstraintsAndTime),
+ * for any constraint pattern of the plan (the fork's nonlinear class uses the
+ * tube pattern: start/end fully fixed, every intermediate derivative free,
+ * qcqp_impl:95-117).  params: time_penalty and the soft-constraint fields of
+ * mtg_time_params (increment, w_d, w_t, grad_mode unused).
+ *   mode 0  objectiveFunctionFreeConstraints (nonlinear_impl:1021-1113):
+ *           J = J_d [+ soft], J_d = sum_dim d^T R d (getCostAndGradientDerivative,
+ *           :1537-1606) = 2 computeCost(); grad (nullable) = dJ_d/dd_p =
+ *           2 (R_pf d_f + R_pp d_p) per dimension (:1591-1592; the soft term
+ *           is not differentiated, :1100-1110).
+ *   mode 1  objectiveFunctionTimeAndConstraints (:947-1019): with the given
+ *           times and d_p (no re-solve), J = computeCost() + time_penalty
+ *           (sum T)^2 [+ soft]; no gradient (the reference CHECKs it empty).
+ * Inputs (device): fixed_vals B x D x n_fixed, free_vals B x D x n_free
+ * (dimension-major, the x layout of :1040-1052), times B x S.
+ * Outputs (device, nullable): cost B, grad B x D x n_free (mode 0), status B.
+ */
+int mtg_free_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                  const double* free_vals, const double* times,
+                  const mtg_time_params* params, int mode, double* cost, double* grad,
+                  int32_t* status, void* stream);
+
+/* Batched optimisation of the free derivatives (optimizeFreeConstraints,
+ * nonlinear_impl:399-493, objective of mode 0).  NLopt is not available; the
+ * device optimiser takes projected Newton steps of the quadratic J_d,
+ * d <- clamp(d + alpha (d* - d), lower, upper) with d* = argmin J_d from the
+ * linear solve, alpha = 1, x1.5 (capped at 1) on a decrease of J, x0.5
+ * otherwise, until `max_evals` objective evaluations or a step below
+ * 1e-13 (1 + |d|).  lower / upper: B x D x n_free bounds
+ * (setFreeEndpointDerivativeHardConstraints, :2858-2905) or NULL.
+ *   free_io  B x D x n_free   in: initial d_p, out: optimised d_p
+ *   cost     B                final objective; evals B (nullable) */
+int mtg_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                      double* free_io, const double* times, const double* lower,
+                      const double* upper, const mtg_time_params* params, int max_evals,
+                      double* cost, int32_t* evals, int32_t* status, void* stream);
+
+/* ------------------------------------------------------------------------
  * Tube QCQP (PolynomialOptimizationConstrained<N>, qcqp_impl).  The tube
  * pattern is fixed by the reference: start and end vertices fully fixed
  * (derivatives 0..M-1), every intermediate derivative free, including

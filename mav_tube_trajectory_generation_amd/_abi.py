@@ -57,6 +57,12 @@ SIGNATURES = {
     "mtg_plan_destroy": (ctypes.c_int, [_vp]),
     "mtg_plan_counts": (ctypes.c_int, [_vp, _ip, _ip]),
     "mtg_plan_set_kernel": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "mtg_free_cost": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp,
+                                     ctypes.POINTER(TimeParams), ctypes.c_int, _vp, _vp, _vp,
+                                     _vp]),
+    "mtg_free_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp,
+                                         ctypes.POINTER(TimeParams), ctypes.c_int, _vp, _vp,
+                                         _vp, _vp]),
     "mtg_plan_kernel": (ctypes.c_int, [_vp]),
     "mtg_linear_solve": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mtg_linear_solve_host": (ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, _dp, _dp,

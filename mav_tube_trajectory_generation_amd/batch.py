@@ -183,6 +183,51 @@ class LinearPlan:
                                       _stream(dev)), "mtg_time_optimize")
         return dict(times=t, cost=cost, evals=evals, status=status)
 
+    def free_cost(self, fixed_vals, free_vals, times, mode=0, time_penalty=500.0, soft=None,
+                  soft_weight=100.0, grad=True):
+        """Free-derivative objectives (mtg_free_cost): mode 0
+        objectiveFunctionFreeConstraints (J_d [+ soft], gradient of J_d
+        [B, D, n_free]); mode 1 objectiveFunctionTimeAndConstraints."""
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        _require(free_vals, (B, self.D, self.n_free), "free_vals")
+        dev = times.device
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        g = (torch.empty((B, self.D, self.n_free), dtype=torch.float64, device=dev)
+             if (grad and mode == 0) else None)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        p = make_time_params(time_penalty, 0.1, 0.1, 1.0, 0, soft, soft_weight)
+        check(lib().mtg_free_cost(self._h, B, _ptr(fixed_vals), _ptr(free_vals), _ptr(times),
+                                  ctypes.byref(p), mode, _ptr(cost), _ptr(g), _ptr(status),
+                                  _stream(dev)), "mtg_free_cost")
+        return dict(cost=cost, grad=g, status=status)
+
+    def free_optimize(self, fixed_vals, free_vals, times, max_evals=50, lower=None, upper=None,
+                      soft=None, soft_weight=100.0):
+        """Optimise the free derivatives (mtg_free_optimize) on a copy of
+        free_vals; returns dict(free, cost, evals, status)."""
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        _require(free_vals, (B, self.D, self.n_free), "free_vals")
+        for name, a in (("lower", lower), ("upper", upper)):
+            if a is not None:
+                _require(a, (B, self.D, self.n_free), name)
+        dev = times.device
+        d = free_vals.clone()
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        evals = torch.empty(B, dtype=torch.int32, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        p = make_time_params(500.0, 0.1, 0.1, 1.0, 0, soft, soft_weight)
+        check(lib().mtg_free_optimize(self._h, B, _ptr(fixed_vals), _ptr(d), _ptr(times),
+                                      _ptr(lower), _ptr(upper), ctypes.byref(p), max_evals,
+                                      _ptr(cost), _ptr(evals), _ptr(status), _stream(dev)),
+              "mtg_free_optimize")
+        return dict(free=d, cost=cost, evals=evals, status=status)
+
     # -- host (numpy) API ---------------------------------------------------
     def solve_host(self, fixed_vals, times):
         fixed_vals = np.ascontiguousarray(fixed_vals, dtype=np.float64)

@@ -1,0 +1,342 @@
+// mtg_free.hip — free-derivative objectives of PolynomialOptimizationNonLinear
+//  for any constraint pattern, on the generic
+// per-trajectory state of mtg_device.h (one 64-lane workgroup per trajectory):
+//   mode 0  objectiveFunctionFreeConstraints (nonlinear_impl:1021-1113):
+//           setFreeConstraints(d_p); J = J_d [+ soft], J_d = sum_dim d^T R d
+//           (getCostAndGradientDerivative, :1537-1606), gradient
+//           dJ_d/dd_p = 2 (R_pf d_f + R_pp d_p) per dimension (:1591-1592);
+//           the soft term is not differentiated (:1100-1110);
+//   mode 1  objectiveFunctionTimeAndConstraints (:947-1019):
+//           updateSegmentTimes(T); setFreeConstraints(d_p);
+//           J = computeCost() + time_penalty (sum T)^2 [+ soft].
+// R d is formed segment by segment: (R d) at vertex v gathers the rows of
+// H_s e_s (e_s = [d(vertex s); d(vertex s+1)]) of the two segments meeting
+// there, so no R is assembled.  J_d = sum_s e_s^T H_s e_s = 2 computeCost().
+//
+// free_optimize_kernel: the device optimiser of mtg_free_optimize on the
+// mode-0 objective (oracle restatement: orc_free_optimize).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "mtg_device.h"
+#include "mtg_extrema_device.h"
+#include "mtg_internal.h"
+
+namespace mtg {
+
+namespace {
+
+// LDS after the generic layout: [cbuf S*D*N (kSoft)] [gv (S+1)*M*D]
+// [free-optimiser state 3*D*np].
+struct FreeLds {
+  size_t cbuf, gv, opt, bytes;
+};
+
+__host__ __device__ inline FreeLds free_lds(int N, int S, int D, int np, bool soft) {
+  const Layout lay = make_layout(N, S, D);
+  FreeLds f;
+  size_t o = (lay.bytes() + 15) / 16 * 16;
+  f.cbuf = o;
+  if (soft) o += sizeof(double) * S * D * N;
+  f.gv = o;
+  o += sizeof(double) * (S + 1) * (N / 2) * D;
+  f.opt = o;
+  o += sizeof(double) * 3 * D * (np > 0 ? np : 1);
+  f.bytes = o;
+  return f;
+}
+
+template <typename T>
+__device__ inline T* lds_at(double* smem, size_t byte_offset) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(smem) + byte_offset);
+}
+
+// Loads d_f, d_p (free values into dv via free_map), times and powers.
+// Returns true on an invalid segment time (wave-uniform).
+template <int N>
+__device__ bool free_setup(Traj<N>& t, const PlanDev& pl, const double* __restrict__ fixed_b,
+                           const double* __restrict__ free_b, const double* __restrict__ times_b) {
+  t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times_b, fixed_b, pl.nf);
+  if (free_b)
+    for (int i = t.lane; i < t.D * pl.np; i += kWave)
+      t.dv()[pl.free_map[i % pl.np] * t.D + i / pl.np] = free_b[i];
+  __syncthreads();
+  t.compute_powers();
+  __syncthreads();
+  return (t.flag()[0] & 1) != 0;
+}
+
+// J of `mode` at the current dv (all lanes; wave-uniform result).
+template <int N, bool kSoft>
+__device__ double free_objective(Traj<N>& t, const double* __restrict__ tab,
+                                 const mtg_time_params& p, int mode, double* cbuf) {
+  double c;
+  if constexpr (kSoft) {
+    c = t.template coeffs_and_cost<true>(tab, cbuf);  // coefficients into LDS
+  } else {
+    c = t.cost(tab);
+  }
+  double J;
+  if (mode == 0) {
+    J = 2.0 * c;  // J_d = d^T R d = c^T Q c = 2 computeCost()
+  } else {
+    double tot = 0.0;
+    for (int i = 0; i < t.S; ++i) tot += t.T()[i];  // nonlinear_impl:2768-2774
+    J = c + tot * tot * p.time_penalty;
+  }
+  if constexpr (kSoft) {
+    // evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:2735-2766).
+    __syncthreads();
+    double soft = 0.0;
+    for (int k = 0; k < p.n_soft; ++k) {
+      int K = 0;
+      double lim = 1.0;
+#pragma unroll
+      for (int cc = 0; cc < kMaxSoftConstraints; ++cc)  // compile-time indices
+        if (cc == k) {
+          K = p.soft_derivative[cc];
+          lim = p.soft_limit[cc];
+        }
+      const double m = ext_trajectory_max_wave_k<N>(K, cbuf, t.T(), t.S, t.D, t.lane);
+      soft += fmin(p.soft_maximum_cost, exp((m - lim) / lim * p.soft_weight));
+    }
+    J += soft;
+  }
+  __syncthreads();
+  return J;
+}
+
+// gv[(v*M + k)*D + d] = (R d)_(v, k) for dimension d: two passes so each
+// vertex row is written by one lane at a time (half 0 of segment v, then
+// half 1 of segment v-1).
+template <int N>
+__device__ void free_rd(Traj<N>& t, double* gv) {
+  constexpr int M = N / 2;
+  const int S = t.S, D = t.D;
+  for (int i = t.lane; i < (S + 1) * M * D; i += kWave) gv[i] = 0.0;
+  __syncthreads();
+  for (int h = 0; h < 2; ++h) {
+    for (int item = t.lane; item < S * D; item += kWave) {
+      const int s = item / D, d = item % D;
+      double e[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) e[j] = t.dval(s + j / M, j % M, d);
+#pragma unroll 1
+      for (int kk = 0; kk < M; ++kk) {
+        const int a = h * M + kk;
+        double row = 0.0;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+          row = fma(t.tabH()[a * N + j] * t.pwr(s, 1 - 2 * t.r + kk + (j % M)), e[j], row);
+        gv[((s + h) * M + kk) * D + d] += row;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+template <int N, bool kSoft>
+__global__ __launch_bounds__(kWave) void free_cost_kernel(
+    PlanDev pl, const double* __restrict__ fixed_vals, const double* __restrict__ free_vals,
+    const double* __restrict__ times, mtg_time_params p, int mode, double* __restrict__ cost,
+    double* __restrict__ grad, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf, np = pl.np;
+  const Layout lay = make_layout(N, S, D);
+  const FreeLds fl = free_lds(N, S, D, np, kSoft);
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
+  const int64_t b = blockIdx.x;
+  const bool bad = free_setup(t, pl, fixed_vals + b * D * nf, free_vals + b * D * np,
+                              times + b * S);
+  double J = NAN;
+  if (!bad) J = free_objective<N, kSoft>(t, pl.tab, p, mode, lds_at<double>(smem, fl.cbuf));
+  if (grad && mode == 0) {
+    if (bad) {
+      for (int i = t.lane; i < D * np; i += kWave) grad[b * D * np + i] = NAN;
+    } else {
+      double* gv = lds_at<double>(smem, fl.gv);
+      free_rd(t, gv);
+      for (int i = t.lane; i < D * np; i += kWave)
+        grad[b * D * np + i] = 2.0 * gv[pl.free_map[i % np] * D + i / np];
+    }
+  }
+  if (t.lane == 0) {
+    if (cost) cost[b] = J;
+    if (status) status[b] = bad ? MTG_TRAJ_BAD_TIME : MTG_TRAJ_OK;
+  }
+}
+
+// Device optimiser on the mode-0 objective J_d + [soft] (the objective of
+// optimizeFreeConstraints, nonlinear_impl:399-493, whose NLopt run is
+// replaced): d* = argmin J_d by the linear solve (the Newton step of the
+// quadratic J_d), then d <- clamp(d + alpha (d* - d), lower, upper) with
+// alpha = 1, x1.5 (capped at 1) on a decrease, x0.5 otherwise, `max_evals`
+// objective evaluations; stops when a trial moves no entry by more than
+// 1e-13 (1 + |d_i|).  One objective call site (state machine).
+template <int N, bool kSoft>
+__global__ __launch_bounds__(kWave) void free_optimize_kernel(
+    PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ free_io,
+    const double* __restrict__ times, const double* __restrict__ lower,
+    const double* __restrict__ upper, mtg_time_params p, int max_evals,
+    double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf, np = pl.np, n = D * np;
+  const Layout lay = make_layout(N, S, D);
+  const FreeLds fl = free_lds(N, S, D, np, kSoft);
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
+  const int64_t b = blockIdx.x;
+  double* cbuf = lds_at<double>(smem, fl.cbuf);
+  double* dstar = lds_at<double>(smem, fl.opt);  // [d][p]
+  double* dcur = dstar + n;
+  double* dtry = dcur + n;
+  const double* lo = lower ? lower + b * n : nullptr;
+  const double* hi = upper ? upper + b * n : nullptr;
+  const bool bad = free_setup(t, pl, fixed_vals + b * D * nf, nullptr, times + b * S);
+  int evals = 0;
+  double f = NAN;
+  bool not_spd = false;
+  if (!bad) {
+    // d* = the unconstrained minimiser (solveLinear, linear_impl:337-379).
+    t.solve();
+    not_spd = (t.flag()[0] & 2) != 0;
+    for (int i = t.lane; i < n; i += kWave) {
+      const int slot = pl.free_map[i % np] * D + i / np;
+      dstar[i] = t.dv()[slot];
+      const double d0 = free_io[b * n + i];
+      dcur[i] = d0;
+      t.dv()[slot] = d0;
+    }
+    __syncthreads();
+    double alpha = 1.0;
+    bool base = true;
+    for (;;) {
+      const double J = free_objective<N, kSoft>(t, pl.tab, p, 0, cbuf);
+      if (base) {
+        f = J;
+        evals = 1;
+        base = false;
+      } else {
+        ++evals;
+        if (J < f) {
+          f = J;
+          for (int i = t.lane; i < n; i += kWave) dcur[i] = dtry[i];
+          alpha = fmin(alpha * 1.5, 1.0);
+        } else {
+          alpha *= 0.5;
+        }
+      }
+      __syncthreads();
+      if (!(evals < max_evals && alpha > 1e-9)) break;
+      // Next trial, unfused like the oracle: x = d + alpha (d* - d), clamped.
+      bool moved = false;
+      for (int i = t.lane; i < n; i += kWave) {
+        const double d = dcur[i];
+        double x = __dadd_rn(d, __dmul_rn(alpha, __dsub_rn(dstar[i], d)));
+        if (lo) x = fmax(x, lo[i]);
+        if (hi) x = fmin(x, hi[i]);
+        dtry[i] = x;
+        moved = moved || fabs(x - d) > 1e-13 * (1.0 + fabs(d));
+        t.dv()[pl.free_map[i % np] * D + i / np] = x;
+      }
+      if (!__any(moved)) break;
+      __syncthreads();
+    }
+    __syncthreads();
+    for (int i = t.lane; i < n; i += kWave) free_io[b * n + i] = dcur[i];
+  }
+  if (t.lane == 0) {
+    if (cost) cost[b] = f;
+    if (evals_out) evals_out[b] = evals;
+    if (status)
+      status[b] = bad ? MTG_TRAJ_BAD_TIME : (not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
+  }
+}
+
+namespace {
+template <typename K>
+hipError_t prepare_lds_free(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(bytes));
+  return hipSuccess;
+}
+
+template <int N>
+hipError_t free_cost_n(const PlanDev& pl, int64_t B, const double* df, const double* dp,
+                       const double* times, const mtg_time_params& p, int mode, double* cost,
+                       double* grad, int32_t* status, hipStream_t st) {
+  const bool soft = p.n_soft > 0;
+  const size_t bytes = free_lds(N, pl.S, pl.D, pl.np, soft).bytes;
+  if (soft) {
+    hipError_t e = prepare_lds_free(free_cost_kernel<N, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((free_cost_kernel<N, true>), dim3(static_cast<unsigned>(B)), dim3(kWave),
+                       bytes, st, pl, df, dp, times, p, mode, cost, grad, status);
+  } else {
+    hipError_t e = prepare_lds_free(free_cost_kernel<N, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((free_cost_kernel<N, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, dp, times, p, mode, cost, grad, status);
+  }
+  return hipGetLastError();
+}
+
+template <int N>
+hipError_t free_opt_n(const PlanDev& pl, int64_t B, const double* df, double* dp,
+                      const double* times, const double* lower, const double* upper,
+                      const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
+                      int32_t* status, hipStream_t st) {
+  const bool soft = p.n_soft > 0;
+  const size_t bytes = free_lds(N, pl.S, pl.D, pl.np, soft).bytes;
+  if (soft) {
+    hipError_t e = prepare_lds_free(free_optimize_kernel<N, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((free_optimize_kernel<N, true>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, dp, times, lower, upper, p, max_evals,
+                       cost, evals, status);
+  } else {
+    hipError_t e = prepare_lds_free(free_optimize_kernel<N, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((free_optimize_kernel<N, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, dp, times, lower, upper, p, max_evals,
+                       cost, evals, status);
+  }
+  return hipGetLastError();
+}
+}  // namespace
+
+size_t free_lds_bytes(int N, int S, int D, int np, bool soft) {
+  return free_lds(N, S, D, np, soft).bytes;
+}
+
+#define MTG_FREE_DISPATCH(FN, ...)        \
+  switch (pl.N) {                         \
+    case 4: return FN<4>(__VA_ARGS__);    \
+    case 6: return FN<6>(__VA_ARGS__);    \
+    case 8: return FN<8>(__VA_ARGS__);    \
+    case 10: return FN<10>(__VA_ARGS__);  \
+    case 12: return FN<12>(__VA_ARGS__);  \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_free_cost(const PlanDev& pl, int64_t B, const double* df, const double* dp,
+                            const double* times, const mtg_time_params& p, int mode,
+                            double* cost, double* grad, int32_t* status, hipStream_t st) {
+  MTG_FREE_DISPATCH(free_cost_n, pl, B, df, dp, times, p, mode, cost, grad, status, st)
+}
+
+hipError_t launch_free_optimize(const PlanDev& pl, int64_t B, const double* df, double* dp,
+                                const double* times, const double* lower, const double* upper,
+                                const mtg_time_params& p, int max_evals, double* cost,
+                                int32_t* evals, int32_t* status, hipStream_t st) {
+  MTG_FREE_DISPATCH(free_opt_n, pl, B, df, dp, times, lower, upper, p, max_evals, cost, evals,
+                    status, st)
+}
+
+}  // namespace mtg

@@ -582,7 +582,6 @@ struct Solver {
   // aligned) and computeCost of segment-dimension sd; returns this lane's
   // share of the cost (0.5 c^T Q c summed over its (s, d)).
   __device__ double coeff_cost_sd(int sd, double* out) const {
-    constexpr CostW<N, R> kW{};
     constexpr AInvTab<N> kA{};
     const int s = sd / D, d = sd % D;
     const double* ps = pw() + s * PWP + N;

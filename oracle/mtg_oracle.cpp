@@ -1945,4 +1945,125 @@ int orc_bench_linear(int N, int D, int r, int S, int K, int B, const uint8_t* ma
   return failed.load() ? -2 : 0;
 }
 
+
+// ----------------------------------------------------------------------------
+// Free-derivative objectives.
+//
+// mode 0: objectiveFunctionFreeConstraints (nonlinear_impl:1021-1113):
+//   setFreeConstraints(d_p); J = J_d + [soft], J_d = sum_dim d^T R d from
+//   getCostAndGradientDerivative (:1537-1606); gradient (when grad != NULL)
+//   = 2 d_f^T R_pf^T + 2 d_p^T R_pp per dimension (:1591-1592), the soft term
+//   is not differentiated there (:1100-1110).
+// mode 1: objectiveFunctionTimeAndConstraints (:947-1019):
+//   updateSegmentTimes(T); setFreeConstraints(d_p);
+//   J = computeCost() + time_penalty (sum T)^2 + [soft]; no gradient.
+// dp, grad: D x np (dimension-major, the x layout of :1040-1052).
+static int freeCostImpl(LinearProblem& lp, const double* dp, int mode, double time_penalty,
+                        const SoftSpec* soft, double* cost, double* grad) {
+  const int D = lp.D, np = lp.np, nf = lp.nf;
+  for (int d = 0; d < D; ++d)
+    for (int i = 0; i < np; ++i) lp.dp[d][i] = dp[d * np + i];
+  lp.updateSegmentsFromCompactConstraints();
+  double J;
+  if (mode == 0) {
+    J = lp.costDerivativeJd();
+    if (grad) {
+      Mat R = lp.constructR();
+      for (int d = 0; d < D; ++d)
+        for (int i = 0; i < np; ++i) {
+          double g = 0.0;
+          for (int j = 0; j < nf; ++j) g += R(nf + i, j) * lp.df[d][j];
+          for (int j = 0; j < np; ++j) g += R(nf + i, nf + j) * lp.dp[d][j];
+          grad[d * np + i] = 2.0 * g;
+        }
+    }
+  } else {
+    double total = 0.0;
+    for (double v : lp.times) total += v;
+    J = lp.computeCost() + total * total * time_penalty;
+  }
+  if (soft && soft->n > 0) {
+    double c = 0.0;
+    orc_soft_constraint_cost(lp.N, D, lp.S, lp.coeffs.data(), lp.times.data(), soft->n,
+                             soft->derivatives, soft->limits, soft->weight, soft->maximum_cost,
+                             nullptr, &c);
+    J += c;
+  }
+  if (cost) *cost = J;
+  return 0;
+}
+
+int orc_free_cost(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                  const double* times, const double* dp, int mode, double time_penalty,
+                  int n_soft, const int* soft_derivatives, const double* soft_limits,
+                  double soft_weight, double soft_maximum_cost, double* cost, double* grad) {
+  if (!dp || mode < 0 || mode > 1) return -1;
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
+  if (rc) return rc;
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  return freeCostImpl(lp, dp, mode, time_penalty, n_soft > 0 ? &soft : nullptr, cost,
+                      mode == 0 ? grad : nullptr);
+}
+
+// The batched optimiser of mtg_free_optimize (free_optimize_kernel) on the
+// mode-0 objective: d* = the unconstrained minimiser of J_d (solveLinear,
+// linear_impl:337-379) is computed once; then projected steps
+// d <- clamp(d + alpha (d* - d), lower, upper) with alpha = 1 initially,
+// x1.5 (capped at 1) on a decrease of J, x0.5 otherwise, at most max_evals
+// objective evaluations (NLopt maxeval, nonlinear_impl:101).  The direction
+// d* - d is the Newton step of the quadratic J_d (its Hessian 2 R_pp is what
+// the linear solve factors).  The loop also stops when a trial point moves
+// no entry by more than 1e-13 (1 + |d_i|).  lower/upper: D x np or NULL
+// (unbounded).
+int orc_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                      const double* vals, const double* times, double* dp_io,
+                      const double* lower, const double* upper, int n_soft,
+                      const int* soft_derivatives, const double* soft_limits,
+                      double soft_weight, double soft_maximum_cost, int max_evals, double* cost,
+                      int* evals) {
+  if (!dp_io) return -1;
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
+  if (rc) return rc;
+  const int np = lp.np, n = D * np;
+  if (lp.solveLinear() != 0) return -5;
+  std::vector<double> dstar(n), d(dp_io, dp_io + n), trial(n);
+  for (int k = 0; k < D; ++k)
+    for (int i = 0; i < np; ++i) dstar[k * np + i] = lp.dp[k][i];
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  auto objective = [&](const std::vector<double>& x) {
+    double J = 0.0;
+    freeCostImpl(lp, x.data(), 0, 0.0, n_soft > 0 ? &soft : nullptr, &J, nullptr);
+    return J;
+  };
+  double f = objective(d);
+  int n_eval = 1;
+  double alpha = 1.0;
+  while (n_eval < max_evals && alpha > 1e-9) {
+    bool same = true;
+    for (int i = 0; i < n; ++i) {
+      double x = d[i] + alpha * (dstar[i] - d[i]);
+      if (lower) x = std::max(x, lower[i]);
+      if (upper) x = std::min(x, upper[i]);
+      trial[i] = x;
+      same = same && std::fabs(x - d[i]) <= 1e-13 * (1.0 + std::fabs(d[i]));
+    }
+    if (same) break;
+    const double ft = objective(trial);
+    ++n_eval;
+    if (ft < f) {
+      d = trial;
+      f = ft;
+      alpha = std::min(alpha * 1.5, 1.0);
+    } else {
+      alpha *= 0.5;
+    }
+  }
+  std::memcpy(dp_io, d.data(), sizeof(double) * n);
+  if (cost) *cost = f;
+  if (evals) *evals = n_eval;
+  return 0;
+}
+
 }  // extern "C"

@@ -209,6 +209,23 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                        const double* radii, int param_i, double param_d, int threads,
                        double min_seconds, int64_t* units, double* seconds);
 
+// Free-derivative objectives (see mtg_oracle.cpp):
+// mode 0 objectiveFunctionFreeConstraints (nonlinear_impl:1021-1113, J_d and
+// its gradient of :1537-1606), mode 1 objectiveFunctionTimeAndConstraints
+// (:947-1019).  dp, grad: D x np.
+int orc_free_cost(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                  const double* times, const double* dp, int mode, double time_penalty,
+                  int n_soft, const int* soft_derivatives, const double* soft_limits,
+                  double soft_weight, double soft_maximum_cost, double* cost, double* grad);
+// The mtg_free_optimize algorithm restated (projected Newton steps of J_d
+// with backtracking on J_d + soft).  dp_io, lower, upper: D x np.
+int orc_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                      const double* vals, const double* times, double* dp_io,
+                      const double* lower, const double* upper, int n_soft,
+                      const int* soft_derivatives, const double* soft_limits,
+                      double soft_weight, double soft_maximum_cost, int max_evals, double* cost,
+                      int* evals);
+
 #ifdef __cplusplus
 }
 #endif

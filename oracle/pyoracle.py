@@ -362,3 +362,56 @@ def soft_constraint_cost(N, coeffs, times, derivatives, limits, weight=100.0,
                                       der.ctypes.data_as(_ip), _d(lim), weight, maximum_cost,
                                       _d(maxima), _d(cost)), "soft_constraint_cost")
     return float(cost[0]), maxima
+
+
+def _soft_arrays(soft):
+    der = np.ascontiguousarray([d for d, _ in soft] if soft else [0], dtype=np.int32)
+    lim = np.ascontiguousarray([v for _, v in soft] if soft else [1.0], dtype=np.float64)
+    return (len(soft) if soft else 0), der, lim
+
+
+def free_cost(N, r, vertices, times, dp, mode=0, time_penalty=500.0, soft=None,
+              soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """orc_free_cost: objectiveFunctionFreeConstraints (mode 0: J_d [+ soft],
+    gradient of J_d) / objectiveFunctionTimeAndConstraints (mode 1).
+    dp: D x n_free.  Returns (J, grad or None)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    dp = np.ascontiguousarray(dp, dtype=np.float64)
+    grad = np.zeros(dp.shape)
+    cost = np.zeros(1)
+    ns, der, lim = _soft_arrays(soft)
+    L = lib()
+    L.orc_free_cost.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, ctypes.c_int, ctypes.c_double, ctypes.c_int, _ip, _dp,
+        ctypes.c_double, ctypes.c_double, _dp, _dp]
+    _check(L.orc_free_cost(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p), _d(vertices.vals),
+                           _d(times), _d(dp), mode, time_penalty, ns, der.ctypes.data_as(_ip),
+                           _d(lim), soft_weight, soft_maximum_cost, _d(cost), _d(grad)),
+           "free_cost")
+    return float(cost[0]), (grad if mode == 0 else None)
+
+
+def free_optimize(N, r, vertices, times, dp0, max_evals, lower=None, upper=None, soft=None,
+                  soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """orc_free_optimize: the mtg_free_optimize algorithm on the oracle.
+    Returns (dp, J, evals)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    dp = np.ascontiguousarray(dp0, dtype=np.float64).copy()
+    lo = None if lower is None else np.ascontiguousarray(lower, dtype=np.float64)
+    hi = None if upper is None else np.ascontiguousarray(upper, dtype=np.float64)
+    cost = np.zeros(1)
+    evals = ctypes.c_int()
+    ns, der, lim = _soft_arrays(soft)
+    L = lib()
+    L.orc_free_optimize.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, _dp, _dp, ctypes.c_int, _ip, _dp, ctypes.c_double,
+        ctypes.c_double, ctypes.c_int, _dp, ctypes.POINTER(ctypes.c_int)]
+    _check(L.orc_free_optimize(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                               _d(vertices.vals), _d(times), _d(dp),
+                               None if lo is None else _d(lo), None if hi is None else _d(hi),
+                               ns, der.ctypes.data_as(_ip), _d(lim), soft_weight,
+                               soft_maximum_cost, max_evals, _d(cost), ctypes.byref(evals)),
+           "free_optimize")
+    return dp, float(cost[0]), evals.value

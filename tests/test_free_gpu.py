@@ -1,0 +1,168 @@
+"""GPU parity of the free-derivative objectives (mtg_free_cost: the NLopt
+callbacks objectiveFunctionFreeConstraints, nonlinear_impl:1021-1113, and
+objectiveFunctionTimeAndConstraints, :947-1019) and of the free-derivative
+optimiser (mtg_free_optimize) against the oracle.
+
+Patterns: the standard one (intermediate positions fixed) and the fork's tube
+pattern (every intermediate derivative free, qcqp_impl:95-117), which is what
+the reference's nonlinear class optimises."""
+import numpy as np
+import pytest
+
+from helpers import compact_fixed, rel_err, standard_vertices
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+N, R = 10, 4
+
+
+def _problem(oracle, S, D, seed, pattern):
+    v = standard_vertices(N, S, D, seed)
+    times = oracle.estimate_segment_times(v, 3.0, 5.0)
+    if pattern == "tube":
+        v.mask[1:S, :] = 0
+    return v, times
+
+
+def _plan(ctx, v):
+    import mav_tube_trajectory_generation_amd as mtg
+    mask, df = compact_fixed(v, N)
+    return mtg.LinearPlan(ctx, N, v.D, R, v.S, mask), df
+
+
+def _T(dev, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _soft_near(oracle, plan, dev, df, dp, times):
+    """Limits 3% above the trajectory's own max |v| and |a|: the soft cost is
+    in its exponential regime (exp(100 * -0.03) ~ 0.05)."""
+    c, _, _ = plan.coefficients(_T(dev, df[None]), _T(dev, dp[None]), _T(dev, times[None]))
+    c = c.cpu().numpy()[0]
+    return [(k, 1.03 * oracle.max_magnitude(N, c, times, k)["value"]) for k in (1, 2)]
+
+
+@pytest.mark.parametrize("pattern", ["standard", "tube"])
+@pytest.mark.parametrize("soft", [False, True], ids=["nosoft", "soft"])
+def test_free_cost_vs_oracle(ctx, dev, oracle, pattern, soft):
+    S, D = 6, 3
+    rng = np.random.default_rng(3)
+    for b in range(4):
+        v, times = _problem(oracle, S, D, 700 + b, pattern)
+        ref = oracle.linear_solve(N, R, v, times)
+        dp = ref["dp"] + rng.normal(scale=0.3, size=ref["dp"].shape)
+        plan, df = _plan(ctx, v)
+        soft = _soft_near(oracle, plan, dev, df, dp, times) if soft else None
+        J, g = oracle.free_cost(N, R, v, times, dp, mode=0, soft=soft)
+        out = plan.free_cost(_T(dev, df[None]), _T(dev, dp[None]), _T(dev, times[None]),
+                             mode=0, soft=soft)
+        assert int(out["status"][0]) == 0
+        assert rel_err(float(out["cost"][0]), J) <= 1e-9, (b, float(out["cost"][0]), J)
+        gg = out["grad"].cpu().numpy()[0]
+        assert np.max(np.abs(gg - g)) <= 1e-8 * np.max(np.abs(g)), b
+        J1, _ = oracle.free_cost(N, R, v, times, dp, mode=1, soft=soft)
+        out1 = plan.free_cost(_T(dev, df[None]), _T(dev, dp[None]), _T(dev, times[None]),
+                              mode=1, soft=soft)
+        assert out1["grad"] is None
+        assert rel_err(float(out1["cost"][0]), J1) <= 1e-9, b
+        if soft:
+            J0, _ = oracle.free_cost(N, R, v, times, dp, mode=0)
+            assert J > J0  # the soft term is present
+
+
+def test_free_gradient_is_derivative_of_jd(ctx, dev):
+    """Size-independent property on a config-2-sized batch: the analytic
+    gradient equals central differences of the device J_d (J_d is quadratic,
+    so central differences are exact up to rounding)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    D, S, B = 3, 10, 256
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=105)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    fd, td = _T(dev, fixed), _T(dev, times)
+    dp = plan.solve(fd, td, free=True)["free"]
+    dp = dp + 0.2 * torch.randn(dp.shape, dtype=torch.float64, device=dev,
+                                generator=torch.Generator(device=dev).manual_seed(1))
+    base = plan.free_cost(fd, dp, td)
+    g = base["grad"]
+    h = 1e-3
+    for (d, p) in [(0, 0), (1, 5), (2, plan.n_free - 1)]:
+        e = torch.zeros_like(dp)
+        e[:, d, p] = h
+        jp = plan.free_cost(fd, dp + e, td, grad=False)["cost"]
+        jm = plan.free_cost(fd, dp - e, td, grad=False)["cost"]
+        num = (jp - jm) / (2 * h)
+        scale = g.abs().amax(dim=(1, 2))
+        assert torch.all((num - g[:, d, p]).abs() <= 1e-6 * scale + 1e-9), (d, p)
+
+
+@pytest.mark.parametrize("pattern", ["standard", "tube"])
+def test_free_optimize_reaches_linear_solution(ctx, dev, oracle, pattern):
+    """Without soft constraints or bounds J_d is minimised by the linear
+    solve: the optimiser's first (Newton) step lands there."""
+    S, D = 8, 3
+    rng = np.random.default_rng(5)
+    vs = [_problem(oracle, S, D, 800 + b, pattern) for b in range(6)]
+    plan, _ = _plan(ctx, vs[0][0])
+    dfs = np.stack([compact_fixed(v, N)[1] for v, _ in vs])
+    times = np.stack([t for _, t in vs])
+    refs = [oracle.linear_solve(N, R, v, t) for v, t in vs]
+    dp0 = np.stack([r["dp"] + rng.normal(scale=0.5, size=r["dp"].shape) for r in refs])
+    out = plan.free_optimize(_T(dev, dfs), _T(dev, dp0), _T(dev, times), max_evals=20)
+    d = out["free"].cpu().numpy()
+    for b, r in enumerate(refs):
+        assert np.max(np.abs(d[b] - r["dp"])) <= 1e-7 * (1 + np.max(np.abs(r["dp"]))), b
+        # At the minimum the quadratic form cancels (tube pattern: J_d ~ 3e-5
+        # from terms of order 1), so the value is compared at 1e-7.
+        assert rel_err(float(out["cost"][b]), 2 * r["cost"]) <= 1e-7, b
+        assert int(out["status"][b]) == 0 and 2 <= int(out["evals"][b]) <= 20
+
+
+def test_free_optimize_vs_oracle_driver(ctx, dev, oracle):
+    """Bounds and soft constraints: the device optimiser takes the oracle
+    restatement's steps (orc_free_optimize)."""
+    S, D, E = 6, 3, 15
+    rng = np.random.default_rng(11)
+    agree = 0
+    B = 6
+    for b in range(B):
+        v, times = _problem(oracle, S, D, 900 + b, "tube")
+        ref = oracle.linear_solve(N, R, v, times)
+        dp0 = ref["dp"] + rng.normal(scale=0.5, size=ref["dp"].shape)
+        width = 0.4 + np.abs(rng.normal(size=dp0.shape))
+        lo, hi = dp0 - width, dp0 + width
+        plan, df = _plan(ctx, v)
+        soft = _soft_near(oracle, plan, dev, df, ref["dp"], times)
+        out = plan.free_optimize(_T(dev, df[None]), _T(dev, dp0[None]), _T(dev, times[None]),
+                                 max_evals=E, lower=_T(dev, lo[None]), upper=_T(dev, hi[None]),
+                                 soft=soft)
+        d = out["free"].cpu().numpy()[0]
+        assert np.all(d >= lo - 1e-15) and np.all(d <= hi + 1e-15)
+        # the reported cost is the objective at the returned point
+        chk = plan.free_cost(_T(dev, df[None]), out["free"], _T(dev, times[None]), soft=soft)
+        assert rel_err(float(out["cost"][0]), float(chk["cost"][0])) <= 1e-12
+        J0, _ = oracle.free_cost(N, R, v, times, dp0, soft=soft)
+        assert float(out["cost"][0]) <= J0
+        dr, fr, er = oracle.free_optimize(N, R, v, times, dp0, E, lower=lo, upper=hi, soft=soft)
+        if int(out["evals"][0]) == er and np.max(np.abs(d - dr)) <= 1e-7 * (1 + np.max(np.abs(dr))):
+            assert rel_err(float(out["cost"][0]), fr) <= 1e-8
+            agree += 1
+    # accept/reject decisions compare objectives whose soft terms amplify
+    # rounding by the weight (100); allow one divergent path
+    assert agree >= B - 1
+
+
+def test_free_rejects_bad_arguments(ctx, dev, oracle):
+    from mav_tube_trajectory_generation_amd._abi import MTGError
+    v, times = _problem(oracle, 4, 3, 5, "standard")
+    plan, df = _plan(ctx, v)
+    dp = np.zeros((3, plan.n_free))
+    with pytest.raises(MTGError):
+        plan.free_cost(_T(dev, df[None]), _T(dev, dp[None]), _T(dev, times[None]), mode=2)
+    with pytest.raises(MTGError):
+        plan.free_cost(_T(dev, df[None]), _T(dev, dp[None]), _T(dev, times[None]),
+                       soft=[(1, 0.0)])
+    with pytest.raises(MTGError):
+        plan.free_optimize(_T(dev, df[None]), _T(dev, dp[None]), _T(dev, times[None]),
+                           max_evals=0)

@@ -328,3 +328,37 @@ def test_soft_constraint_cost_formula(oracle):
     assert np.allclose(maxima, [vm, am], rtol=0, atol=0)
     ref = min(1e12, np.exp((vm - 2.0) / 2.0 * 100.0)) + min(1e12, np.exp((am - 1.0) / 1.0 * 100.0))
     assert abs(cost - ref) <= 1e-12 * ref
+
+
+def test_free_objectives_oracle(oracle):
+    """orc_free_cost pinned by identities of the reference's definitions:
+    J_d = d^T R d = 2 computeCost() (getCostAndGradientDerivative,
+    nonlinear_impl:1537-1606), its gradient 2 (R_pf d_f + R_pp d_p) vanishes
+    at the linear solution and equals central differences elsewhere;
+    objectiveFunctionTimeAndConstraints = computeCost + time_penalty (sum T)^2
+    (:947-1019); the optimiser restatement's Newton step lands on d*."""
+    from helpers import standard_vertices
+    N, R, D, S = 10, 4, 3, 5
+    for pattern in ("standard", "tube"):
+        v = standard_vertices(N, S, D, 321)
+        t = oracle.estimate_segment_times(v, 3.0, 5.0)
+        if pattern == "tube":
+            v.mask[1:S, :] = 0
+        ref = oracle.linear_solve(N, R, v, t)
+        J, g = oracle.free_cost(N, R, v, t, ref["dp"])
+        assert abs(J - 2 * ref["cost"]) <= 1e-9 * J
+        assert np.max(np.abs(g)) <= 1e-7 * (1 + J)
+        J1, _ = oracle.free_cost(N, R, v, t, ref["dp"], mode=1, time_penalty=500.0)
+        assert abs(J1 - (ref["cost"] + 500.0 * t.sum() ** 2)) <= 1e-12 * J1
+        dp = ref["dp"] + np.random.default_rng(2).normal(scale=0.2, size=ref["dp"].shape)
+        J2, g2 = oracle.free_cost(N, R, v, t, dp)
+        h = 1e-4
+        for idx in [(0, 0), (1, dp.shape[1] // 2), (2, dp.shape[1] - 1)]:
+            a, b = dp.copy(), dp.copy()
+            a[idx] += h
+            b[idx] -= h
+            num = (oracle.free_cost(N, R, v, t, a)[0] - oracle.free_cost(N, R, v, t, b)[0]) / (2 * h)
+            assert abs(num - g2[idx]) <= 1e-6 * np.max(np.abs(g2))
+        d3, J3, e3 = oracle.free_optimize(N, R, v, t, dp, 10)
+        assert np.max(np.abs(d3 - ref["dp"])) <= 1e-8 * (1 + np.max(np.abs(ref["dp"])))
+        assert J3 <= J2 and 2 <= e3 <= 10
