@@ -29,6 +29,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (AMD spec; 1/2 of the 157.3 TF FP32 vector peak)
 
 
 def parse():
@@ -300,6 +301,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    fp64 = None
+    if wl == "linear":
+        # SURVEY.md 8(d) dense FLOP count per trajectory (81 032 at S=10);
+        # the kernel's banded / time-scaled route does fewer operations.
+        nf_, np_ = plan.n_fixed, plan.n_free
+        flops = (4 * N ** 3 * S + N ** 2 * S + np_ ** 3 / 3 + 2 * np_ * nf_ * D
+                 + 2 * np_ ** 2 * D + 2 * N ** 2 * D * S + D * S * (2 * N ** 2 + 2 * N))
+        tf = flops * B / (kernel_ms * 1e-3) / 1e12
+        fp64 = {"algorithmic_flops_per_traj": flops, "achieved_tflops": tf,
+                "peak_tflops": FP64_PEAK_TFLOPS, "frac": tf / FP64_PEAK_TFLOPS}
     total_units = units_per_step * args.steps * world
     value = total_units / elapsed
     alg_bytes = bytes_per_traj * B
@@ -335,7 +346,8 @@ def main():
                          "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes,
                          "kernel_timing": ("HIP events around one graph replay of the K "
                                            "launches, / K" if use_graph else
-                                           "HIP event pair per launch, mean")},
+                                           "HIP event pair per launch, mean"),
+                         "fp64_vector": fp64},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
