@@ -2,8 +2,8 @@
 // the segment-time optimisation of the reference
 // (include/mav_tube_trajectory_generation/polynomial_optimization_nonlinear.h:
 // 46-674, impl/polynomial_optimization_nonlinear_impl.h "nonlinear_impl"),
-// restricted to the objective on the hot path:
-// kOptimizeTime with the time-only cost callback
+// restricted to the objectives on the hot path (SURVEY.md §8a T1-T6 and §8f
+// rank 2): kOptimizeTime with the time-only cost callback
 //   J(T) = computeCost() + time_penalty * (sum_i T_i)^2
 // (objectiveFunctionTime, nonlinear_impl:877-945, w_c = 0, optional soft
 // magnitude constraints).  Both the callback (evaluateTimeCost -> mtg_time_cost) and
@@ -82,6 +82,10 @@ struct NonlinearOptimizationParameters {
   cost_weights weights;
   double map_resolution = 0.0;
   int side = 5;
+  // Map bounds on the intermediate positions (read by the hard bounds of
+  // kOptimizeFreeConstraints, nonlinear_impl:2876-2887; Eigen::Vector3d there).
+  VectorXd min_bound = VectorXd::Zero(3);
+  VectorXd max_bound = VectorXd::Zero(3);
   bool use_numeric_grad = false;
   bool use_continous_distance = false;
   double increment_time = 0.1;  // read (gradient step)
@@ -191,11 +195,31 @@ class PolynomialOptimizationNonLinear {
     return J;
   }
 
-  // Runs the optimisation (objective kOptimizeTime only).  Returns a
-  // positive NLopt-style success code (1) or a negative failure code.
+  // objectiveFunctionFreeConstraints (nonlinear_impl:1021-1113) on the
+  // tube-pattern problem (poly_opt_): J_d = sum_dim d^T R d [+ soft], with
+  // gradient dJ_d/dd_p per dimension when `gradient` is non-null.
+  double evaluateFreeConstraintsCost(const std::vector<VectorXd>& free_constraints,
+                                     std::vector<VectorXd>* gradient) {
+    return freeCost(segmentTimesOfQcqp(), free_constraints, 0, gradient);
+  }
+
+  // objectiveFunctionTimeAndConstraints (nonlinear_impl:947-1019): segment
+  // times and free derivatives given, J = computeCost() + time_penalty
+  // (sum T)^2 [+ soft], no re-solve.
+  double evaluateTimeAndFreeConstraintsCost(const std::vector<double>& segment_times,
+                                            const std::vector<VectorXd>& free_constraints) {
+    return freeCost(segment_times, free_constraints, 1, nullptr);
+  }
+
+  // Runs the optimisation: kOptimizeTime, or kOptimizeFreeConstraints
+  // (optimizeFreeConstraints, nonlinear_impl:399-493, on the device).
+  // Returns a positive NLopt-style success code or a negative failure code.
   int optimize() {
+    if (params_.objective == NonlinearOptimizationParameters::kOptimizeFreeConstraints)
+      return optimizeFreeConstraints();
     MTG_CHECK(params_.objective == NonlinearOptimizationParameters::kOptimizeTime,
-              "only kOptimizeTime is part of this build (SURVEY.md 8a T1-T6)");
+              "objective not part of this build: kOptimizeTime and kOptimizeFreeConstraints "
+              "(SURVEY.md 8a T1-T6, 8f rank 2)");
     warnCollision();
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<double> times;
@@ -238,7 +262,14 @@ class PolynomialOptimizationNonLinear {
     return optimization_info_.stopping_reason;
   }
 
-  void getTrajectory(Trajectory* trajectory) const { linear_.getTrajectory(trajectory); }
+  // The optimised trajectory: the linear problem's (kOptimizeTime) or the
+  // tube-pattern problem's (after kOptimizeFreeConstraints).
+  void getTrajectory(Trajectory* trajectory) const {
+    if (free_optimized_)
+      poly_opt_.getTrajectory(trajectory);
+    else
+      linear_.getTrajectory(trajectory);
+  }
   void getQCQPTrajectory(Trajectory* trajectory) const { poly_opt_.getTrajectory(trajectory); }
   void getInitialSolutionTrajectory(Trajectory* trajectory) const {
     MTG_CHECK(trajectory != nullptr, "trajectory must not be null");
@@ -263,6 +294,133 @@ class PolynomialOptimizationNonLinear {
   }
 
  private:
+  std::vector<double> segmentTimesOfQcqp() const {
+    std::vector<double> t;
+    poly_opt_.getSegmentTimes(&t);
+    return t;
+  }
+
+  std::vector<double> packFree(const std::vector<VectorXd>& free_constraints) const {
+    const size_t np = poly_opt_.getNumberFreeConstraints();
+    MTG_CHECK(free_constraints.size() == dimension_,
+              "free constraints: need " << dimension_ << " dimensions");
+    std::vector<double> out;
+    for (const VectorXd& v : free_constraints) {
+      MTG_CHECK(static_cast<size_t>(v.size()) == np, "free constraints: need " << np
+                                                         << " entries per dimension");
+      for (long i = 0; i < v.size(); ++i) out.push_back(v[i]);
+    }
+    return out;
+  }
+
+  std::vector<double> packFixedQcqp() const {
+    std::vector<VectorXd> df;
+    poly_opt_.getFixedConstraints(&df);
+    std::vector<double> out;
+    for (const VectorXd& v : df)
+      for (long i = 0; i < v.size(); ++i) out.push_back(v[i]);
+    return out;
+  }
+
+  double freeCost(const std::vector<double>& segment_times,
+                  const std::vector<VectorXd>& free_constraints, int mode,
+                  std::vector<VectorXd>* gradient) {
+    const size_t np = poly_opt_.getNumberFreeConstraints();
+    MTG_CHECK(segment_times.size() == poly_opt_.getNumberSegments(), "segment_times size");
+    warnCollision();
+    const std::vector<double> dp = packFree(free_constraints);
+    internal::DeviceBuffer<double> d_df, d_dp, d_t, d_cost(1), d_g(dp.size() ? dp.size() : 1);
+    d_df.upload(packFixedQcqp());
+    d_dp.upload(dp);
+    d_t.upload(segment_times);
+    const mtg_time_params p = timeParams(0);
+    internal::checkStatus(
+        mtg_free_cost(poly_opt_.getPlan(), 1, d_df.get(), d_dp.get(), d_t.get(), &p, mode,
+                      d_cost.get(), (gradient && mode == 0) ? d_g.get() : nullptr, nullptr,
+                      nullptr),
+        "mtg_free_cost");
+    internal::synchronize();
+    double J = 0.0;
+    d_cost.download(&J, 1);
+    if (gradient && mode == 0) {
+      const std::vector<double> g = d_g.download();
+      gradient->assign(dimension_, VectorXd(static_cast<long>(np)));
+      for (size_t d = 0; d < dimension_; ++d)
+        for (size_t i = 0; i < np; ++i) (*gradient)[d][i] = g[d * np + i];
+    }
+    return J;
+  }
+
+  // optimizeFreeConstraints (nonlinear_impl:399-493): initial solution from
+  // the tube QCQP (:405-416; the fork's
+  // computeInitialSolutionWithPositionConstraints rebuilds the same tube
+  // pattern and recovers the same d_p), hard bounds of
+  // setFreeEndpointDerivativeHardConstraints (:2858-2905), then the device
+  // optimiser of mtg_free_optimize in place of NLopt with max_iterations
+  // objective evaluations.
+  int optimizeFreeConstraints() {
+    warnCollision();
+    const auto t0 = std::chrono::steady_clock::now();
+    poly_opt_.solveQCQP();
+    poly_opt_.getTrajectory(&trajectory_initial_);
+    std::vector<VectorXd> free;
+    poly_opt_.getFreeConstraints(&free);
+    const std::vector<double> x0 = packFree(free);
+    const size_t np = poly_opt_.getNumberFreeConstraints();
+    const size_t S = poly_opt_.getNumberSegments();
+    std::vector<double> lo(x0.size(), -HUGE_VAL), hi(x0.size(), HUGE_VAL);
+    const int r = poly_opt_.getDerivativeToOptimize();
+    for (size_t k = 0; k < dimension_; ++k)
+      for (size_t n = 0; n + 1 < S; ++n) {
+        size_t start;
+        if (params_.solve_with_position_constraint) {
+          start = k * np + n * r;
+        } else {
+          start = k * np + n * (r + 1);
+          lo[start] = params_.min_bound[static_cast<long>(k)];
+          hi[start] = params_.max_bound[static_cast<long>(k)];
+        }
+        for (const auto& c : soft_) {
+          const size_t idx =
+              start + (params_.solve_with_position_constraint ? c.first - 1 : c.first);
+          lo[idx] = -std::abs(c.second);
+          hi[idx] = std::abs(c.second);
+        }
+      }
+    internal::DeviceBuffer<double> d_df, d_dp, d_t, d_lo, d_hi, d_cost(1);
+    internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
+    d_df.upload(packFixedQcqp());
+    d_dp.upload(x0);
+    d_t.upload(segmentTimesOfQcqp());
+    d_lo.upload(lo);
+    d_hi.upload(hi);
+    const mtg_time_params p = timeParams(0);
+    const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
+    internal::checkStatus(mtg_free_optimize(poly_opt_.getPlan(), 1, d_df.get(), d_dp.get(),
+                                            d_t.get(), d_lo.get(), d_hi.get(), &p, budget,
+                                            d_cost.get(), d_ev.get(), d_st.get(), nullptr),
+                          "mtg_free_optimize");
+    internal::synchronize();
+    const std::vector<double> x = d_dp.download();
+    for (size_t d = 0; d < dimension_; ++d)
+      for (size_t i = 0; i < np; ++i) free[d][i] = x[d * np + i];
+    poly_opt_.setFreeConstraints(free);
+    int32_t evals = 0, st = 0;
+    d_ev.download(&evals, 1);
+    d_st.download(&st, 1);
+    double J = 0.0;
+    d_cost.download(&J, 1);
+    optimization_info_.n_iterations = evals;
+    optimization_info_.cost_trajectory = 2.0 * poly_opt_.computeCost();  // J_d
+    optimization_info_.cost_soft_constraints =
+        soft_.empty() ? 0.0 : J - optimization_info_.cost_trajectory;
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
+    optimization_info_.optimization_time =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    free_optimized_ = true;
+    return optimization_info_.stopping_reason;
+  }
+
   mtg_time_params timeParams(int grad_mode) const {
     mtg_time_params p;
     p.time_penalty = params_.time_penalty;
@@ -301,6 +459,7 @@ class PolynomialOptimizationNonLinear {
   Trajectory trajectory_initial_;
   OptimizationInfo optimization_info_;
   std::vector<std::pair<int, double>> soft_;  // (derivative, maximum_value)
+  bool free_optimized_ = false;
 };
 
 }  // namespace mav_trajectory_generation
