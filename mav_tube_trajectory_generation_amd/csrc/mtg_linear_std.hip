@@ -29,17 +29,20 @@ __global__ __launch_bounds__(kWave) void linear_std_kernel(
   // Inputs: times, fixed values and the lane's two rows of H(1) are all
   // issued before the first use.
   Sv sv;
-  sv.init(S, smem, tab);
+  sv.init(S, smem, nullptr);
   const int lane = sv.lane, nf = sv.nf;
   const double* tb = times + b * S;
   const double* fb = fixed_vals + b * D * nf;
+  // Times first, then fixed values, then the table rows: loads retire in
+  // issue order, so the powers wait only for the times.
   const double t_l = lane < S ? tb[lane] : 1.0;
   const double f_l = lane < D * nf ? fb[lane] : 0.0;
-  if (lane < D * nf) sv.put_fixed(lane, f_l);
-  for (int i = lane + kWave; i < D * nf; i += kWave) sv.put_fixed(i, fb[i]);
-  MTG_STAMP(7);
+  sv.load_first_rows(tab);
   bool bad = lane < S ? sv.powers(lane, t_l) : false;
   for (int s = lane + kWave; s < S; s += kWave) bad = sv.powers(s, tb[s]) || bad;
+  MTG_STAMP(7);
+  if (lane < D * nf) sv.put_fixed(lane, f_l);
+  for (int i = lane + kWave; i < D * nf; i += kWave) sv.put_fixed(i, fb[i]);
   if (lane < Sv::BS) smem[sv.L.Tm + lane] = 0.0;
   const bool bad_time = __any(bad);
   __syncthreads();

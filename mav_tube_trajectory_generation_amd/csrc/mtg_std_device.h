@@ -241,12 +241,19 @@ struct Solver {
   __device__ double* dv() const { return sm + L.dv; }
   __device__ double* aux() const { return sm + L.aux; }
 
+  // tab == nullptr: the caller issues its own input loads first and calls
+  // load_first_rows(tab) afterwards (vector loads retire in issue order, so
+  // the inputs are then not held back behind the table rows).
   __device__ void init(int S_, double* smem, const double* __restrict__ tab) {
     S = S_;
     lane = threadIdx.x;
     nf = 2 * M + S - 1;
     L = layout(N, S, D);
     sm = smem;
+    if (tab) load_first_rows(tab);
+  }
+
+  __device__ void load_first_rows(const double* __restrict__ tab) {
     const int nrows = (S - 1) * MF;
     load_rows(tab, (lane < nrows ? lane : 0) % MF + 1);
   }

@@ -38,7 +38,7 @@ def main():
         L.mtg_debug_stamps_std(st, 512)
         runs.append(np.array(st[:], dtype=np.int64))
     st = np.median(np.array(runs), axis=0)
-    order = [(0, "start"), (7, "inputs arrived, fixed stored"), (1, "powers"),
+    order = [(0, "start"), (7, "times arrived, powers"), (1, "fixed stored"),
              (2, "assembly")]
     k = 0
     while st[100 + 2 * k] > 0:
