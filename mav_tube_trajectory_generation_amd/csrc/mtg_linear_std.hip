@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kWave) void linear_std_kernel(
   MTG_STAMP(7);
   if (lane < D * nf) sv.put_fixed(lane, f_l);
   for (int i = lane + kWave; i < D * nf; i += kWave) sv.put_fixed(i, fb[i]);
-  if (lane < Sv::BS) smem[sv.L.Tm + lane] = 0.0;
+  sv.clear_mid_terms();
   const bool bad_time = __any(bad);
   __syncthreads();
   MTG_STAMP(1);

@@ -22,8 +22,9 @@
 //   * twisted block LDL^T: lanes 0.. sweep forward over v = 1..m-1, lanes
 //     32.. backward over v = S-1..m+1 in one instruction stream; in a chain
 //     lane c < MF maps coupling column c, lane MF + d right-hand side d, all
-//     through the same code (r = u - G^T w, x = S^-1 r, out = a - G^T x; the
-//     data decides the role).  Every operand is a contiguous row (C_v and
+//     through the same code with the step's coupling P (x = S^-1 u,
+//     out = a - P^T x: the next Schur column, or the next right-hand side
+//     b_next - P^T z_v; the data decides the role).  Every operand is a contiguous row (C_v and
 //     C_v^T are both stored, Schur complements by rows), so a lane's
 //     addresses are one base plus immediate offsets; next-step operands are
 //     prefetched before the barrier;
@@ -57,22 +58,22 @@ __device__ inline double rcp64_1(double d) {
 }
 
 // x = S^-1 r for a symmetric MF x MF block (lower triangle of S used) by
-// LDL^T in registers.  Returns false on a non-positive pivot (the pivot is
-// then replaced by 1 to keep the arithmetic finite).
+// LDL^T in registers.  pmin <- min(pmin, pivots): a non-positive value flags
+// a matrix that is not positive definite (the caller reports it; the values
+// computed from such a pivot are not used).
 template <int MF>
-__device__ inline bool ldlt_solve(const double (&S)[MF][MF], const double (&r)[MF],
-                                  double (&x)[MF]) {
+__device__ inline void ldlt_solve(const double (&S)[MF][MF], const double (&r)[MF],
+                                  double (&x)[MF], double& pmin) {
   double Lr[MF][MF];  // Lr[i][j] = L_ij * d_j (i > j)
   double l[MF][MF];   // l[i][j]  = L_ij
   double inv[MF];
-  bool ok = true;
 #pragma unroll
   for (int j = 0; j < MF; ++j) {
     double dj = S[j][j];
 #pragma unroll
     for (int k = 0; k < j; ++k) dj = fma(-Lr[j][k], l[j][k], dj);
-    ok = ok && (dj > 0.0);
-    inv[j] = rcp64_1(dj > 0.0 ? dj : 1.0);
+    pmin = fmin(pmin, dj);
+    inv[j] = rcp64_1(dj);
 #pragma unroll
     for (int i = j + 1; i < MF; ++i) {
       double s = S[i][j];
@@ -97,7 +98,6 @@ __device__ inline bool ldlt_solve(const double (&S)[MF][MF], const double (&r)[M
     for (int k = i + 1; k < MF; ++k) s = fma(-l[k][i], x[k], s);
     x[i] = s;
   }
-  return ok;
 }
 
 // K doubles from / to LDS, 16-byte accesses for the pairs (callers keep the
@@ -203,7 +203,7 @@ struct Layout {
   int Zt;    // (S+1) * BS: Z_v^T (row c = column c of Z_v)
   int bz;    // (S+1) * D * RS: b_v, then z_v, [v][d][i]
   int Tm;    // BS: backward chain's Schur term at the middle vertex
-  int junk;  // RS: sink for the rhs lanes' unused sweep output
+  int Rmb;   // D * RS: backward chain's right-hand-side term at the middle vertex
   int aux;   // 6S + 8: segment times and optimiser state (time kernels)
   int n;
 };
@@ -222,7 +222,7 @@ __host__ __device__ inline Layout layout(int N, int S, int D) {
   l.Zt = o; o += (S + 1) * BS;
   l.bz = o; o += (S + 1) * D * RS;
   l.Tm = o; o += BS;
-  l.junk = o; o += RS;
+  l.Rmb = o; o += D * RS;
   l.aux = o; o += even(6 * S + 8);
   l.n = o;
   return l;
@@ -310,12 +310,17 @@ struct Solver {
     return bad;
   }
 
+  // Tm and Rmb (contiguous) start at zero: a chain with no steps leaves them.
+  __device__ void clear_mid_terms() {
+    for (int i = lane; i < BS + D * RS; i += kWave) sm[L.Tm + i] = 0.0;
+  }
+
   // Powers of every segment from times in LDS (all lanes call; wave-uniform
   // result: any invalid time).  Also clears Tm.  Caller barriers after.
   __device__ bool powers_from(const double* T) {
     bool bad = false;
     for (int s = lane; s < S; s += kWave) bad = powers(s, T[s]) || bad;
-    if (lane < BS) sm[L.Tm + lane] = 0.0;
+    clear_mid_terms();
     return __any(bad);
   }
 
@@ -386,7 +391,7 @@ struct Solver {
   __device__ bool solve() {
     const int m = S / 2;  // middle vertex, 1 <= m <= S-1
     const int g = lane >> 5, q = lane & 31;
-    bool ok = true;
+    double pmin = 1.0;  // smallest pivot seen by this lane
     {
       const bool cpl = q < MF;  // coupling-column lane
       const bool rhs = q >= MF && q < MF + D;
@@ -395,29 +400,31 @@ struct Solver {
       const int kmax = (m - 1) > (S - 1 - m) ? (m - 1) : (S - 1 - m);
       const int dir = g == 0 ? 1 : -1;
       const int v0 = g == 0 ? 1 : S - 1;
-      // Per-lane operand rows at step 0 and their per-step strides.
-      //   coupling lane c: G = P (forward C_v, backward C_{v-1}^T), u = P[:, c]
-      //   (= row c of P^T), a = row c of S_next; x -> row c of Z_v^T,
-      //   out -> row c of S_next (or Tm at the backward chain's last step).
-      //   rhs lane d: G = Q (forward C_{v-1}, backward C_v^T), u = b_v[d];
-      //   x -> z_v[d] (in place of b), out -> junk.
-      const int gofs = cpl ? (g == 0 ? L.Cs + v0 * BS : L.Ct + (v0 - 1) * BS)
-                           : (g == 0 ? L.Cs + (v0 - 1) * BS : L.Ct + v0 * BS);
+      // Every lane of a chain uses the same coupling P of its step (forward
+      // C_v, backward C_{v-1}^T) and computes x = S_v^-1 u, out = a - P^T x:
+      //   coupling lane c: u = P[:, c] (= row c of P^T), a = row c of A_next;
+      //     x -> row c of Z_v^T, out -> row c of S_next;
+      //   rhs lane d: u = r_v[d] (b_v at the first step), a = b_next[d];
+      //     x = z_v -> in place of r_v, out = r_next = b_next - P^T z_v -> in
+      //     place of b_next, where the next step reads it as u.
+      // The forward chain's last step leaves S_m and r_m with its term
+      // subtracted in place; the backward chain's last step (a = 0) stores its
+      // terms alone into Tm and Rmb.
+      const int gofs = g == 0 ? L.Cs + v0 * BS : L.Ct + (v0 - 1) * BS;
+      const int gstep = dir * BS;
       const int uofs = cpl ? (g == 0 ? L.Ct + v0 * BS : L.Cs + (v0 - 1) * BS) + c * RS
                            : L.bz + (v0 * D + dd) * RS;
       const int ustep = cpl ? dir * BS : dir * D * RS;
-      const int aofs = L.Sb + (v0 + dir) * BS + c * RS;
+      const int aofs = cpl ? L.Sb + (v0 + dir) * BS + c * RS : L.bz + ((v0 + dir) * D + dd) * RS;
       const int xofs = cpl ? L.Zt + v0 * BS + c * RS : uofs;
-      const double rf = rhs ? 1.0 : 0.0;
-      double w[MF], G[MF][MF], u[MF], a[MF];
-#pragma unroll
-      for (int i = 0; i < MF; ++i) w[i] = 0.0;
+      const int mofs = cpl ? L.Tm + c * RS : L.Rmb + dd * RS;  // backward last step
+      double G[MF][MF], u[MF], a[MF];
       auto load_ops = [&](int k) {
-        const double* Gp = sm + gofs + k * dir * BS;
+        const double* Gp = sm + gofs + k * gstep;
 #pragma unroll
         for (int i = 0; i < MF; ++i) lds_load(Gp + i * RS, G[i]);
         lds_load(sm + uofs + k * ustep, u);
-        lds_load(sm + aofs + k * dir * BS, a);
+        lds_load(sm + aofs + k * ustep, a);
       };
       const bool lane_act = cpl || rhs;
       if (lane_act && nst > 0) load_ops(0);
@@ -433,20 +440,10 @@ struct Solver {
 #pragma unroll
             for (int j = 0; j <= i; ++j) Sv[i][j] = row[j];
           }
-          double rr[MF];
-#pragma unroll
-          for (int i = 0; i < MF; ++i) rr[i] = u[i];
-          if (k > 0) {  // r = u - Q^T z_prev (w = 0 on coupling lanes)
-#pragma unroll
-            for (int i = 0; i < MF; ++i)
-#pragma unroll
-              for (int j = 0; j < MF; ++j) rr[i] = fma(-G[j][i], w[j], rr[i]);
-          }
           double x[MF];
-          ok = ldlt_solve<MF>(Sv, rr, x) && ok;
-          // The backward chain's last step stores its term alone (into Tm).
-          const bool to_tm = cpl && g == 1 && k == nst - 1;
-          const double af = to_tm ? 0.0 : 1.0;
+          ldlt_solve<MF>(Sv, u, x, pmin);
+          const bool last_b = g == 1 && k == nst - 1;
+          const double af = last_b ? 0.0 : 1.0;
           double out[MF];
 #pragma unroll
           for (int i = 0; i < MF; ++i) {
@@ -455,13 +452,8 @@ struct Solver {
             for (int j = 0; j < MF; ++j) s = fma(-G[j][i], x[j], s);
             out[i] = s;
           }
-          const int xo = xofs + k * (cpl ? dir * BS : ustep);
-          int oo = cpl ? aofs + k * dir * BS : L.junk;
-          if (to_tm) oo = L.Tm + c * RS;
-          lds_store(sm + xo, x);
-          lds_store(sm + oo, out);
-#pragma unroll
-          for (int i = 0; i < MF; ++i) w[i] = x[i] * rf;
+          lds_store(sm + xofs + k * ustep, x);
+          lds_store(sm + (last_b ? mofs : aofs + k * ustep), out);
           if (k + 1 < nst) load_ops(k + 1);
         }
         __syncthreads();
@@ -470,8 +462,8 @@ struct Solver {
     MTG_STAMP(3);
 
     // Middle vertex and back substitution outward from it:
-    //   S_m = (A_m - forward term) + Tm,
-    //   r_m = b_m - C_{m-1}^T z_{m-1} - C_m z'_{m+1},  x_v = z_v - Z_v x_(toward m).
+    //   S_m = (A_m - forward term) + Tm,  r_m = (b_m - forward term) + Rmb
+    //   (= b_m - C_{m-1}^T z_{m-1} - C_m z'_{m+1}),  x_v = z_v - Z_v x_(toward m).
     // Lanes: for MF <= 4 a quad per (half g, dimension d), lane = g*32 + 4d + i
     // owning row i (the middle block is solved redundantly by all of them, so
     // no exchange precedes the back substitution, whose x_next rows are
@@ -495,30 +487,14 @@ struct Solver {
 #pragma unroll
         for (int j = 0; j <= i; ++j) Sv[i][j] = row[j] + tm[j];
       }
-      lds_load(bz + (m * D + d) * RS, rr);
-      if (m >= 2) {
-        double z[MF];
-        lds_load(bz + ((m - 1) * D + d) * RS, z);
+      {
+        double r0[MF], r1[MF];
+        lds_load(bz + (m * D + d) * RS, r0);
+        lds_load(sm + L.Rmb + d * RS, r1);
 #pragma unroll
-        for (int i = 0; i < MF; ++i) {
-          double row[MF];
-          lds_load(sm + L.Ct + (m - 1) * BS + i * RS, row);
-#pragma unroll
-          for (int j = 0; j < MF; ++j) rr[i] = fma(-row[j], z[j], rr[i]);
-        }
+        for (int i = 0; i < MF; ++i) rr[i] = r0[i] + r1[i];
       }
-      if (m <= S - 2) {
-        double z[MF];
-        lds_load(bz + ((m + 1) * D + d) * RS, z);
-#pragma unroll
-        for (int i = 0; i < MF; ++i) {
-          double row[MF];
-          lds_load(sm + L.Cs + m * BS + i * RS, row);
-#pragma unroll
-          for (int j = 0; j < MF; ++j) rr[i] = fma(-row[j], z[j], rr[i]);
-        }
-      }
-      ok = ldlt_solve<MF>(Sv, rr, x) && ok;
+      ldlt_solve<MF>(Sv, rr, x, pmin);
       MTG_STAMP(4);
       const int n_back = g == 0 ? m - 1 : S - 1 - m;
       const int vstep = g == 0 ? -1 : 1;
@@ -579,7 +555,7 @@ struct Solver {
         }
       }
     }
-    const bool not_spd = __any(!ok);
+    const bool not_spd = __any(!(pmin > 0.0));
     __syncthreads();
     MTG_STAMP(5);
     return not_spd;
