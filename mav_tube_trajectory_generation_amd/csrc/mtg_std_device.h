@@ -135,13 +135,14 @@ __device__ inline double dpp_add(double x) {
   return x + join64(lo, hi);
 }
 
-// Value of lane j of this lane's quad (DPP quad_perm [j, j, j, j]).
+// Value of lane j of this lane's quad (DPP quad_perm [j, j, j, j]).  Every
+// source lane is valid, so the DPP `old` operand is left undefined (mov_dpp):
+// one v_mov_b32_dpp per half, no initialisation of the destination.
 template <int J>
 __device__ inline double quad_bcast(double x) {
   const long long u = __builtin_bit_cast(long long, x);
-  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(u), J * 0x55, 0xf, 0xf, false);
-  const int hi =
-      __builtin_amdgcn_update_dpp(0, static_cast<int>(u >> 32), J * 0x55, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(u), J * 0x55, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(u >> 32), J * 0x55, 0xf, 0xf, false);
   return join64(lo, hi);
 }
 
@@ -503,15 +504,8 @@ struct Solver {
 #pragma unroll
         for (int i = 1; i < MF; ++i) xi = pi == i ? x[i] : xi;
         if (g == 0) dvp[(m * D + d) * MP + 1 + pi] = xi;
-        double zr[MF], zz = 0.0;  // row pi of Z_v and z_v[pi][d] of the next step
-        auto load_b = [&](int vv) {
-#pragma unroll
-          for (int c2 = 0; c2 < MF; ++c2) zr[c2] = Zt[vv * BS + c2 * RS + pi];
-          zz = bz[(vv * D + d) * RS + pi];
-        };
-        int v = m + vstep;
-        if (n_back > 0) load_b(v);
-        for (int k = 0; k < n_back; ++k, v += vstep) {
+        MTG_STAMP(8);
+        auto step = [&](const double (&zr)[MF], double zz) {
           double xb[4];
           xb[0] = quad_bcast<0>(xi);
           if (MF > 1) xb[1] = quad_bcast<1>(xi);
@@ -520,9 +514,27 @@ struct Solver {
           double s2 = zz;
 #pragma unroll
           for (int j = 0; j < MF; ++j) s2 = fma(-zr[j], xb[j], s2);
-          if (k + 1 < n_back) load_b(v + vstep);
           xi = s2;
-          dvp[(v * D + d) * MP + 1 + pi] = s2;
+        };
+        // x_next row pi from Z_v's row pi and the broadcast rows of x (the
+        // next step's operands are loaded before this step's chain).  A DPP
+        // broadcast after a VALU result costs ~20 cycles of latency
+        // (tools/ubench/fp64_latency.hip), so a step is ~70 cycles.
+        double zr[MF], zz = 0.0;
+        auto load_b = [&](int vv) {
+#pragma unroll
+          for (int c2 = 0; c2 < MF; ++c2) zr[c2] = Zt[vv * BS + c2 * RS + pi];
+          zz = bz[(vv * D + d) * RS + pi];
+        };
+        int v = m + vstep;
+        if (n_back > 0) load_b(v);
+        for (int k = 0; k < n_back; ++k, v += vstep) {
+          double zc[MF], zzc = zz;
+#pragma unroll
+          for (int c2 = 0; c2 < MF; ++c2) zc[c2] = zr[c2];
+          if (k + 1 < n_back) load_b(v + vstep);
+          step(zc, zzc);
+          dvp[(v * D + d) * MP + 1 + pi] = xi;
         }
       } else {
         if (g == 0) {
@@ -554,6 +566,7 @@ struct Solver {
           }
         }
       }
+      MTG_STAMP(9);
     }
     const bool not_spd = __any(!(pmin > 0.0));
     __syncthreads();

@@ -3,9 +3,10 @@ diagnostic build (make STAMPS=1 STAMPS_OUT=...):
 
 MTG_LIB_PATH=mav_tube_trajectory_generation_amd/libmtg_hip_stamps.so \
     python tools/stamps_std.py [B]
-Slots (mtg_linear_std.hip): 0 start, 1 inputs+powers, 2 assembly,
-100+2k sweep step k start, 3 sweep end, 4 middle vertex, 5 back
-substitution, 6 coefficients/cost/stores.
+Slots (mtg_linear_std.hip, mtg_std_device.h): 0 start, 7 times + powers,
+1 fixed values, 2 assembly, 100+2k sweep step k start, 3 sweep end,
+4 middle-vertex loads, 8 middle-vertex LDL^T, 9 back-substitution steps,
+5 back substitution end (any/barrier), 6 coefficients/cost/stores.
 """
 import ctypes
 import os
@@ -44,8 +45,13 @@ def main():
     while st[100 + 2 * k] > 0:
         order.append((100 + 2 * k, f"(sweep step {k} start)"))
         k += 1
-    order += [(3, "sweep end"), (4, "middle vertex solve"), (5, "back substitution"),
-              (6, "coeffs + cost + stores")]
+    order += [(3, "sweep end"), (4, "middle vertex loads")]
+    if st[8] > 0:  # finer slots of the middle vertex / back substitution
+        order += [(8, "middle vertex LDL^T")]
+        if st[10] > 0:
+            order += [(10, "back-sub loads"), (11, "back-sub chain")]
+        order += [(9, "back substitution steps")]
+    order += [(5, "back substitution end"), (6, "coeffs + cost + stores")]
     print(f"phase cycles (workgroup 0, median of 7, B={B}):")
     prev = st[0]
     for slot, name in order[1:]:

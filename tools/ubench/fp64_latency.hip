@@ -43,6 +43,16 @@ __global__ void bench(double* out, unsigned long long* cyc, double seed) {
       x0 = fma(__builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo), b, c);
     } else if (KIND == 6) {  // dependent mul chain
       x0 = x0 * b;
+    } else if (KIND == 8) {  // back-substitution step: 4 quad broadcasts (mov_dpp) + 4-FMA chain
+      long long u = __builtin_bit_cast(long long, x0);
+      double xb[4];
+#define QB(J) xb[J] = __builtin_bit_cast(double, ((long long)__builtin_amdgcn_mov_dpp((int)(u >> 32), J * 0x55, 0xf, 0xf, false) << 32) | \
+                      (unsigned)__builtin_amdgcn_mov_dpp((int)u, J * 0x55, 0xf, 0xf, false))
+      QB(0); QB(1); QB(2); QB(3);
+#undef QB
+      double s2 = x1;
+      s2 = fma(-x2, xb[0], s2); s2 = fma(-x3, xb[1], s2); s2 = fma(-x4, xb[2], s2); s2 = fma(-x5, xb[3], s2);
+      x0 = s2 * 1e-3;
     } else if (KIND == 7) {  // dependent readlane broadcast through fma
       x0 = fma(__builtin_bit_cast(double, (long long)(unsigned)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(long long, x0)), 3) |
                   ((long long)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(long long, x0) >> 32), 3) << 32)), b, c);
@@ -57,10 +67,10 @@ __global__ void bench(double* out, unsigned long long* cyc, double seed) {
 int main() {
   double* out; unsigned long long* cyc;
   hipMalloc(&out, 1 << 20); hipMalloc(&cyc, 4096);
-  const char* names[] = {"fma_f64 dep", "fma_f64 8-indep", "rcp_f64 dep", "rcp_f64 8-indep", "ds_read_b64 dep", "dpp+fma dep", "mul_f64 dep", "readlane+fma dep"};
-  const int ops[] = {256, 2048, 256, 2048, 256, 256, 256, 256};
+  const char* names[] = {"fma_f64 dep", "fma_f64 8-indep", "rcp_f64 dep", "rcp_f64 8-indep", "ds_read_b64 dep", "dpp+fma dep", "mul_f64 dep", "readlane+fma dep", "backsub step"};
+  const int ops[] = {256, 2048, 256, 2048, 256, 256, 256, 256, 256};
   for (int rep = 0; rep < 2; ++rep) {
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 9; ++k) {
       switch (k) {
         case 0: bench<0><<<1, 64>>>(out, cyc, 1.0); break;
         case 1: bench<1><<<1, 64>>>(out, cyc, 1.0); break;
@@ -70,6 +80,7 @@ int main() {
         case 5: bench<5><<<1, 64>>>(out, cyc, 1.0); break;
         case 6: bench<6><<<1, 64>>>(out, cyc, 1.0); break;
         case 7: bench<7><<<1, 64>>>(out, cyc, 1.0); break;
+        case 8: bench<8><<<1, 64>>>(out, cyc, 1.0); break;
       }
       unsigned long long h;
       hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost);
