@@ -288,6 +288,42 @@ int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                    double* coeffs, double* cost, int32_t* iters,
                    int32_t* status, void* stream);
 
+/* Segment-time objective with the QCQP inner solve: the fork's
+ * objectiveFunctionTime (nonlinear_impl:877-945), which calls solveQCQP()
+ * after updateSegmentTimes (:891-892; mtg_time_cost is the upstream,
+ * linear-inner form).  J = computeCost() of the QCQP solution at `times`
+ * + time_penalty (sum T)^2 [+ soft, as mtg_time_cost]; the control-point
+ * maps use `times_cp` (the times at setup, qcqp_impl:152-157).  J is NaN
+ * where the QCQP breaks down (status MTG_TRAJ_NOT_SPD) or a time is not
+ * positive.  grad_mode 0 (none; the reference callback is gradient-free) or
+ * 2 (central differences of the re-solved J, clamp rule of :2525-2530; 2S
+ * extra QCQP solves per trajectory, all in the same launch); grad_mode 1 is
+ * MTG_ERR_UNSUPPORTED.  tol / max_iter as mtg_tube_solve.  Outputs
+ * (device): cost B, grad B x S (grad_mode 2), status B (nullable; the
+ * QCQP status at `times`).  Device scratch is taken stream-ordered
+ * (hipMallocAsync) for the duration of the call. */
+int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                       const double* positions, const double* fixed_vals,
+                       const double* times_cp, const double* times, const double* radii,
+                       double tol, int max_iter, const mtg_time_params* params,
+                       double* cost, double* grad, int32_t* status, void* stream);
+
+/* Batched segment-time optimisation over that objective (optimizeTime,
+ * nonlinear_impl:332-397, in the fork's QCQP form): the optimiser of
+ * mtg_time_optimize (projected, scaled steepest descent with expand /
+ * backtrack on the grad_mode 2 gradient, bounds [0.1, 2 T0], max_evals
+ * counted evaluations), stopping also at a non-finite gradient.  Each round
+ * is one tube launch over B x (2S+1) problems (every trial with its gradient
+ * points); the host waits for each round to know whether any trajectory is
+ * still active, so this call synchronises the stream.
+ *   times_io  B x S  in: T0 (also the control-point times), out: optimised
+ *   cost B, evals B, status B (nullable). */
+int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                           const double* positions, const double* fixed_vals,
+                           const double* radii, double* times_io, double tol, int max_iter,
+                           const mtg_time_params* params, int max_evals, double* cost,
+                           int32_t* evals, int32_t* status, void* stream);
+
 /* ------------------------------------------------------------------------
  * Batched trajectory sampling: Trajectory::evaluateRange (src/trajectory.cpp:
  * 74-134) for derivatives 0..max_derivative at once (the [t, p, v, a, j, s]

@@ -9,8 +9,10 @@ package is the batched front end used by tests and bench.py.
 from ._abi import LIB_PATH, MTGError, lib  # noqa: F401
 from .batch import (Context, LinearPlan, generate_random_problems, max_magnitude,  # noqa: F401
                     sample_trajectories, segment_matrices, soft_constraint_cost,
-                    tube_num_constraints, tube_residuals, tube_solve)
+                    tube_num_constraints, tube_residuals, tube_solve, tube_time_cost,
+                    tube_time_optimize)
 
 __all__ = ["Context", "LinearPlan", "MTGError", "generate_random_problems", "max_magnitude",
            "sample_trajectories", "segment_matrices", "soft_constraint_cost",
-           "tube_num_constraints", "tube_residuals", "tube_solve", "lib", "LIB_PATH"]
+           "tube_num_constraints", "tube_residuals", "tube_solve", "tube_time_cost",
+           "tube_time_optimize", "lib", "LIB_PATH"]

@@ -317,6 +317,59 @@ def tube_solve(ctx, N, r, positions, fixed_vals, times_cp, times, radii, tol=1e-
     return dict(x=x, coeffs=coeffs, cost=cost, iters=iters, status=status)
 
 
+def _tube_geometry(N, positions, fixed_vals, radii, B, S):
+    for name, t, shp in (("positions", positions, (B, S + 1, 3)),
+                         ("fixed_vals", fixed_vals, (B, 3, N)), ("radii", radii, (B, S, 2))):
+        _require(t, shp, name)
+
+
+def tube_time_cost(ctx, N, r, positions, fixed_vals, times_cp, times, radii, time_penalty=500.0,
+                   grad=False, increment=0.1, soft=None, soft_weight=100.0, tol=1e-10,
+                   max_iter=100):
+    """objectiveFunctionTime with the QCQP inner solve (mtg_tube_time_cost):
+    J = computeCost() of the tube QCQP at `times` + time_penalty (sum T)^2
+    [+ soft]; grad=True adds the central-difference gradient (grad_mode 2).
+    Returns dict(cost [B], grad [B, S] or None, status [B])."""
+    import torch
+    B, S = times.shape
+    dev = times.device
+    _tube_geometry(N, positions, fixed_vals, radii, B, S)
+    _require(times_cp, (B, S), "times_cp")
+    _require(times, (B, S), "times")
+    p = make_time_params(time_penalty, increment, 0.1, 1.0, 2 if grad else 0, soft, soft_weight)
+    cost = torch.empty(B, dtype=torch.float64, device=dev)
+    g = torch.empty((B, S), dtype=torch.float64, device=dev) if grad else None
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    check(lib().mtg_tube_time_cost(ctx.handle, N, r, S, B, _ptr(positions), _ptr(fixed_vals),
+                                   _ptr(times_cp), _ptr(times), _ptr(radii), tol, max_iter,
+                                   ctypes.byref(p), _ptr(cost), _ptr(g), _ptr(status),
+                                   _stream(dev)), "mtg_tube_time_cost")
+    return dict(cost=cost, grad=g, status=status)
+
+
+def tube_time_optimize(ctx, N, r, positions, fixed_vals, radii, times, max_evals,
+                       time_penalty=500.0, increment=0.1, soft=None, soft_weight=100.0,
+                       tol=1e-10, max_iter=100):
+    """optimizeTime in the fork's QCQP form (mtg_tube_time_optimize).  times
+    [B, S] are the initial times (and the control-point times); returns
+    dict(times, cost, evals, status) with new tensors."""
+    import torch
+    B, S = times.shape
+    dev = times.device
+    _tube_geometry(N, positions, fixed_vals, radii, B, S)
+    _require(times, (B, S), "times")
+    p = make_time_params(time_penalty, increment, 0.1, 1.0, 2, soft, soft_weight)
+    t = times.clone()
+    cost = torch.empty(B, dtype=torch.float64, device=dev)
+    evals = torch.empty(B, dtype=torch.int32, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    check(lib().mtg_tube_time_optimize(ctx.handle, N, r, S, B, _ptr(positions),
+                                       _ptr(fixed_vals), _ptr(radii), _ptr(t), tol, max_iter,
+                                       ctypes.byref(p), max_evals, _ptr(cost), _ptr(evals),
+                                       _ptr(status), _stream(dev)), "mtg_tube_time_optimize")
+    return dict(times=t, cost=cost, evals=evals, status=status)
+
+
 def sample_trajectories(coeffs, times, dt, t_start=0.0, t_end=-1.0, max_derivative=0,
                         n_max=None, with_times=True):
     """Batched Trajectory::evaluateRange (trajectory.cpp:74-134) for derivatives

@@ -545,6 +545,52 @@ int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* p
                                          static_cast<hipStream_t>(stream)));
 }
 
+static bool valid_tube_time_params(int N, int S, const mtg_time_params* p) {
+  if (!p || p->n_soft < 0 || p->n_soft > mtg::kMaxSoftConstraints) return false;
+  if (p->n_soft > 0 && S > 256) return false;
+  for (int c = 0; c < p->n_soft; ++c) {
+    const int k = p->soft_derivative[c];
+    if (k < 0 || k > mtg::kMaxExtremaDerivative || N - k - 1 <= 0) return false;
+    if (!(p->soft_limit[c] > 0.0)) return false;
+  }
+  return p->increment > 0.0;
+}
+
+int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* positions,
+                       const double* fixed_vals, const double* times_cp, const double* times,
+                       const double* radii, double tol, int max_iter,
+                       const mtg_time_params* params, double* cost, double* grad,
+                       int32_t* status, void* stream) {
+  mtg::TubeArgs a;
+  int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_cp, times, radii, &a);
+  if (rc) return rc;
+  if (!valid_tube_time_params(N, S, params) || !(tol > 0) || max_iter < 1)
+    return MTG_ERR_INVALID_ARG;
+  if (params->grad_mode == 1) return MTG_ERR_UNSUPPORTED;
+  if (params->grad_mode != 0 && params->grad_mode != 2) return MTG_ERR_INVALID_ARG;
+  if (params->grad_mode == 2 && B && !grad) return MTG_ERR_INVALID_ARG;
+  if (B && !cost) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return mtg::tube_time_cost(a, tol, max_iter, *params, cost, grad, status,
+                             static_cast<hipStream_t>(stream));
+}
+
+int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                           const double* positions, const double* fixed_vals,
+                           const double* radii, double* times_io, double tol, int max_iter,
+                           const mtg_time_params* params, int max_evals, double* cost,
+                           int32_t* evals, int32_t* status, void* stream) {
+  mtg::TubeArgs a;
+  // times_cp = the initial times (read before the first write of times_io).
+  int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_io, times_io, radii, &a);
+  if (rc) return rc;
+  if (!valid_tube_time_params(N, S, params) || !(tol > 0) || max_iter < 1 || max_evals < 1)
+    return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  return mtg::tube_time_optimize(a, times_io, tol, max_iter, *params, max_evals, cost, evals,
+                                 status, static_cast<hipStream_t>(stream));
+}
+
 int mtg_generate_random_problems(int N, int D, int S, int64_t B, uint64_t seed0,
                                  double pos_bound, double v_max, double a_max,
                                  uint8_t* fixed_mask, double* fixed_vals, double* times,

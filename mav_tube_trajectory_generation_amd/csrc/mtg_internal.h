@@ -86,6 +86,10 @@ struct TubeArgs {
   const double* times_cp;   // B x S
   const double* times;      // B x S
   const double* radii;      // B x S x 2
+  // Problems per trajectory: problem b takes its times from row b and its
+  // geometry (positions, fixed values, times_cp, radii) from row b / rep
+  // (the evaluation points of mtg_tube_time_cost / _optimize).
+  int rep = 1;
 };
 hipError_t launch_tube_residuals(const TubeArgs& a, const double* x, double* resid,
                                  hipStream_t st);
@@ -93,6 +97,13 @@ hipError_t launch_tube_solve(const TubeArgs& a, double tol, int max_iter, double
                              double* coeffs, double* cost, int32_t* iters,
                              int32_t* status, hipStream_t st);
 size_t tube_lds_bytes(int N, int S);
+// Segment-time objective / optimiser with the QCQP inner solve
+// (mtg_tube_time.hip); return MTG_* codes.
+int tube_time_cost(const TubeArgs& a, double tol, int max_iter, const mtg_time_params& p,
+                   double* cost, double* grad, int32_t* status, hipStream_t st);
+int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_iter,
+                       const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
+                       int32_t* status, hipStream_t st);
 
 constexpr int kMaxLdsBytes = 160 * 1024;
 

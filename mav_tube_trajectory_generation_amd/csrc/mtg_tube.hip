@@ -18,7 +18,7 @@ __device__ inline Tube<N> make_tube(const TubeLayout* L, double* smem, int S, in
 // qcqp_impl:357-474) at x given in the reference's dimension-major order.
 template <int N>
 __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
-    int S, int r, const double* __restrict__ tab, const double* __restrict__ positions,
+    int S, int r, int rep, const double* __restrict__ tab, const double* __restrict__ positions,
     const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
     const double* __restrict__ times, const double* __restrict__ radii,
     const double* __restrict__ x, double* __restrict__ resid) {
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
   int* bad = reinterpret_cast<int*>(smem + L.ndouble);
   const int64_t b = blockIdx.x;
   constexpr int M = N / 2;
-  t.setup(tab, b, positions, fixed_vals, times_cp, times, radii, bad);
+  t.setup(tab, b, b / rep, positions, fixed_vals, times_cp, times, radii, bad);
   const int n = t.nv * 3 * M;
   for (int idx = t.lane; idx < n; idx += kWave) {
     // reference order d*(S-1)*M + (u-1)*M + m  ->  internal ((u-1)*3+d)*M + m
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
 
 template <int N>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void tube_solve_kernel(
-    int S, int r, const double* __restrict__ tab, const double* __restrict__ positions,
+    int S, int r, int rep, const double* __restrict__ tab, const double* __restrict__ positions,
     const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
     const double* __restrict__ times, const double* __restrict__ radii, double tol,
     int max_iter, double* __restrict__ x_out, double* __restrict__ coeffs,
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   int* bad = reinterpret_cast<int*>(smem + L.ndouble);
   const int64_t b = blockIdx.x;
   constexpr int M = N / 2;
-  t.setup(tab, b, positions, fixed_vals, times_cp, times, radii, bad);
+  t.setup(tab, b, b / rep, positions, fixed_vals, times_cp, times, radii, bad);
   int st = 1;
   int it = 0;
   if (!(*bad & 1)) it = t.ipm(tol, max_iter, &st, bad);
@@ -127,7 +127,7 @@ hipError_t residuals_n(const TubeArgs& a, const double* x, double* resid, hipStr
   hipError_t e = prepare_lds(tube_residuals_kernel<N>, bytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tube_residuals_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(kWave),
-                     bytes, st, a.S, a.r, a.tab, a.positions, a.fixed_vals, a.times_cp,
+                     bytes, st, a.S, a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp,
                      a.times, a.radii, x, resid);
   return hipGetLastError();
 }
@@ -139,7 +139,7 @@ hipError_t solve_n(const TubeArgs& a, double tol, int max_iter, double* x, doubl
   hipError_t e = prepare_lds(tube_solve_kernel<N>, bytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tube_solve_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(kWave),
-                     bytes, st, a.S, a.r, a.tab, a.positions, a.fixed_vals, a.times_cp,
+                     bytes, st, a.S, a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp,
                      a.times, a.radii, tol, max_iter, x, coeffs, cost, iters, status);
   return hipGetLastError();
 }

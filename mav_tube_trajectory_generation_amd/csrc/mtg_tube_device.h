@@ -160,7 +160,10 @@ struct Tube {
 
   // ------------------------------------------------------------------ setup
   // Loads inputs, builds B_ul^-1 (zero-snapped), tube geometry, P and q.
-  __device__ void setup(const double* __restrict__ tab, int64_t b,
+  // Times are those of problem b; the geometry (positions, fixed values,
+  // control-point times, radii) that of trajectory bin (a trajectory's
+  // several evaluation points share it).
+  __device__ void setup(const double* __restrict__ tab, int64_t b, int64_t bin,
                         const double* __restrict__ positions,
                         const double* __restrict__ fixed_vals,
                         const double* __restrict__ times_cp,
@@ -169,18 +172,18 @@ struct Tube {
     const int NN = N * N;
     for (int i = lane; i < 2 * NN + M * M; i += kWave) sm[L->tabH + i] = tab[i];
     for (int i = lane; i < S; i += kWave) sm[L->T + i] = times[b * S + i];
-    for (int i = lane; i < (S + 1) * 3; i += kWave) sm[L->pos + i] = positions[b * (S + 1) * 3 + i];
+    for (int i = lane; i < (S + 1) * 3; i += kWave) sm[L->pos + i] = positions[bin * (S + 1) * 3 + i];
     for (int i = lane; i < 3 * N; i += kWave) {
       // fixed_vals[d][end*M + m] -> fixv[end][d][m]
       const int d = i / N, e = (i % N) / M, m = i % M;
-      sm[L->fixv + (e * 3 + d) * M + m] = fixed_vals[b * 3 * N + i];
+      sm[L->fixv + (e * 3 + d) * M + m] = fixed_vals[bin * 3 * N + i];
     }
     if (lane == 0) *bad = 0;
     __syncthreads();
     // B_ul^-1(T_cp) = C^-1 diag(T^l), snapped |x| < 1e-5 (qcqp_impl:299-307).
     for (int idx = lane; idx < S * M * M; idx += kWave) {
       const int i = idx / (M * M), k = (idx / M) % M, l = idx % M;
-      const double tc = times_cp[b * S + i];
+      const double tc = times_cp[bin * S + i];
       if (!(tc > 0.0)) atomicOr(bad, 1);
       double p = 1.0;
       for (int q = 0; q < l; ++q) p *= tc;
@@ -235,10 +238,10 @@ struct Tube {
         for (int k = 0; k < 3; ++k) s += bb[k] * A[k * 3 + c];
         G[12 + c] = 2.0 * s;  // L = 2 b^T A
       }
-      const double r1 = radii[(b * S + i) * 2 + 0];
-      const double r2 = radii[(b * S + i) * 2 + 1];
+      const double r1 = radii[(bin * S + i) * 2 + 0];
+      const double r2 = radii[(bin * S + i) * 2 + 1];
       G[15] = bb[0] * bb[0] + bb[1] * bb[1] + bb[2] * bb[2] - r1 * r1;  // mu
-      const double rs = (i == 0) ? radii[(b * S + 0) * 2 + 0] : radii[(b * S + i - 1) * 2 + 1];
+      const double rs = (i == 0) ? radii[(bin * S + 0) * 2 + 0] : radii[(bin * S + i - 1) * 2 + 1];
       double nps = 0.0, npe = 0.0;
       for (int k = 0; k < 3; ++k) {
         nps += n[k] * (p0[k] - n[k] * rs);
@@ -719,7 +722,8 @@ struct Tube {
   // optimum; *bad bit 2 set for a non-positive pivot of the start system.
   // Safeguard (same in the oracle): when the KKT factorisation or the step
   // breaks down, stop at the current iterate and accept it if every
-  // residual is within 1e3 * tol.
+  // residual is within 1e3 * tol (status 0); with the dual residual within
+  // 1e5 * tol instead, report it not converged (status 1).
   __device__ int ipm(double tol, int max_iter, int* status, int* bad) {
     int* fail = bad + 1;
     if (lane == 0) *fail = 0;
@@ -797,6 +801,10 @@ struct Tube {
         break;
       }
       const bool near = rdn <= 1e3 * tol * (1.0 + qn) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
+      // Stalled dual residual (lam / s ~ 1e12 on active constraints): not
+      // converged, value usable (same tiers in the oracle).
+      const bool stalled = rdn <= 1e5 * tol * (1.0 + qn) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
+      const int brk = near ? 0 : (stalled ? 1 : 2);
       MTG_TACC(200, tl);
       assemble_g();
       MTG_TACC(201, tl);
@@ -806,7 +814,7 @@ struct Tube {
       __syncthreads();
       MTG_TACC(202, tl);
       if (*fail) {
-        *status = near ? 0 : 2;
+        *status = brk;
         break;
       }
       // Affine (predictor) direction: rc = s * lam.
@@ -834,7 +842,7 @@ struct Tube {
       for (int idx = lane; idx < nv * BS; idx += kWave) dxn = fmax(dxn, fabs(sm[L->dx + idx]));
       dxn = wave_max(dxn);
       if (!(alpha > 0.0) || !(dxn < 1e300) || !(sigma < 1e300)) {
-        *status = near ? 0 : 2;
+        *status = brk;
         break;
       }
       for (int idx = lane; idx < nv * BS; idx += kWave) sm[L->x + idx] += alpha * sm[L->dx + idx];

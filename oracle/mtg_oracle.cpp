@@ -14,6 +14,7 @@
 #include <thread>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
 #include <random>
@@ -911,8 +912,14 @@ struct TubeProblem {
         break;
       }
       // Safeguard: on a breakdown of the KKT factorisation or step, stop at
-      // the current iterate and accept it if within 1e3 * tol.
+      // the current iterate and accept it if within 1e3 * tol (status 0), or
+      // report it as not converged (status 1, value usable) when it is
+      // primal feasible and complementary to 1e3 * tol with the dual
+      // residual within 1e5 * tol: with lam_k / s_k ~ 1e12 on the active
+      // constraints the dual residual stalls at the KKT solve's accuracy.
       const bool near = rdn <= 1e3 * tol * (1.0 + qnorm) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
+      const bool stalled = rdn <= 1e5 * tol * (1.0 + qnorm) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
+      const int brk = near ? 0 : (stalled ? 1 : 2);
       // K = P + sum lam_k Q_k + sum (lam_k/s_k) a_k a_k^T.
       Mat Kmat = P;
       for (int k = 0; k < m; ++k) {
@@ -925,7 +932,7 @@ struct TubeProblem {
                 lam[k] * c.quad[static_cast<size_t>(u) * ms + v] + w * a[k][u] * a[k][v];
       }
       if (!cholesky(&Kmat)) {
-        status = near ? 0 : 2;
+        status = brk;
         break;
       }
       auto direction = [&](const std::vector<double>& rc, std::vector<double>* dx,
@@ -972,7 +979,7 @@ struct TubeProblem {
       double dxn = 0.0;
       for (int i = 0; i < n; ++i) dxn = std::max(dxn, std::fabs(dx[i]));
       if (!(alpha > 0.0) || !(dxn < 1e300) || !(sigma < 1e300)) {
-        status = near ? 0 : 2;
+        status = brk;
         break;
       }
       for (int i = 0; i < n; ++i) x[i] += alpha * dx[i];
@@ -1813,6 +1820,120 @@ int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mas
   const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
   return timeOptimizeImpl(N, D, r, S, K, mask, vals, times_io, time_penalty, increment,
                           max_evals, &soft, cost, evals);
+}
+
+// objectiveFunctionTime in the fork's form (nonlinear_impl:877-945):
+// updateSegmentTimes + solveQCQP (:891-892) + computeCost + time penalty
+// [+ soft]; NaN where the QCQP setup or solve fails (mtg_tube_time_cost).
+static double tubeTimeObjective(int N, int D, int r, int S, int K, const uint8_t* mask,
+                                const double* vals, const double* times_cp,
+                                const double* radii, double tol, int max_iter,
+                                double time_penalty, const SoftSpec* soft,
+                                const std::vector<double>& t) {
+  std::vector<double> coeffs(static_cast<size_t>(S) * D * N);
+  double c = 0.0;
+  int it = 0;
+  const int rc = orc_tube_qcqp_solve(N, D, r, S, K, mask, vals, times_cp, t.data(), radii, tol,
+                                     max_iter, nullptr, coeffs.data(), &c, &it);
+  if (rc < 0) return std::numeric_limits<double>::quiet_NaN();
+  double total = 0.0;
+  for (double v : t) total += v;  // nonlinear_impl:2768-2774
+  double J = c + total * total * time_penalty;
+  if (soft && soft->n > 0) {
+    double sc = 0.0;
+    orc_soft_constraint_cost(N, D, S, coeffs.data(), t.data(), soft->n, soft->derivatives,
+                             soft->limits, soft->weight, soft->maximum_cost, nullptr, &sc);
+    J += sc;
+  }
+  return J;
+}
+
+// Central differences of the re-solved objective (grad_mode 2 and the
+// clamp rule of getCostAndGradientTime, nonlinear_impl:2525-2530).
+static void fdTimeGradient(int S, double increment, const std::vector<double>& t,
+                           const std::function<double(const std::vector<double>&)>& objective,
+                           double* g) {
+  for (int n = 0; n < S; ++n) {
+    std::vector<double> ts = t, tb = t;
+    ts[n] = ts[n] <= 0.1 ? 0.1 : ts[n] - increment;
+    tb[n] = tb[n] <= 0.1 ? 0.1 : tb[n] + increment;
+    const double Js = objective(ts);
+    const double Jb = objective(tb);
+    g[n] = (Jb - Js) / (2.0 * increment);
+  }
+}
+
+int orc_tube_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times_cp, const double* times,
+                       const double* radii, double tol, int max_iter, double time_penalty,
+                       int grad_mode, double increment, int n_soft,
+                       const int* soft_derivatives, const double* soft_limits,
+                       double soft_weight, double soft_maximum_cost, double* cost,
+                       double* grad) {
+  if (grad_mode != 0 && grad_mode != 2) return -1;
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  auto objective = [&](const std::vector<double>& t) {
+    return tubeTimeObjective(N, D, r, S, K, mask, vals, times_cp, radii, tol, max_iter,
+                             time_penalty, &soft, t);
+  };
+  const std::vector<double> t(times, times + S);
+  if (cost) *cost = objective(t);
+  if (grad_mode == 2 && grad) fdTimeGradient(S, increment, t, objective, grad);
+  return 0;
+}
+
+// mtg_tube_time_optimize's algorithm: timeOptimizeImpl's steps on the QCQP
+// objective, control-point maps at the initial times, stopping also at a
+// non-finite objective or gradient.
+int orc_tube_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, const double* radii, double* times_io,
+                           double tol, int max_iter, double time_penalty, double increment,
+                           int max_evals, int n_soft, const int* soft_derivatives,
+                           const double* soft_limits, double soft_weight,
+                           double soft_maximum_cost, double* cost, int* evals) {
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  const std::vector<double> T0(times_io, times_io + S);
+  auto objective = [&](const std::vector<double>& t) {
+    return tubeTimeObjective(N, D, r, S, K, mask, vals, T0.data(), radii, tol, max_iter,
+                             time_penalty, &soft, t);
+  };
+  std::vector<double> T = T0, g(S), trial(S);
+  double f = objective(T);
+  int n_eval = 1;
+  if (std::isfinite(f)) {
+    fdTimeGradient(S, increment, T, objective, g.data());
+    double alpha = 0.1;
+    while (n_eval < max_evals && alpha > 1e-9) {
+      double gmax = 0.0;
+      bool finite = true;
+      for (int n = 0; n < S; ++n) {
+        finite = finite && std::isfinite(g[n]);
+        gmax = std::max(gmax, std::fabs(g[n] * T0[n]));
+      }
+      if (!finite || !(gmax > 0.0)) break;
+      bool same = true;
+      for (int n = 0; n < S; ++n) {
+        const double x = T[n] - alpha * T0[n] * (g[n] * T0[n]) / gmax;
+        trial[n] = std::min(std::max(x, 0.1), 2.0 * T0[n]);
+        same = same && trial[n] == T[n];
+      }
+      if (same) break;
+      const double ft = objective(trial);
+      ++n_eval;
+      if (ft < f) {
+        T = trial;
+        f = ft;
+        alpha = std::min(alpha * 1.5, 1.0);
+        fdTimeGradient(S, increment, T, objective, g.data());
+      } else {
+        alpha *= 0.5;
+      }
+    }
+  }
+  std::memcpy(times_io, T.data(), sizeof(double) * S);
+  if (cost) *cost = f;
+  if (evals) *evals = n_eval;
+  return 0;
 }
 
 int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,

@@ -158,6 +158,23 @@ int orc_tube_qcqp_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
                         int max_iter, double* x_out, double* coeffs,
                         double* cost, int* iters);
 
+// objectiveFunctionTime with the QCQP inner solve (mtg_tube_time_cost):
+// grad_mode 0 or 2; NaN cost where the QCQP fails.
+int orc_tube_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times_cp, const double* times,
+                       const double* radii, double tol, int max_iter, double time_penalty,
+                       int grad_mode, double increment, int n_soft,
+                       const int* soft_derivatives, const double* soft_limits,
+                       double soft_weight, double soft_maximum_cost, double* cost,
+                       double* grad);
+// The mtg_tube_time_optimize algorithm on that objective.
+int orc_tube_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, const double* radii, double* times_io,
+                           double tol, int max_iter, double time_penalty, double increment,
+                           int max_evals, int n_soft, const int* soft_derivatives,
+                           const double* soft_limits, double soft_weight,
+                           double soft_maximum_cost, double* cost, int* evals);
+
 // CPU baseline timing (bench.py cpu_baseline leg): repeat setupFromVertices +
 // solveLinear + computeCost (the region polynomial_timing_evaluation.cpp:
 // 93-110 times) over B trajectories given in dense vertex form

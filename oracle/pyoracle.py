@@ -297,6 +297,55 @@ def tube_solve(N, r, vertices, times, radii, times_cp=None, tol=1e-10, max_iter=
     return dict(x=x, coeffs=coeffs, cost=float(cost[0]), iters=iters.value, status=rc)
 
 
+def tube_time_cost(N, r, vertices, times, radii, times_cp=None, tol=1e-10, max_iter=100,
+                   time_penalty=500.0, grad_mode=0, increment=0.1, soft=None,
+                   soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """orc_tube_time_cost: objectiveFunctionTime with the QCQP inner solve.
+    Returns (J, grad or None)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    times_cp = times if times_cp is None else np.ascontiguousarray(times_cp, dtype=np.float64)
+    radii = np.ascontiguousarray(radii, dtype=np.float64).reshape(S, 2)
+    cost = np.zeros(1)
+    grad = np.zeros(S)
+    ns, der, lim = _soft_arrays(soft)
+    L = lib()
+    L.orc_tube_time_cost.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+        ctypes.c_double, ctypes.c_int, _ip, _dp, ctypes.c_double, ctypes.c_double, _dp, _dp]
+    _check(L.orc_tube_time_cost(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                _d(vertices.vals), _d(times_cp), _d(times), _d(radii), tol,
+                                max_iter, time_penalty, grad_mode, increment, ns,
+                                der.ctypes.data_as(_ip), _d(lim), soft_weight, soft_maximum_cost,
+                                _d(cost), _d(grad)), "tube_time_cost")
+    return float(cost[0]), (grad if grad_mode == 2 else None)
+
+
+def tube_time_optimize(N, r, vertices, times, radii, max_evals, tol=1e-10, max_iter=100,
+                       time_penalty=500.0, increment=0.1, soft=None, soft_weight=100.0,
+                       soft_maximum_cost=1.0e12):
+    """orc_tube_time_optimize: the mtg_tube_time_optimize algorithm.
+    Returns (times, cost, evals)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    t = np.array(times, dtype=np.float64)
+    radii = np.ascontiguousarray(radii, dtype=np.float64).reshape(S, 2)
+    cost = np.zeros(1)
+    evals = ctypes.c_int()
+    ns, der, lim = _soft_arrays(soft)
+    L = lib()
+    L.orc_tube_time_optimize.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+        ctypes.c_int, ctypes.c_int, _ip, _dp, ctypes.c_double, ctypes.c_double, _dp,
+        ctypes.POINTER(ctypes.c_int)]
+    _check(L.orc_tube_time_optimize(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                    _d(vertices.vals), _d(radii), _d(t), tol, max_iter,
+                                    time_penalty, increment, max_evals, ns,
+                                    der.ctypes.data_as(_ip), _d(lim), soft_weight,
+                                    soft_maximum_cost, _d(cost), ctypes.byref(evals)),
+           "tube_time_optimize")
+    return t, float(cost[0]), evals.value
+
+
 def evaluate_range(N, coeffs, times, t_start, t_end, dt, derivative, max_out=None):
     """Trajectory::evaluateRange (trajectory.cpp:74-134) on coeffs [S, D, N]."""
     coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)

@@ -112,3 +112,33 @@ def test_ipm_matches_scipy(oracle, case):
     Jg = (np.einsum("kij,j->ki", Qk, x) + lk)[act]
     _, resid = nnls(Jg.T, -(P @ x + q))
     assert resid <= 1e-8 * max(1.0, np.linalg.norm(P @ x + q))
+
+
+def test_tube_time_objective_oracle(oracle):
+    """objectiveFunctionTime with the QCQP inner solve (nonlinear_impl:877-945,
+    solveQCQP at :892): J = computeCost of the QCQP solution + time_penalty
+    (sum T)^2; the gradient is the central difference of that J (clamp rule
+    :2525-2530); the optimiser only accepts decreases, stays in [0.1, 2 T0]
+    and counts its evaluations."""
+    S = 4
+    v = main_cpp_vertices(oracle)
+    t0 = oracle.estimate_segment_times(v, 2.0, 2.0)
+    radii = np.full((S, 2), 0.15)
+    t = t0 * 1.1
+    ref = oracle.tube_solve(N, R, v, t, radii, times_cp=t0)
+    J, g = oracle.tube_time_cost(N, R, v, t, radii, times_cp=t0, grad_mode=2)
+    assert J == pytest.approx(ref["cost"] + 500.0 * t.sum() ** 2, rel=1e-14)
+    h = 0.1
+    for n in range(S):
+        lo, hi = t.copy(), t.copy()
+        lo[n] -= h
+        hi[n] += h
+        Jl, _ = oracle.tube_time_cost(N, R, v, lo, radii, times_cp=t0)
+        Jh, _ = oracle.tube_time_cost(N, R, v, hi, radii, times_cp=t0)
+        assert g[n] == pytest.approx((Jh - Jl) / (2 * h), rel=1e-12)
+    J0, _ = oracle.tube_time_cost(N, R, v, t0, radii, times_cp=t0)
+    topt, Jopt, evals = oracle.tube_time_optimize(N, R, v, t0, radii, max_evals=12)
+    assert Jopt <= J0 and 1 <= evals <= 12
+    assert np.all(topt >= 0.1) and np.all(topt <= 2 * t0)
+    Jchk, _ = oracle.tube_time_cost(N, R, v, topt, radii, times_cp=t0)
+    assert Jchk == Jopt
