@@ -12,9 +12,10 @@
 //
 // Semantics and deliberate differences:
 //   * inner solve = the linear solve with the vertices' own constraint
-//     pattern (upstream mav_trajectory_generation semantics).  The fork calls
-//     solveQCQP inside the callback (nonlinear_impl:892); that mode is not
-//     provided yet — solveQCQP() is available on its own;
+//     pattern (upstream mav_trajectory_generation semantics) by default.
+//     With the build's extension field `solve_time_with_qcqp` the callback
+//     re-solves the tube QCQP instead, as the fork does (solveQCQP at
+//     nonlinear_impl:892; mtg_tube_time_cost / mtg_tube_time_optimize);
 //   * NLopt (LN_SBPLX, nonlinear_impl:95-107) is absent; the optimiser is the
 //     device-side projected descent of mtg_time_optimize with the same
 //     bounds [0.1, 2 T0] (:350-378), initial relative step 0.1 (the
@@ -87,6 +88,10 @@ struct NonlinearOptimizationParameters {
   VectorXd min_bound = VectorXd::Zero(3);
   VectorXd max_bound = VectorXd::Zero(3);
   bool use_numeric_grad = false;
+  // Build extension (not in the reference struct): kOptimizeTime's callback
+  // re-solves the tube QCQP (the fork, nonlinear_impl:892) instead of the
+  // linear problem.  Read.
+  bool solve_time_with_qcqp = false;
   bool use_continous_distance = false;
   double increment_time = 0.1;  // read (gradient step)
   double epsilon = 0.5;
@@ -181,6 +186,10 @@ class PolynomialOptimizationNonLinear {
                                                               << " entries, need " << S);
     MTG_CHECK(grad_mode == 0 || gradient != nullptr, "gradient must not be null");
     warnCollision();
+    if (params_.solve_time_with_qcqp) {
+      MTG_CHECK(grad_mode != 1, "grad_mode 1 holds d fixed: not defined for the QCQP callback");
+      return poly_opt_.evaluateTimeCostQCQP(segment_times, timeParams(grad_mode), gradient);
+    }
     internal::DeviceBuffer<double> d_df, d_t, d_cost(1), d_g(S);
     d_df.upload(packFixed());
     d_t.upload(segment_times);
@@ -221,6 +230,7 @@ class PolynomialOptimizationNonLinear {
               "objective not part of this build: kOptimizeTime and kOptimizeFreeConstraints "
               "(SURVEY.md 8a T1-T6, 8f rank 2)");
     warnCollision();
+    if (params_.solve_time_with_qcqp) return optimizeTimeQCQP();
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<double> times;
     linear_.getSegmentTimes(&times);
@@ -263,9 +273,10 @@ class PolynomialOptimizationNonLinear {
   }
 
   // The optimised trajectory: the linear problem's (kOptimizeTime) or the
-  // tube-pattern problem's (after kOptimizeFreeConstraints).
+  // tube-pattern problem's (after kOptimizeFreeConstraints, or kOptimizeTime
+  // with solve_time_with_qcqp).
   void getTrajectory(Trajectory* trajectory) const {
-    if (free_optimized_)
+    if (free_optimized_ || qcqp_time_optimized_)
       poly_opt_.getTrajectory(trajectory);
     else
       linear_.getTrajectory(trajectory);
@@ -294,6 +305,37 @@ class PolynomialOptimizationNonLinear {
   }
 
  private:
+  // optimizeTime in the fork's form: initial QCQP solve (nonlinear_impl:
+  // 341-349), device optimiser over the QCQP objective, final QCQP solve at
+  // the optimised times.
+  int optimizeTimeQCQP() {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> times = segmentTimesOfQcqp();
+    poly_opt_.solveQCQP();
+    poly_opt_.getTrajectory(&trajectory_initial_);
+    const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
+    double J = 0.0;
+    int32_t evals = 0;
+    const int st = poly_opt_.optimizeTimeQCQP(timeParams(2), budget, &times, &J, &evals);
+    poly_opt_.updateSegmentTimes(times);
+    poly_opt_.solveQCQP();
+    qcqp_time_optimized_ = true;
+    double tot = 0.0;
+    for (double t : times) tot += t;
+    optimization_info_.n_iterations = evals;
+    optimization_info_.cost_trajectory = poly_opt_.computeCost();
+    optimization_info_.cost_time = tot * tot * params_.time_penalty;
+    optimization_info_.cost_soft_constraints =
+        soft_.empty() ? 0.0
+                      : J - optimization_info_.cost_trajectory - optimization_info_.cost_time;
+    for (const auto& c : soft_)
+      optimization_info_.maxima[c.first] = poly_opt_.computeMaximumOfMagnitude(c.first, nullptr);
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
+    optimization_info_.optimization_time =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return optimization_info_.stopping_reason;
+  }
+
   std::vector<double> segmentTimesOfQcqp() const {
     std::vector<double> t;
     poly_opt_.getSegmentTimes(&t);
@@ -460,6 +502,7 @@ class PolynomialOptimizationNonLinear {
   OptimizationInfo optimization_info_;
   std::vector<std::pair<int, double>> soft_;  // (derivative, maximum_value)
   bool free_optimized_ = false;
+  bool qcqp_time_optimized_ = false;
 };
 
 }  // namespace mav_trajectory_generation

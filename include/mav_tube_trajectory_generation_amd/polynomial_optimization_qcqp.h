@@ -76,18 +76,8 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
   int solveQCQP(double tol = 1e-10, int max_iter = 100) {
     const int S = static_cast<int>(this->n_segments_);
     const int M = N / 2;
-    std::vector<double> pos((S + 1) * 3), df(3 * N), radii(S * 2);
-    for (int v = 0; v <= S; ++v) {
-      VectorXd p;
-      this->vertices_[v].getConstraint(derivative_order::POSITION, &p);
-      for (int d = 0; d < 3; ++d) pos[v * 3 + d] = p[d];
-    }
-    for (int d = 0; d < 3; ++d)
-      for (int j = 0; j < N; ++j) df[d * N + j] = this->fixed_constraints_compact_[d][j];
-    for (int s = 0; s < S; ++s) {
-      radii[2 * s] = segment_radii_[s].first;
-      radii[2 * s + 1] = segment_radii_[s].second;
-    }
+    std::vector<double> pos, df, radii;
+    packTubeInputs(&pos, &df, &radii);
     const size_t nx = static_cast<size_t>(3) * (S - 1) * M;
     internal::DeviceBuffer<double> d_pos, d_df, d_tcp, d_t, d_r, d_x(nx ? nx : 1),
         d_c(static_cast<size_t>(S) * 3 * N), d_cost(1);
@@ -126,18 +116,8 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
     const int S = static_cast<int>(this->n_segments_);
     const int n_con = mtg_tube_num_constraints(N, S);
     MTG_CHECK(n_con >= 0, "invalid tube size");
-    std::vector<double> pos((S + 1) * 3), df(3 * N), radii(S * 2), x;
-    for (int v = 0; v <= S; ++v) {
-      VectorXd p;
-      this->vertices_[v].getConstraint(derivative_order::POSITION, &p);
-      for (int d = 0; d < 3; ++d) pos[v * 3 + d] = p[d];
-    }
-    for (int d = 0; d < 3; ++d)
-      for (int j = 0; j < N; ++j) df[d * N + j] = this->fixed_constraints_compact_[d][j];
-    for (int s = 0; s < S; ++s) {
-      radii[2 * s] = segment_radii_[s].first;
-      radii[2 * s + 1] = segment_radii_[s].second;
-    }
+    std::vector<double> pos, df, radii, x;
+    packTubeInputs(&pos, &df, &radii);
     for (int d = 0; d < 3; ++d) {
       const VectorXd& v = this->free_constraints_compact_[d];
       MTG_CHECK(static_cast<size_t>(v.size()) == this->n_free_constraints_,
@@ -162,6 +142,70 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
     return res;
   }
 
+  // objectiveFunctionTime in the fork's form (nonlinear_impl:877-945, with
+  // solveQCQP at :892): J(T) = computeCost() of the QCQP at T + time_penalty
+  // (sum T)^2 [+ soft] (mtg_tube_time_cost; params.grad_mode 0 or 2).
+  // Control-point maps stay at the setup times.
+  double evaluateTimeCostQCQP(const std::vector<double>& segment_times,
+                              const mtg_time_params& params, std::vector<double>* gradient,
+                              int32_t* status = nullptr, double tol = 1e-10,
+                              int max_iter = 100) const {
+    const size_t S = this->n_segments_;
+    MTG_CHECK(segment_times.size() == S, "segment_times has " << segment_times.size()
+                                                              << " entries, need " << S);
+    MTG_CHECK(params.grad_mode == 0 || gradient != nullptr, "gradient must not be null");
+    std::vector<double> pos, df, radii;
+    packTubeInputs(&pos, &df, &radii);
+    internal::DeviceBuffer<double> d_pos, d_df, d_tcp, d_t, d_r, d_cost(1), d_g(S);
+    internal::DeviceBuffer<int32_t> d_st(1);
+    d_pos.upload(pos);
+    d_df.upload(df);
+    d_tcp.upload(times_cp_);
+    d_t.upload(segment_times);
+    d_r.upload(radii);
+    internal::checkStatus(
+        mtg_tube_time_cost(internal::defaultContext(), N, this->derivative_to_optimize_,
+                           static_cast<int>(S), 1, d_pos.get(), d_df.get(), d_tcp.get(),
+                           d_t.get(), d_r.get(), tol, max_iter, &params, d_cost.get(),
+                           params.grad_mode ? d_g.get() : nullptr, d_st.get(), nullptr),
+        "mtg_tube_time_cost");
+    internal::synchronize();
+    double J = 0.0;
+    d_cost.download(&J, 1);
+    if (params.grad_mode) *gradient = d_g.download();
+    if (status) d_st.download(status, 1);
+    return J;
+  }
+
+  // optimizeTime over that objective (mtg_tube_time_optimize): `times` in =
+  // the setup times (also the control-point times), out = optimised.
+  int optimizeTimeQCQP(const mtg_time_params& params, int max_evals, std::vector<double>* times,
+                       double* cost, int32_t* evals, double tol = 1e-10,
+                       int max_iter = 100) const {
+    MTG_CHECK(times != nullptr && times->size() == this->n_segments_, "times size");
+    std::vector<double> pos, df, radii;
+    packTubeInputs(&pos, &df, &radii);
+    internal::DeviceBuffer<double> d_pos, d_df, d_t, d_r, d_cost(1);
+    internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
+    d_pos.upload(pos);
+    d_df.upload(df);
+    d_t.upload(*times);
+    d_r.upload(radii);
+    internal::checkStatus(
+        mtg_tube_time_optimize(internal::defaultContext(), N, this->derivative_to_optimize_,
+                               static_cast<int>(this->n_segments_), 1, d_pos.get(), d_df.get(),
+                               d_r.get(), d_t.get(), tol, max_iter, &params, max_evals,
+                               d_cost.get(), d_ev.get(), d_st.get(), nullptr),
+        "mtg_tube_time_optimize");
+    internal::synchronize();
+    d_t.download(times->data(), times->size());
+    if (cost) d_cost.download(cost, 1);
+    if (evals) d_ev.download(evals, 1);
+    int32_t st = 0;
+    d_st.download(&st, 1);
+    return st;
+  }
+
   void getSegmentRadii(std::vector<std::pair<double, double>>* segment_radii) const {
     MTG_CHECK(segment_radii != nullptr, "segment_radii must not be null");
     *segment_radii = segment_radii_;
@@ -170,6 +214,27 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
   int getIterations() const { return iterations_; }
 
  private:
+  // Device layouts of mtg_tube_*: positions (S+1) x 3, fixed values 3 x N
+  // (start then end derivatives per dimension), radii S x 2.
+  void packTubeInputs(std::vector<double>* pos, std::vector<double>* df,
+                      std::vector<double>* radii) const {
+    const int S = static_cast<int>(this->n_segments_);
+    pos->assign(static_cast<size_t>(S + 1) * 3, 0.0);
+    df->assign(static_cast<size_t>(3) * N, 0.0);
+    radii->assign(static_cast<size_t>(S) * 2, 0.0);
+    for (int v = 0; v <= S; ++v) {
+      VectorXd p;
+      this->vertices_[v].getConstraint(derivative_order::POSITION, &p);
+      for (int d = 0; d < 3; ++d) (*pos)[v * 3 + d] = p[d];
+    }
+    for (int d = 0; d < 3; ++d)
+      for (int j = 0; j < N; ++j) (*df)[d * N + j] = this->fixed_constraints_compact_[d][j];
+    for (int s = 0; s < S; ++s) {
+      (*radii)[2 * s] = segment_radii_[s].first;
+      (*radii)[2 * s + 1] = segment_radii_[s].second;
+    }
+  }
+
   std::vector<std::pair<double, double>> segment_radii_;
   std::vector<double> times_cp_;
   int32_t iterations_ = 0;

@@ -556,6 +556,45 @@ TEST(gpu, OptimizeTimeLowersObjective) {
   checkPath(vs, segs, 10);
 }
 
+// The fork's callback form (solveQCQP inside objectiveFunctionTime,
+// nonlinear_impl:892): J and its central-difference gradient match the
+// oracle; the optimiser lowers J and ends with the QCQP trajectory.
+TEST(gpu, TimeCostWithQCQPInnerSolve) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> t0 = estimateSegmentTimes(vs, 2.0, 2.0);
+  const std::vector<std::pair<double, double>> radii(4, {0.15, 0.15});
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.weights.w_c = 0.0;
+  p.solve_time_with_qcqp = true;
+  p.max_iterations = 8;
+  PolynomialOptimizationNonLinear<10> opt(3, p);
+  opt.setupFromVertices(vs, t0, radii, 4);
+  const Dense d = toDense(vs, 5);
+  std::vector<double> t = t0, rad(8, 0.15);
+  for (double& v : t) v *= 1.05;
+  std::vector<double> g, og(4);
+  const double J = opt.evaluateTimeCost(t, 2, &g);
+  double oJ = 0.0;
+  EXPECT_TRUE(orc_tube_time_cost(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), t0.data(),
+                                 t.data(), rad.data(), 1e-10, 100, p.time_penalty, 2,
+                                 p.increment_time, 0, nullptr, nullptr, 100.0, 1e12, &oJ,
+                                 og.data()) == 0);
+  EXPECT_LE(std::fabs(J - oJ), 1e-5 * 30.0);  // 1e-6 of the QCQP cost (~26), penalty exact
+  for (int n = 0; n < 4; ++n) EXPECT_LE(std::fabs(g[n] - og[n]), 1e-5 * 30.0 / 0.1);
+  const double J0 = opt.evaluateTimeCost(t0);
+  EXPECT_TRUE(opt.optimize() > 0);
+  const OptimizationInfo info = opt.getOptimizationInfo();
+  EXPECT_TRUE(info.n_iterations >= 1 && info.n_iterations <= 8);
+  EXPECT_LE(info.cost_trajectory + info.cost_time, J0 * (1 + 1e-9));
+  Trajectory traj;
+  opt.getTrajectory(&traj);
+  Segment::Vector segs;
+  traj.getSegments(&segs);
+  EXPECT_TRUE(segs.size() == 4);
+  EXPECT_LE(std::fabs(segs.front().evaluate(0.0, 0)[0] - 2.7), 1e-9);
+}
+
 // Extrema test of the reference (test_polynomial_optimization.cpp:370-400):
 // the analytic maximum of |v| and |a| agrees with dense sampling within 0.01
 // (getMaximumMagnitude, test_utils.h) and with the oracle's
