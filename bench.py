@@ -39,7 +39,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
     p.add_argument("--segments", type=int, default=10)
-    p.add_argument("--workload", choices=["linear", "time", "tube", "sample", "extrema"], default="linear")
+    p.add_argument("--workload", choices=["linear", "time", "tube", "time-qcqp", "sample",
+                                          "extrema"], default="linear")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph)")
@@ -78,8 +79,10 @@ def cpu_baseline(wl, N, D, r, S, seconds, sample_args=None):
     """Oracle (reference-faithful C++ port, 1 thread) on a bounded sample of
     the same workload.  Returns (rate, units, description)."""
     import ctypes
-    seeds = range(105, 105 + (256 if wl in ("linear", "sample", "extrema") else 64))
-    pyoracle, masks, vals, times = _oracle_problems(N, D, S, seeds, tube=(wl == "tube"))
+    seeds = range(105, 105 + (256 if wl in ("linear", "sample", "extrema") else
+                              16 if wl == "time-qcqp" else 64))
+    pyoracle, masks, vals, times = _oracle_problems(N, D, S, seeds,
+                                                    tube=wl in ("tube", "time-qcqp"))
     K = N // 2
     B = len(seeds)
     if wl == "linear":
@@ -106,6 +109,12 @@ def cpu_baseline(wl, N, D, r, S, seconds, sample_args=None):
         units, sec = pyoracle.bench_workload(2, N, D, r, S, K, masks, vals, times, radii=radii,
                                              seconds=seconds)
         what = "tube QCQP solves (oracle primal-dual IPM, tol 1e-10)"
+    elif wl == "time-qcqp":
+        radii = np.full((B, S, 2), 0.15)
+        units, sec = pyoracle.bench_workload(5, N, D, r, S, K, masks, vals, times, radii=radii,
+                                             seconds=seconds)
+        what = ("time-objective evaluations with the QCQP inner solve and the central-"
+                "difference gradient (2S+1 oracle IPM solves each)")
     elif wl == "extrema":
         units, sec = pyoracle.bench_workload(4, N, D, r, S, K, masks, vals, times,
                                              seconds=seconds)
@@ -154,8 +163,8 @@ def main():
 
     N, D, r, S = 10, 3, 4, args.segments
     wl = args.workload
-    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "sample": 1024,
-                       "extrema": 1024}[wl]
+    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "time-qcqp": 1024,
+                       "sample": 1024, "extrema": 1024}[wl]
     from mav_tube_trajectory_generation_amd.shard import select_best, shard_range
     global_batch = B * world
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
@@ -232,7 +241,7 @@ def main():
         metric = "soft-constraint evaluations/sec (max |v|, |a| extremum search, 10-seg, N=10, 3D)"
         unit = "trajectories/s"
         units_per_step = B
-    else:
+    else:  # tube, time-qcqp
         radii = torch.full((B, S, 2), 0.15, dtype=torch.float64, device=dev)
         pos_d = torch.from_numpy(pos).to(dev)
         # Tube fixed values: start derivs 0..M-1 then end derivs, per dim.
@@ -242,11 +251,24 @@ def main():
         tf[:, :, M] = pos[:, S, :]
         tfix = torch.from_numpy(tf).to(dev)
 
-        def step():
-            return mtg.tube_solve(ctx, N, r, pos_d, tfix, times_d, times_d, radii)
+        if wl == "tube":
+            def step():
+                return mtg.tube_solve(ctx, N, r, pos_d, tfix, times_d, times_d, radii)
 
-        bytes_per_traj = ((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8 + (S * 3 * N + 1) * 8
-        metric = "tube QCQP solves/sec (4096 x 10-seg, N=10, 3D)"
+            bytes_per_traj = ((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8 + (S * 3 * N + 1) * 8
+            metric = "tube QCQP solves/sec (4096 x 10-seg, N=10, 3D)"
+        else:
+            # config 5's callback in the fork's form (solveQCQP inside
+            # objectiveFunctionTime, nonlinear_impl:892) with the central-
+            # difference gradient the optimiser uses: 2S+1 QCQPs per unit.
+            def step():
+                return mtg.tube_time_cost(ctx, N, r, pos_d, tfix, times_d, times_d, radii,
+                                          grad=True)
+
+            # inputs once + cost and gradient out (scratch traffic not counted)
+            bytes_per_traj = ((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8 + (S + 1) * 8 + 4
+            metric = ("time-objective evaluations/sec with the QCQP inner solve + FD gradient "
+                      "(1024 x 10-seg, N=10, 3D)")
         unit = "trajectories/s"
         units_per_step = B
 
@@ -255,7 +277,8 @@ def main():
     # per-launch duration is (end - start) / K from two HIP events on the
     # launch stream.  Otherwise (collective per step, or millisecond kernels)
     # eager launches with one event pair per launch.
-    use_graph = world == 1 and not args.no_graph
+    # (time-qcqp takes stream-ordered scratch inside the call: eager.)
+    use_graph = world == 1 and not args.no_graph and wl != "time-qcqp"
     if use_graph:
         graphs = {}
         for name, n in (("warmup", args.warmup), ("timed", args.steps)):

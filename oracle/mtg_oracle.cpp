@@ -1940,8 +1940,8 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                        const uint8_t* masks, const double* vals, const double* times,
                        const double* radii, int param_i, double param_d, int threads,
                        double min_seconds, int64_t* units, double* seconds) {
-  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 4) return -1;
-  if (kind == 2 && !radii) return -1;
+  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 5) return -1;
+  if ((kind == 2 || kind == 5) && !radii) return -1;
   if (kind == 3 && !(param_d > 0.0)) return -1;
   const size_t mstride = static_cast<size_t>(S + 1) * K;
   // kinds 3, 4: coefficients solved before the clock starts.
@@ -1986,6 +1986,17 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                                            nullptr, nullptr, &c, &itn);
         if (rc < 0 && rc != -22) failed = 1;
         acc += c;
+        ++n;
+      } else if (kind == 5) {
+        // objectiveFunctionTime with the QCQP inner solve and its
+        // central-difference gradient (2S + 1 QCQP solves).
+        double c = 0.0;
+        std::vector<double> g(S);
+        if (orc_tube_time_cost(N, D, r, S, K, mk, vl, tb, tb,
+                               radii + static_cast<size_t>(b) * S * 2, 1e-10, 100, 500.0, 2, 0.1,
+                               0, nullptr, nullptr, 100.0, 1.0e12, &c, g.data()))
+          failed = 1;
+        acc += std::isfinite(c) ? c : 0.0;
         ++n;
       } else if (kind == 4) {
         const int ders[2] = {1, 2};

@@ -218,9 +218,10 @@ int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mas
 // dt = param_d over the whole trajectory, on coefficients solved once before
 // the clock starts; kind 4: the soft-constraint cost of max |v| <= 3,
 // max |a| <= 5 (two computeMaximumOfMagnitude searches) on coefficients
-// solved before the clock starts.  *units = optimisations (1), solves (2),
-// samples (3, one sample = all derivatives of all dimensions at one time)
-// or trajectories (4).
+// solved before the clock starts; kind 5: orc_tube_time_cost with the
+// grad_mode 2 gradient (2S + 1 QCQP solves, times_cp = times).  *units =
+// optimisations (1), solves (2), samples (3, one sample = all derivatives of
+// all dimensions at one time), trajectories (4) or evaluations (5).
 int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                        const uint8_t* masks, const double* vals, const double* times,
                        const double* radii, int param_i, double param_d, int threads,
