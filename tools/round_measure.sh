@@ -8,6 +8,7 @@ timeout -k 10 300 python bench.py > gpurun_out/bench_linear.json 2> gpurun_out/b
 timeout -k 10 300 python bench.py --workload time --steps 20 --warmup 3 > gpurun_out/bench_time.json 2> gpurun_out/bench_time.err
 timeout -k 10 300 python bench.py --workload time --soft --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_time_soft.json 2> gpurun_out/bench_time_soft.err
 timeout -k 10 300 python bench.py --workload tube --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_tube.json 2> gpurun_out/bench_tube.err
+timeout -k 10 300 python bench.py --workload time-qcqp --steps 5 --warmup 1 > gpurun_out/bench_time_qcqp.json 2> gpurun_out/bench_time_qcqp.err
 bash tools/profile.sh linear
 bash tools/profile.sh time --workload time --steps 5 --warmup 1
 bash tools/profile.sh tube --workload tube --steps 5 --warmup 1
