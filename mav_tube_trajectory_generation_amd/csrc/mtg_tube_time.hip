@@ -178,16 +178,23 @@ __global__ void tube_time_opt_final_kernel(int S, int64_t B, OptState s,
 
 unsigned blocks_for(int64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
-// Stream-ordered scratch, released in the destructor (after the stream's
-// work: hipFreeAsync is ordered on the same stream).
+// Scratch for one call, released in the destructor after the stream's work.
+// Plain hipMalloc/hipFree, not the stream-ordered pool: the C++ shim's
+// hipMalloc'd buffers interleaved with hipMallocAsync/hipFreeAsync on the
+// null stream intermittently read a stale cost back (one run in three on
+// MI355X, tests/cpp TimeCostWithQCQPInnerSolve); the allocation is
+// microseconds against a QCQP launch of milliseconds.
 struct Scratch {
   hipStream_t st;
   void* p = nullptr;
   explicit Scratch(hipStream_t s) : st(s) {}
   ~Scratch() {
-    if (p) (void)hipFreeAsync(p, st);
+    if (p) {
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(p);
+    }
   }
-  hipError_t alloc(size_t bytes) { return hipMallocAsync(&p, bytes, st); }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes); }
 };
 
 // Points -> QCQP -> soft -> J for B trajectories x P rows.

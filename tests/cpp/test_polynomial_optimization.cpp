@@ -582,9 +582,23 @@ TEST(gpu, TimeCostWithQCQPInnerSolve) {
                                  og.data()) == 0);
   EXPECT_LE(std::fabs(J - oJ), 1e-5 * 30.0);  // 1e-6 of the QCQP cost (~26), penalty exact
   for (int n = 0; n < 4; ++n) EXPECT_LE(std::fabs(g[n] - og[n]), 1e-5 * 30.0 / 0.1);
+  // J at the control-point times themselves, against the oracle.
+  std::vector<double> g0;
   const double J0 = opt.evaluateTimeCost(t0);
+  const double J0g = opt.evaluateTimeCost(t0, 2, &g0);
+  double oJ0 = 0.0;
+  EXPECT_TRUE(orc_tube_time_cost(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), t0.data(),
+                                 t0.data(), rad.data(), 1e-10, 100, p.time_penalty, 0,
+                                 p.increment_time, 0, nullptr, nullptr, 100.0, 1e12, &oJ0,
+                                 nullptr) == 0);
+  std::fprintf(stderr, "J0 %.17g J0(grad) %.17g oracle %.17g J(1.05 T) %.17g oracle %.17g\n",
+               J0, J0g, oJ0, J, oJ);
+  EXPECT_LE(std::fabs(J0 - oJ0), 1e-5 * 30.0);
+  EXPECT_LE(std::fabs(J0g - oJ0), 1e-5 * 30.0);
   EXPECT_TRUE(opt.optimize() > 0);
   const OptimizationInfo info = opt.getOptimizationInfo();
+  std::fprintf(stderr, "after optimize: evals %d cost_trajectory %.17g cost_time %.17g\n",
+               static_cast<int>(info.n_iterations), info.cost_trajectory, info.cost_time);
   EXPECT_TRUE(info.n_iterations >= 1 && info.n_iterations <= 8);
   EXPECT_LE(info.cost_trajectory + info.cost_time, J0 * (1 + 1e-9));
   Trajectory traj;
