@@ -92,6 +92,23 @@ def test_tube_time_cost_main_cpp(ctx, dev, oracle):
     assert abs(J - (ref["cost"] + 500.0 * t.sum() ** 2)) <= 1e-6 * ref["cost"]
 
 
+def test_tube_time_cost_repeated_calls(ctx, dev, oracle):
+    """Back-to-back calls alternating grad on/off, each with fresh output
+    buffers, return the same J every time.  Regression for a stale cost read
+    when the call's scratch came from the stream-ordered pool (the C++
+    shim's TimeCostWithQCQPInnerSolve failed one run in three)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    v = main_cpp_vertices(oracle)
+    t = oracle.estimate_segment_times(v, 2.0, 2.0)
+    pos, fv, radii = _geometry(dev, [(v, t)])
+    Jr, _ = oracle.tube_time_cost(N, R, v, t, np.full((4, 2), 0.15))
+    for i in range(24):
+        out = mtg.tube_time_cost(ctx, N, R, pos, fv, _T(dev, t[None]), _T(dev, t[None]), radii,
+                                 grad=bool(i & 1))
+        J = float(out["cost"][0])
+        assert abs(J - Jr) <= 1e-6 * abs(Jr), (i, J, Jr)
+
+
 def test_tube_time_optimize_vs_oracle(ctx, dev, oracle):
     """Same steps as the oracle's driver: accepted points, evaluation counts
     and the final J, with one divergent path allowed (accept/reject compares
