@@ -158,6 +158,8 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
     packTubeInputs(&pos, &df, &radii);
     internal::DeviceBuffer<double> d_pos, d_df, d_tcp, d_t, d_r, d_cost(1), d_g(S);
     internal::DeviceBuffer<int32_t> d_st(1);
+    internal::DeviceBuffer<unsigned char> d_ws(
+        workspaceBytes(static_cast<int>(S), params, 0));
     d_pos.upload(pos);
     d_df.upload(df);
     d_tcp.upload(times_cp_);
@@ -167,7 +169,8 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
         mtg_tube_time_cost(internal::defaultContext(), N, this->derivative_to_optimize_,
                            static_cast<int>(S), 1, d_pos.get(), d_df.get(), d_tcp.get(),
                            d_t.get(), d_r.get(), tol, max_iter, &params, d_cost.get(),
-                           params.grad_mode ? d_g.get() : nullptr, d_st.get(), nullptr),
+                           params.grad_mode ? d_g.get() : nullptr, d_st.get(), d_ws.get(),
+                           d_ws.size(), nullptr),
         "mtg_tube_time_cost");
     internal::synchronize();
     double J = 0.0;
@@ -187,6 +190,8 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
     packTubeInputs(&pos, &df, &radii);
     internal::DeviceBuffer<double> d_pos, d_df, d_t, d_r, d_cost(1);
     internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
+    internal::DeviceBuffer<unsigned char> d_ws(
+        workspaceBytes(static_cast<int>(this->n_segments_), params, 1));
     d_pos.upload(pos);
     d_df.upload(df);
     d_t.upload(*times);
@@ -195,7 +200,8 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
         mtg_tube_time_optimize(internal::defaultContext(), N, this->derivative_to_optimize_,
                                static_cast<int>(this->n_segments_), 1, d_pos.get(), d_df.get(),
                                d_r.get(), d_t.get(), tol, max_iter, &params, max_evals,
-                               d_cost.get(), d_ev.get(), d_st.get(), nullptr),
+                               d_cost.get(), d_ev.get(), d_st.get(), d_ws.get(), d_ws.size(),
+                               nullptr),
         "mtg_tube_time_optimize");
     internal::synchronize();
     d_t.download(times->data(), times->size());
@@ -214,6 +220,12 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
   int getIterations() const { return iterations_; }
 
  private:
+  static size_t workspaceBytes(int S, const mtg_time_params& params, int optimize) {
+    const int64_t n = mtg_tube_time_workspace_bytes(N, S, 1, &params, optimize);
+    internal::checkStatus(n < 0 ? static_cast<int>(n) : MTG_OK, "mtg_tube_time_workspace_bytes");
+    return static_cast<size_t>(n);
+  }
+
   // Device layouts of mtg_tube_*: positions (S+1) x 3, fixed values 3 x N
   // (start then end derivatives per dimension), radii S x 2.
   void packTubeInputs(std::vector<double>* pos, std::vector<double>* df,

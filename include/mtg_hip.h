@@ -273,7 +273,10 @@ int mtg_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
  * primal-dual interior-point method (MOSEK in the reference), then recover
  * coefficients (qcqp_impl:777-785).  Outputs: x B x 3(S-1)M, coeffs
  * B x S x 3 x N, cost B (computeCost), iters B, status B (nullable except
- * coeffs).
+ * coeffs).  Where a time is not positive (MTG_TRAJ_BAD_TIME) or the start
+ * system is not positive definite (MTG_TRAJ_NOT_SPD with 0 iterations), x,
+ * coeffs and cost are NaN.  B < 2^26 (one 64-lane workgroup per
+ * trajectory).
  */
 int mtg_tube_num_constraints(int N, int S);
 int mtg_tube_residuals(mtg_ctx* ctx, int N, int r, int S, int64_t B,
@@ -300,13 +303,22 @@ int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B,
  * extra QCQP solves per trajectory, all in the same launch); grad_mode 1 is
  * MTG_ERR_UNSUPPORTED.  tol / max_iter as mtg_tube_solve.  Outputs
  * (device): cost B, grad B x S (grad_mode 2), status B (nullable; the
- * QCQP status at `times`).  Device scratch is taken stream-ordered
- * (hipMallocAsync) for the duration of the call. */
+ * QCQP status at `times`).
+ *
+ * Scratch: `workspace` is a caller-owned device buffer of at least
+ * mtg_tube_time_workspace_bytes(N, S, B, params, 0) bytes (optimize = 1
+ * for mtg_tube_time_optimize), used for the duration of the stream's work.
+ * Neither call allocates or synchronises, so both can be captured in a HIP
+ * graph.  The query returns < 0 (MTG_ERR_INVALID_ARG) for invalid sizes or
+ * when B x (2S+1) problems would exceed one launch's grid (2^26 problems). */
+int64_t mtg_tube_time_workspace_bytes(int N, int S, int64_t B,
+                                      const mtg_time_params* params, int optimize);
 int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                        const double* positions, const double* fixed_vals,
                        const double* times_cp, const double* times, const double* radii,
                        double tol, int max_iter, const mtg_time_params* params,
-                       double* cost, double* grad, int32_t* status, void* stream);
+                       double* cost, double* grad, int32_t* status,
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* Batched segment-time optimisation over that objective (optimizeTime,
  * nonlinear_impl:332-397, in the fork's QCQP form): the optimiser of
@@ -314,15 +326,17 @@ int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B,
  * backtrack on the grad_mode 2 gradient, bounds [0.1, 2 T0], max_evals
  * counted evaluations), stopping also at a non-finite gradient.  Each round
  * is one tube launch over B x (2S+1) problems (every trial with its gradient
- * points); the host waits for each round to know whether any trajectory is
- * still active, so this call synchronises the stream.
+ * points).  The call enqueues max_evals rounds; a trajectory that has
+ * stopped is skipped by every later round on the device (its QCQP
+ * workgroups exit at once), so there is no host round trip.
  *   times_io  B x S  in: T0 (also the control-point times), out: optimised
- *   cost B, evals B, status B (nullable). */
+ *   cost B, evals B, status B (nullable); workspace as above (optimize = 1). */
 int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                            const double* positions, const double* fixed_vals,
                            const double* radii, double* times_io, double tol, int max_iter,
                            const mtg_time_params* params, int max_evals, double* cost,
-                           int32_t* evals, int32_t* status, void* stream);
+                           int32_t* evals, int32_t* status, void* workspace,
+                           size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Batched trajectory sampling: Trajectory::evaluateRange (src/trajectory.cpp:

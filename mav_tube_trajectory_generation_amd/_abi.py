@@ -83,15 +83,20 @@ SIGNATURES = {
     "mtg_tube_solve": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_double,
                                       ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mtg_tube_time_workspace_bytes": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int,
+                                                       ctypes.c_int64,
+                                                       ctypes.POINTER(TimeParams),
+                                                       ctypes.c_int]),
     "mtg_tube_time_cost": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int64, _vp, _vp, _vp, _vp, _vp,
                                           ctypes.c_double, ctypes.c_int,
-                                          ctypes.POINTER(TimeParams), _vp, _vp, _vp, _vp]),
+                                          ctypes.POINTER(TimeParams), _vp, _vp, _vp, _vp,
+                                          ctypes.c_size_t, _vp]),
     "mtg_tube_time_optimize": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int64, _vp, _vp, _vp, _vp,
                                               ctypes.c_double, ctypes.c_int,
                                               ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
-                                              _vp, _vp, _vp]),
+                                              _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "mtg_sample_trajectories": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int64, _vp, _vp, ctypes.c_double,
                                                ctypes.c_double, ctypes.c_double, ctypes.c_int,

@@ -323,12 +323,33 @@ def _tube_geometry(N, positions, fixed_vals, radii, B, S):
         _require(t, shp, name)
 
 
+def tube_time_workspace_bytes(N, S, B, params, optimize):
+    """Device scratch the QCQP time objective / optimiser needs
+    (mtg_tube_time_workspace_bytes)."""
+    n = lib().mtg_tube_time_workspace_bytes(N, S, B, ctypes.byref(params), 1 if optimize else 0)
+    if n < 0:
+        check(int(n), "mtg_tube_time_workspace_bytes")
+    return int(n)
+
+
+def _workspace(workspace, nbytes, dev):
+    import torch
+    if workspace is None:
+        return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    if not isinstance(workspace, torch.Tensor) or not workspace.is_cuda or \
+            not workspace.is_contiguous() or workspace.numel() * workspace.element_size() < nbytes:
+        raise MTGError(f"workspace must be a contiguous CUDA tensor of >= {nbytes} bytes")
+    return workspace
+
+
 def tube_time_cost(ctx, N, r, positions, fixed_vals, times_cp, times, radii, time_penalty=500.0,
                    grad=False, increment=0.1, soft=None, soft_weight=100.0, tol=1e-10,
-                   max_iter=100):
+                   max_iter=100, workspace=None):
     """objectiveFunctionTime with the QCQP inner solve (mtg_tube_time_cost):
     J = computeCost() of the tube QCQP at `times` + time_penalty (sum T)^2
     [+ soft]; grad=True adds the central-difference gradient (grad_mode 2).
+    workspace: optional device tensor of >= tube_time_workspace_bytes bytes
+    (allocated from torch's caching allocator when None).
     Returns dict(cost [B], grad [B, S] or None, status [B])."""
     import torch
     B, S = times.shape
@@ -340,16 +361,19 @@ def tube_time_cost(ctx, N, r, positions, fixed_vals, times_cp, times, radii, tim
     cost = torch.empty(B, dtype=torch.float64, device=dev)
     g = torch.empty((B, S), dtype=torch.float64, device=dev) if grad else None
     status = torch.empty(B, dtype=torch.int32, device=dev)
+    nbytes = tube_time_workspace_bytes(N, S, B, p, False)
+    ws = _workspace(workspace, nbytes, dev)
     check(lib().mtg_tube_time_cost(ctx.handle, N, r, S, B, _ptr(positions), _ptr(fixed_vals),
                                    _ptr(times_cp), _ptr(times), _ptr(radii), tol, max_iter,
-                                   ctypes.byref(p), _ptr(cost), _ptr(g), _ptr(status),
-                                   _stream(dev)), "mtg_tube_time_cost")
+                                   ctypes.byref(p), _ptr(cost), _ptr(g), _ptr(status), _ptr(ws),
+                                   ws.numel() * ws.element_size(), _stream(dev)),
+          "mtg_tube_time_cost")
     return dict(cost=cost, grad=g, status=status)
 
 
 def tube_time_optimize(ctx, N, r, positions, fixed_vals, radii, times, max_evals,
                        time_penalty=500.0, increment=0.1, soft=None, soft_weight=100.0,
-                       tol=1e-10, max_iter=100):
+                       tol=1e-10, max_iter=100, workspace=None):
     """optimizeTime in the fork's QCQP form (mtg_tube_time_optimize).  times
     [B, S] are the initial times (and the control-point times); returns
     dict(times, cost, evals, status) with new tensors."""
@@ -363,10 +387,13 @@ def tube_time_optimize(ctx, N, r, positions, fixed_vals, radii, times, max_evals
     cost = torch.empty(B, dtype=torch.float64, device=dev)
     evals = torch.empty(B, dtype=torch.int32, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
+    nbytes = tube_time_workspace_bytes(N, S, B, p, True)
+    ws = _workspace(workspace, nbytes, dev)
     check(lib().mtg_tube_time_optimize(ctx.handle, N, r, S, B, _ptr(positions),
                                        _ptr(fixed_vals), _ptr(radii), _ptr(t), tol, max_iter,
                                        ctypes.byref(p), max_evals, _ptr(cost), _ptr(evals),
-                                       _ptr(status), _stream(dev)), "mtg_tube_time_optimize")
+                                       _ptr(status), _ptr(ws), ws.numel() * ws.element_size(),
+                                       _stream(dev)), "mtg_tube_time_optimize")
     return dict(times=t, cost=cost, evals=evals, status=status)
 
 

@@ -504,10 +504,18 @@ int mtg_tube_num_constraints(int N, int S) {
   return (S - 1) + S * (N - 2) + 2 * S * (N - 2);
 }
 
+// One 64-lane workgroup per QCQP problem: the launch must stay below 2^32
+// work-items (and 2^32 workgroups), and the B x P x S point arrays below
+// 2^31 entries.
+static bool tube_grid_ok(int S, int64_t problems) {
+  return problems >= 0 && problems < (int64_t(1) << 26) &&
+         problems * static_cast<int64_t>(S) < (int64_t(1) << 31);
+}
+
 static int tube_args(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* positions,
                      const double* fixed_vals, const double* times_cp, const double* times,
                      const double* radii, mtg::TubeArgs* a) {
-  if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || S < 2 || B < 0 || B > 0x7fffffff)
+  if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || S < 2 || !tube_grid_ok(S, B))
     return MTG_ERR_INVALID_ARG;
   if (B && (!positions || !fixed_vals || !times_cp || !times || !radii))
     return MTG_ERR_INVALID_ARG;
@@ -556,11 +564,21 @@ static bool valid_tube_time_params(int N, int S, const mtg_time_params* p) {
   return p->increment > 0.0;
 }
 
+int64_t mtg_tube_time_workspace_bytes(int N, int S, int64_t B, const mtg_time_params* params,
+                                      int optimize) {
+  if (!valid_N(N) || S < 2 || B < 0 || !valid_tube_time_params(N, S, params))
+    return MTG_ERR_INVALID_ARG;
+  if (!tube_grid_ok(S, mtg::tube_time_problems(S, B, *params, optimize != 0)))
+    return MTG_ERR_INVALID_ARG;
+  return static_cast<int64_t>(mtg::tube_time_workspace_bytes(N, S, B, *params, optimize != 0));
+}
+
 int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* positions,
                        const double* fixed_vals, const double* times_cp, const double* times,
                        const double* radii, double tol, int max_iter,
                        const mtg_time_params* params, double* cost, double* grad,
-                       int32_t* status, void* stream) {
+                       int32_t* status, void* workspace, size_t workspace_bytes,
+                       void* stream) {
   mtg::TubeArgs a;
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_cp, times, radii, &a);
   if (rc) return rc;
@@ -570,25 +588,32 @@ int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B, const doubl
   if (params->grad_mode != 0 && params->grad_mode != 2) return MTG_ERR_INVALID_ARG;
   if (params->grad_mode == 2 && B && !grad) return MTG_ERR_INVALID_ARG;
   if (B && !cost) return MTG_ERR_INVALID_ARG;
+  if (!tube_grid_ok(S, mtg::tube_time_problems(S, B, *params, false)))
+    return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
-  return mtg::tube_time_cost(a, tol, max_iter, *params, cost, grad, status,
-                             static_cast<hipStream_t>(stream));
+  if (!workspace) return MTG_ERR_INVALID_ARG;
+  return mtg::tube_time_cost(a, tol, max_iter, *params, cost, grad, status, workspace,
+                             workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
 int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                            const double* positions, const double* fixed_vals,
                            const double* radii, double* times_io, double tol, int max_iter,
                            const mtg_time_params* params, int max_evals, double* cost,
-                           int32_t* evals, int32_t* status, void* stream) {
+                           int32_t* evals, int32_t* status, void* workspace,
+                           size_t workspace_bytes, void* stream) {
   mtg::TubeArgs a;
   // times_cp = the initial times (read before the first write of times_io).
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_io, times_io, radii, &a);
   if (rc) return rc;
   if (!valid_tube_time_params(N, S, params) || !(tol > 0) || max_iter < 1 || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
+  if (!tube_grid_ok(S, mtg::tube_time_problems(S, B, *params, true))) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
+  if (!workspace) return MTG_ERR_INVALID_ARG;
   return mtg::tube_time_optimize(a, times_io, tol, max_iter, *params, max_evals, cost, evals,
-                                 status, static_cast<hipStream_t>(stream));
+                                 status, workspace, workspace_bytes,
+                                 static_cast<hipStream_t>(stream));
 }
 
 int mtg_generate_random_problems(int N, int D, int S, int64_t B, uint64_t seed0,

@@ -90,6 +90,9 @@ struct TubeArgs {
   // geometry (positions, fixed values, times_cp, radii) from row b / rep
   // (the evaluation points of mtg_tube_time_cost / _optimize).
   int rep = 1;
+  // Optional per-trajectory skip flags (indexed by problem / rep): a set flag
+  // makes the problem's QCQP workgroup return without touching its outputs.
+  const int32_t* skip = nullptr;
 };
 hipError_t launch_tube_residuals(const TubeArgs& a, const double* x, double* resid,
                                  hipStream_t st);
@@ -99,11 +102,18 @@ hipError_t launch_tube_solve(const TubeArgs& a, double tol, int max_iter, double
 size_t tube_lds_bytes(int N, int S);
 // Segment-time objective / optimiser with the QCQP inner solve
 // (mtg_tube_time.hip); return MTG_* codes.
+// All scratch comes from the caller's workspace (tube_time_workspace_bytes).
+size_t tube_time_workspace_bytes(int N, int S, int64_t B, const mtg_time_params& p,
+                                 bool optimiser);
+// QCQP problems of one launch (B x evaluation points).
+int64_t tube_time_problems(int S, int64_t B, const mtg_time_params& p, bool optimiser);
 int tube_time_cost(const TubeArgs& a, double tol, int max_iter, const mtg_time_params& p,
-                   double* cost, double* grad, int32_t* status, hipStream_t st);
+                   double* cost, double* grad, int32_t* status, void* workspace,
+                   size_t workspace_bytes, hipStream_t st);
 int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_iter,
                        const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
-                       int32_t* status, hipStream_t st);
+                       int32_t* status, void* workspace, size_t workspace_bytes,
+                       hipStream_t st);
 
 constexpr int kMaxLdsBytes = 160 * 1024;
 

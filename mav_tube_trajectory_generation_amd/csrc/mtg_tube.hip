@@ -49,27 +49,32 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
     int S, int r, int rep, const double* __restrict__ tab, const double* __restrict__ positions,
     const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
     const double* __restrict__ times, const double* __restrict__ radii, double tol,
-    int max_iter, double* __restrict__ x_out, double* __restrict__ coeffs,
-    double* __restrict__ cost, int32_t* __restrict__ iters, int32_t* __restrict__ status) {
+    int max_iter, const int32_t* __restrict__ skip, double* __restrict__ x_out,
+    double* __restrict__ coeffs, double* __restrict__ cost, int32_t* __restrict__ iters,
+    int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int64_t b = blockIdx.x;
+  if (skip && skip[b / rep]) return;  // workgroup-uniform
   const TubeLayout L = make_tube_layout(N, S);
   Tube<N> t = make_tube<N>(&L, smem, S, r);
   int* bad = reinterpret_cast<int*>(smem + L.ndouble);
-  const int64_t b = blockIdx.x;
   constexpr int M = N / 2;
   t.setup(tab, b, b / rep, positions, fixed_vals, times_cp, times, radii, bad);
   int st = 1;
   int it = 0;
   if (!(*bad & 1)) it = t.ipm(tol, max_iter, &st, bad);
   __syncthreads();
+  // Bit 0: a time is not positive; bit 1: the start system is not positive
+  // definite, so x was never written.  Either way the outputs are NaN.
   const int fl = *bad;
+  const bool no_x = (fl & 3) != 0;
   // Outputs: x (reference order), coefficients (qcqp_impl:777-785 ->
   // linear_impl:254-275) and computeCost (linear_impl:113-130).
   const int n = t.nv * 3 * M;
   if (x_out)
     for (int idx = t.lane; idx < n; idx += kWave) {
       const int d = idx / ((S - 1) * M), a = (idx / M) % (S - 1), m = idx % M;
-      x_out[b * n + idx] = smem[L.x + (a * 3 + d) * M + m];
+      x_out[b * n + idx] = no_x ? NAN : smem[L.x + (a * 3 + d) * M + m];
     }
   const double* xv = smem + L.x;
   double acc = 0.0;
@@ -85,12 +90,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
       c += smem[L.tabA + k * N + j] * t.pwr(s, l - k) * e;
       h += smem[L.tabH + k * N + j] * t.pwr(s, 1 - 2 * r + lk + l) * e;
     }
-    coeffs[b * per + i] = (fl & 1) ? NAN : c;
+    coeffs[b * per + i] = no_x ? NAN : c;
     acc += h * t.xval(xv, s + k / M, d, lk);
   }
   const double J = 0.5 * Tube<N>::wave_sum(acc);
   if (t.lane == 0) {
-    if (cost) cost[b] = (fl & 1) ? NAN : J;
+    if (cost) cost[b] = no_x ? NAN : J;
     if (iters) iters[b] = it;
     if (status)
       status[b] = (fl & 1) ? MTG_TRAJ_BAD_TIME
@@ -140,7 +145,7 @@ hipError_t solve_n(const TubeArgs& a, double tol, int max_iter, double* x, doubl
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tube_solve_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(kWave),
                      bytes, st, a.S, a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp,
-                     a.times, a.radii, tol, max_iter, x, coeffs, cost, iters, status);
+                     a.times, a.radii, tol, max_iter, a.skip, x, coeffs, cost, iters, status);
   return hipGetLastError();
 }
 }  // namespace

@@ -11,9 +11,11 @@
 // geometry (TubeArgs::rep).  Small kernels around the launch build the
 // points, form J from the QCQP cost, and (optimiser) advance a per-trajectory
 // state machine.  The optimiser evaluates the gradient points of every trial
-// together with the trial itself, so one round = one counted evaluation and
-// the host loop runs at most max_evals rounds (ending early when no
-// trajectory is active).
+// together with the trial itself, so one round = one counted evaluation; the
+// call enqueues max_evals rounds and a finished trajectory is skipped by
+// every later kernel (no host round trip).  All scratch is the caller's
+// workspace (mtg_tube_time_workspace_bytes): the call never allocates or
+// synchronises.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -47,11 +49,12 @@ __global__ void tube_time_finish_kernel(int S, int64_t B, int P, const double* _
                                         const double* __restrict__ qcost,
                                         const int32_t* __restrict__ qstatus,
                                         const double* __restrict__ soft, double time_penalty,
-                                        double h, double* __restrict__ Jall,
+                                        double h, const int32_t* __restrict__ skip,
+                                        double* __restrict__ Jall,
                                         double* __restrict__ cost, double* __restrict__ grad,
                                         int32_t* __restrict__ status) {
   const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  if (b >= B || (skip && skip[b])) return;
   double J0 = 0.0, Jprev = 0.0;
   for (int j = 0; j < P; ++j) {
     const int64_t q = b * P + j;
@@ -104,8 +107,7 @@ __global__ void tube_time_opt_init_kernel(int S, int64_t B, const double* __rest
 // next trial (or finish).
 __global__ void tube_time_opt_step_kernel(int S, int64_t B, int P, int first, int max_evals,
                                           double h, const double* __restrict__ Jall,
-                                          const int32_t* __restrict__ qstatus, OptState s,
-                                          int32_t* __restrict__ n_active) {
+                                          const int32_t* __restrict__ qstatus, OptState s) {
   const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= B || s.done[b]) return;
   const double* J = Jall + b * P;
@@ -155,11 +157,7 @@ __global__ void tube_time_opt_step_kernel(int S, int64_t B, int P, int first, in
     }
     stop = same;
   }
-  if (stop) {
-    s.done[b] = 1;
-  } else {
-    atomicAdd(n_active, 1);
-  }
+  if (stop) s.done[b] = 1;
 }
 
 __global__ void tube_time_opt_final_kernel(int S, int64_t B, OptState s,
@@ -178,127 +176,136 @@ __global__ void tube_time_opt_final_kernel(int S, int64_t B, OptState s,
 
 unsigned blocks_for(int64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
-// Scratch for one call, released in the destructor after the stream's work.
-// Plain hipMalloc/hipFree, not the stream-ordered pool: the C++ shim's
-// hipMalloc'd buffers interleaved with hipMallocAsync/hipFreeAsync on the
-// null stream intermittently read a stale cost back (one run in three on
-// MI355X, tests/cpp TimeCostWithQCQPInnerSolve); the allocation is
-// microseconds against a QCQP launch of milliseconds.
-struct Scratch {
-  hipStream_t st;
-  void* p = nullptr;
-  explicit Scratch(hipStream_t s) : st(s) {}
-  ~Scratch() {
-    if (p) {
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(p);
-    }
-  }
-  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes); }
+// Caller-owned workspace (mtg_tube_time_workspace_bytes), carved in a fixed
+// order; each array starts on a 256-byte boundary.  With base == nullptr only
+// the size is computed.
+struct Workspace {
+  double *coeffs, *pts, *qcost, *softc, *Jall, *maxima;
+  int32_t* qstatus;
+  OptState s;  // optimiser only
 };
+struct Carver {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(int64_t n) {
+    off = (off + 255) & ~size_t(255);
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += sizeof(T) * static_cast<size_t>(n);
+    return p;
+  }
+};
+size_t carve(void* base, int N, int S, int64_t B, int P, int n_soft, bool optimiser,
+             Workspace* w) {
+  Carver c{static_cast<char*>(base)};
+  const int64_t BP = B * P;
+  w->coeffs = c.take<double>(BP * S * 3 * N);
+  w->pts = c.take<double>(BP * S);
+  w->qcost = c.take<double>(BP);
+  w->softc = c.take<double>(BP);
+  w->Jall = c.take<double>(BP);
+  w->maxima = c.take<double>(BP * (n_soft > 0 ? n_soft : 1));
+  w->qstatus = c.take<int32_t>(BP);
+  w->s = OptState{};
+  if (optimiser) {
+    w->s.T0 = c.take<double>(B * S);
+    w->s.Tc = c.take<double>(B * S);
+    w->s.g = c.take<double>(B * S);
+    w->s.Ttr = c.take<double>(B * S);
+    w->s.f = c.take<double>(B);
+    w->s.alpha = c.take<double>(B);
+    w->s.evals = c.take<int32_t>(B);
+    w->s.done = c.take<int32_t>(B);
+    w->s.st = c.take<int32_t>(B);
+  }
+  return c.off;
+}
 
-// Points -> QCQP -> soft -> J for B trajectories x P rows.
+// Points -> QCQP -> soft -> J for B trajectories x P rows.  Every array the
+// finish kernel reads (pts, qcost, qstatus, softc) is written earlier in the
+// same stream for every row: points by tube_time_points_kernel, qcost and
+// qstatus by every workgroup of tube_solve_kernel (also where a trajectory
+// fails), softc by the last extremum launch.  With `skip`, trajectories whose
+// flag is set are left untouched by the QCQP launch and by the finish kernel.
 hipError_t evaluate_points(const TubeArgs& a, int P, const double* T, double tol, int max_iter,
-                           const mtg_time_params& p, double* pts, double* coeffs,
-                           double* qcost, int32_t* qstatus, double* maxima, double* softc,
+                           const mtg_time_params& p, const Workspace& w, const int32_t* skip,
                            double* Jall, double* cost, double* grad, int32_t* status,
                            hipStream_t st) {
   const int S = a.S;
   const int64_t BP = a.B * P;
   hipLaunchKernelGGL(tube_time_points_kernel, dim3(blocks_for(BP * S)), dim3(256), 0, st, S,
-                     a.B, P, T, p.increment, pts);
+                     a.B, P, T, p.increment, w.pts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   TubeArgs q = a;
   q.B = BP;
-  q.times = pts;
+  q.times = w.pts;
   q.rep = P;
-  e = launch_tube_solve(q, tol, max_iter, nullptr, coeffs, qcost, nullptr, qstatus, st);
+  q.skip = skip;
+  e = launch_tube_solve(q, tol, max_iter, nullptr, w.coeffs, w.qcost, nullptr, w.qstatus, st);
   if (e != hipSuccess) return e;
   if (p.n_soft > 0) {
     SoftLimits lim{};
     lim.n = p.n_soft;
     for (int c = 0; c < p.n_soft; ++c) lim.value[c] = p.soft_limit[c];
     const SoftCostArgs none{};
-    const SoftCostArgs last{softc, lim, p.soft_weight, p.soft_maximum_cost};
+    const SoftCostArgs last{w.softc, lim, p.soft_weight, p.soft_maximum_cost};
     for (int c = 0; c < p.n_soft; ++c) {
-      e = launch_max_magnitude(a.N, 3, S, BP, p.soft_derivative[c], coeffs, pts, nullptr, maxima,
-                               nullptr, p.n_soft, c, c == p.n_soft - 1 ? last : none, st);
+      e = launch_max_magnitude(a.N, 3, S, BP, p.soft_derivative[c], w.coeffs, w.pts, nullptr,
+                               w.maxima, nullptr, p.n_soft, c, c == p.n_soft - 1 ? last : none,
+                               st);
       if (e != hipSuccess) return e;
     }
   }
   hipLaunchKernelGGL(tube_time_finish_kernel, dim3(blocks_for(a.B)), dim3(256), 0, st, S, a.B,
-                     P, pts, qcost, qstatus, p.n_soft > 0 ? softc : nullptr, p.time_penalty,
-                     p.increment, Jall, cost, grad, status);
+                     P, w.pts, w.qcost, w.qstatus, p.n_soft > 0 ? w.softc : nullptr,
+                     p.time_penalty, p.increment, skip, Jall, cost, grad, status);
   return hipGetLastError();
 }
 
-// Workspace of evaluate_points for B x P problems, carved from one block.
-struct PointBuffers {
-  double *pts, *coeffs, *qcost, *maxima, *softc, *Jall;
-  int32_t* qstatus;
-};
-size_t point_bytes(int N, int S, int64_t BP, int n_soft) {
-  return sizeof(double) * BP * (S + static_cast<size_t>(S) * 3 * N + 3 + (n_soft > 0 ? n_soft : 1)) +
-         sizeof(int32_t) * (BP + 2);
-}
-PointBuffers carve_points(void* base, int N, int S, int64_t BP, int n_soft) {
-  PointBuffers pb;
-  double* d = static_cast<double*>(base);
-  pb.coeffs = d;  // 16-byte aligned first (S * 3 * N doubles per problem)
-  d += BP * S * 3 * N;
-  pb.pts = d;
-  d += BP * S;
-  pb.qcost = d;
-  d += BP;
-  pb.softc = d;
-  d += BP;
-  pb.Jall = d;
-  d += BP;
-  pb.maxima = d;
-  d += BP * (n_soft > 0 ? n_soft : 1);
-  pb.qstatus = reinterpret_cast<int32_t*>(d);
-  return pb;
+int points_of(const mtg_time_params& p, int S, bool optimiser) {
+  return (optimiser || p.grad_mode == 2) ? 2 * S + 1 : 1;
 }
 
 }  // namespace
 
+size_t tube_time_workspace_bytes(int N, int S, int64_t B, const mtg_time_params& p,
+                                 bool optimiser) {
+  Workspace w;
+  return carve(nullptr, N, S, B, points_of(p, S, optimiser), p.n_soft, optimiser, &w) + 256;
+}
+
+int64_t tube_time_problems(int S, int64_t B, const mtg_time_params& p, bool optimiser) {
+  return B * points_of(p, S, optimiser);
+}
+
 int tube_time_cost(const TubeArgs& a, double tol, int max_iter, const mtg_time_params& p,
-                   double* cost, double* grad, int32_t* status, hipStream_t st) {
-  const int P = p.grad_mode == 2 ? 2 * a.S + 1 : 1;
-  const int64_t BP = a.B * P;
-  Scratch ws(st);
-  if (ws.alloc(point_bytes(a.N, a.S, BP, p.n_soft)) != hipSuccess) return MTG_ERR_HIP;
-  const PointBuffers pb = carve_points(ws.p, a.N, a.S, BP, p.n_soft);
-  const hipError_t e =
-      evaluate_points(a, P, a.times, tol, max_iter, p, pb.pts, pb.coeffs, pb.qcost, pb.qstatus,
-                      pb.maxima, pb.softc, nullptr, cost, p.grad_mode == 2 ? grad : nullptr,
-                      status, st);
+                   double* cost, double* grad, int32_t* status, void* workspace,
+                   size_t workspace_bytes, hipStream_t st) {
+  const int P = points_of(p, a.S, false);
+  Workspace w;
+  if (tube_time_workspace_bytes(a.N, a.S, a.B, p, false) > workspace_bytes)
+    return MTG_ERR_INVALID_ARG;
+  carve(workspace, a.N, a.S, a.B, P, p.n_soft, false, &w);
+  const hipError_t e = evaluate_points(a, P, a.times, tol, max_iter, p, w, nullptr, nullptr,
+                                       cost, p.grad_mode == 2 ? grad : nullptr, status, st);
   return e == hipSuccess ? MTG_OK : MTG_ERR_HIP;
 }
 
+// The optimiser runs max_evals rounds, all stream-ordered: a trajectory that
+// has stopped sets its `done` flag, and later rounds skip it in every kernel
+// (its QCQP workgroups return at once), so no host round trip is needed to
+// know when to stop and the whole call can be captured in a graph.
 int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_iter,
                        const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
-                       int32_t* status, hipStream_t st) {
-  const int S = a.S, P = 2 * S + 1;
-  const int64_t B = a.B, BP = B * P;
-  const size_t state_bytes = sizeof(double) * (4 * B * S + 2 * B) + sizeof(int32_t) * (3 * B + 2);
-  Scratch ws(st);
-  const size_t pbytes = point_bytes(a.N, S, BP, p.n_soft);
-  if (ws.alloc(pbytes + state_bytes + 64) != hipSuccess) return MTG_ERR_HIP;
-  const PointBuffers pb = carve_points(ws.p, a.N, S, BP, p.n_soft);
-  double* d = reinterpret_cast<double*>(static_cast<char*>(ws.p) + ((pbytes + 15) & ~size_t(15)));
-  OptState s;
-  s.T0 = d;
-  s.Tc = d + B * S;
-  s.g = d + 2 * B * S;
-  s.Ttr = d + 3 * B * S;
-  s.f = d + 4 * B * S;
-  s.alpha = s.f + B;
-  s.evals = reinterpret_cast<int32_t*>(s.alpha + B);
-  s.done = s.evals + B;
-  s.st = s.done + B;
-  int32_t* n_active = s.st + B;
+                       int32_t* status, void* workspace, size_t workspace_bytes,
+                       hipStream_t st) {
+  const int S = a.S, P = points_of(p, S, true);
+  const int64_t B = a.B;
+  Workspace w;
+  if (tube_time_workspace_bytes(a.N, S, B, p, true) > workspace_bytes) return MTG_ERR_INVALID_ARG;
+  carve(workspace, a.N, S, B, P, p.n_soft, true, &w);
+  const OptState& s = w.s;
   hipLaunchKernelGGL(tube_time_opt_init_kernel, dim3(blocks_for(B * S)), dim3(256), 0, st, S, B,
                      times_io, s);
   if (hipGetLastError() != hipSuccess) return MTG_ERR_HIP;
@@ -306,22 +313,13 @@ int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_
   // qcqp_impl:152-157); Q and A^-1 follow the evaluation points.
   TubeArgs q = a;
   q.times_cp = s.T0;
-  int32_t host_active = 0;
   for (int round = 0; round < max_evals; ++round) {
-    hipError_t e = evaluate_points(q, P, s.Ttr, tol, max_iter, p, pb.pts, pb.coeffs, pb.qcost,
-                                   pb.qstatus, pb.maxima, pb.softc, pb.Jall, nullptr, nullptr,
-                                   nullptr, st);
+    hipError_t e = evaluate_points(q, P, s.Ttr, tol, max_iter, p, w, s.done, w.Jall, nullptr,
+                                   nullptr, nullptr, st);
     if (e != hipSuccess) return MTG_ERR_HIP;
-    if (hipMemsetAsync(n_active, 0, sizeof(int32_t), st) != hipSuccess) return MTG_ERR_HIP;
     hipLaunchKernelGGL(tube_time_opt_step_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S, B, P,
-                       round == 0 ? 1 : 0, max_evals, p.increment, pb.Jall, pb.qstatus, s,
-                       n_active);
+                       round == 0 ? 1 : 0, max_evals, p.increment, w.Jall, w.qstatus, s);
     if (hipGetLastError() != hipSuccess) return MTG_ERR_HIP;
-    if (hipMemcpyAsync(&host_active, n_active, sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
-            hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return MTG_ERR_HIP;
-    if (host_active == 0) break;
   }
   hipLaunchKernelGGL(tube_time_opt_final_kernel, dim3(blocks_for(B * S)), dim3(256), 0, st, S, B,
                      s, times_io, cost, evals, status);

@@ -157,7 +157,80 @@ def test_tube_time_rejects_bad_arguments(ctx, dev, oracle):
     c = torch.empty(1, dtype=torch.float64, device=dev)
     g = torch.empty((1, 4), dtype=torch.float64, device=dev)
     vp = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
     rc = lib().mtg_tube_time_cost(ctx.handle, N, R, 4, 1, vp(pos), vp(fv), vp(t), vp(t),
                                   vp(radii), 1e-10, 100, ctypes.byref(p), vp(c), vp(g), None,
-                                  None)
+                                  vp(ws), ws.numel(), None)
     assert rc == -4  # MTG_ERR_UNSUPPORTED: grad_mode 1 needs d held fixed
+    # a workspace below mtg_tube_time_workspace_bytes is refused, as is none
+    p2 = make_time_params(grad_mode=2)
+    need = mtg.tube_time_workspace_bytes(N, 4, 1, p2, False)
+    for wp, nb in ((vp(ws), need - 1), (None, need)):
+        rc = lib().mtg_tube_time_cost(ctx.handle, N, R, 4, 1, vp(pos), vp(fv), vp(t), vp(t),
+                                      vp(radii), 1e-10, 100, ctypes.byref(p2), vp(c), vp(g),
+                                      None, wp, nb, None)
+        assert rc == -1
+    # grids beyond one launch (2^26 problems) are refused by the size query
+    assert lib().mtg_tube_time_workspace_bytes(N, 10, 1 << 22, ctypes.byref(p2), 0) == -1
+
+
+def test_tube_time_poisoned_workspace(ctx, dev, oracle):
+    """Every scratch word the objective reads is written first in the same
+    call: with the caller's workspace filled with 0xFF bytes (NaN doubles,
+    int32 -1) the results are bit-identical to a zeroed workspace, for the
+    cost (grad on and off) and for the optimiser.  This is the check for the
+    round-1 stale-J report."""
+    import mav_tube_trajectory_generation_amd as mtg
+    from mav_tube_trajectory_generation_amd._abi import make_time_params
+    S = 4
+    items = _batch(oracle, S, range(500, 504))
+    t0 = _T(dev, np.stack([t for _, t in items]))
+    t = t0 * 1.05
+    pos, fv, radii = _geometry(dev, items)
+    for grad in (False, True):
+        p = make_time_params(grad_mode=2 if grad else 0)
+        nb = mtg.tube_time_workspace_bytes(N, S, len(items), p, False)
+        outs = []
+        for fill in (0x00, 0xFF):
+            ws = torch.full((nb,), fill, dtype=torch.uint8, device=dev)
+            outs.append(mtg.tube_time_cost(ctx, N, R, pos, fv, t0, t, radii, grad=grad,
+                                           workspace=ws))
+        for k in ("cost", "status") + (("grad",) if grad else ()):
+            assert torch.equal(outs[0][k], outs[1][k]), (grad, k)
+        assert torch.isfinite(outs[1]["cost"]).all()
+    p = make_time_params(grad_mode=2)
+    nb = mtg.tube_time_workspace_bytes(N, S, len(items), p, True)
+    outs = []
+    for fill in (0x00, 0xFF):
+        ws = torch.full((nb,), fill, dtype=torch.uint8, device=dev)
+        outs.append(mtg.tube_time_optimize(ctx, N, R, pos, fv, radii, t0, max_evals=6,
+                                           workspace=ws))
+    for k in ("times", "cost", "evals", "status"):
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_tube_time_optimize_graph_capture(ctx, dev, oracle):
+    """The optimiser never allocates or synchronises, so a whole call can be
+    captured in a HIP graph; the replay gives the eager result."""
+    import mav_tube_trajectory_generation_amd as mtg
+    from mav_tube_trajectory_generation_amd._abi import make_time_params
+    S = 4
+    items = _batch(oracle, S, range(510, 513))
+    t0 = _T(dev, np.stack([t for _, t in items]))
+    pos, fv, radii = _geometry(dev, items)
+    eager = mtg.tube_time_optimize(ctx, N, R, pos, fv, radii, t0, max_evals=5)
+    p = make_time_params(grad_mode=2)
+    ws = torch.empty(mtg.tube_time_workspace_bytes(N, S, len(items), p, True), dtype=torch.uint8,
+                     device=dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        tin = t0.clone()
+        with torch.cuda.graph(g, stream=side):
+            out = mtg.tube_time_optimize(ctx, N, R, pos, fv, radii, tin, max_evals=5,
+                                         workspace=ws)
+    g.replay()
+    torch.cuda.synchronize()
+    for k in ("times", "cost", "evals", "status"):
+        assert torch.equal(out[k], eager[k]), k
