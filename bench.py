@@ -41,7 +41,9 @@ def parse():
     p.add_argument("--segments", type=int, default=10)
     p.add_argument("--workload", choices=["linear", "time", "tube", "time-qcqp", "sample",
                                           "extrema"], default="linear")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-seconds", type=float, default=20.0,
+                   help="total CPU-baseline budget (all reps, both modes)")
+    p.add_argument("--cpu-reps", type=int, default=5)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph)")
     p.add_argument("--soft", action="store_true",
@@ -75,9 +77,42 @@ def _oracle_problems(N, D, S, seeds, tube=False):
     return pyoracle, masks, vals, times
 
 
-def cpu_baseline(wl, N, D, r, S, seconds, sample_args=None):
-    """Oracle (reference-faithful C++ port, 1 thread) on a bounded sample of
-    the same workload.  Returns (rate, units, description)."""
+def _cpu_threads():
+    """All-core mode: the CPUs this process may run on, capped by
+    OMP_NUM_THREADS when set (the GPU box's CPU share is 16)."""
+    n = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _median_rate(run, reps, seconds):
+    """run(seconds) -> (units, wall seconds); one short warm-up, then the
+    median over `reps` repetitions of the rate."""
+    run(min(0.3, seconds))
+    rates = sorted(u / s for u, s in (run(seconds) for _ in range(reps)))
+    return rates[len(rates) // 2], rates
+
+
+def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None):
+    """Oracle (reference-faithful C++ port, oracle/mtg_oracle.cpp, built
+    -O3 -march=x86-64-v3) on a bounded sample of the same workload, on the GPU
+    host: 1 thread and all cores (std::thread pool over independent
+    trajectories), median of `reps` repetitions after a warm-up
+    (the harness shape of polynomial_timing_evaluation.cpp:
+    93-127).  The reference's unconditional stdout prints (linear_impl:
+    287-292, 370) are not part of the port, so they are excluded.  For the
+    linear workload also C1 (one 3-segment problem, 1 thread)."""
     import ctypes
     seeds = range(105, 105 + (256 if wl in ("linear", "sample", "extrema") else
                               16 if wl == "time-qcqp" else 64))
@@ -85,49 +120,70 @@ def cpu_baseline(wl, N, D, r, S, seconds, sample_args=None):
                                                     tube=wl in ("tube", "time-qcqp"))
     K = N // 2
     B = len(seeds)
-    if wl == "linear":
+    dp = ctypes.POINTER(ctypes.c_double)
+
+    def linear_runner(m, v, t, nb, s_):
         L = pyoracle.lib()
-        dp = ctypes.POINTER(ctypes.c_double)
         L.orc_bench_linear.argtypes = [ctypes.c_int] * 6 + [
             ctypes.POINTER(ctypes.c_uint8), dp, dp, ctypes.c_int, ctypes.c_double,
             ctypes.POINTER(ctypes.c_int64), dp]
-        n, sec = ctypes.c_int64(), ctypes.c_double()
-        rc = L.orc_bench_linear(N, D, r, S, K, B,
-                                masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
-                                vals.ctypes.data_as(dp), times.ctypes.data_as(dp), 1, seconds,
-                                ctypes.byref(n), ctypes.byref(sec))
-        if rc != 0:
-            raise RuntimeError(f"oracle baseline failed ({rc})")
-        units, sec = n.value, sec.value
+
+        def run(threads, sec):
+            n, el = ctypes.c_int64(), ctypes.c_double()
+            rc = L.orc_bench_linear(N, D, r, s_, K, nb,
+                                    m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                    v.ctypes.data_as(dp), t.ctypes.data_as(dp), threads, sec,
+                                    ctypes.byref(n), ctypes.byref(el))
+            if rc != 0:
+                raise RuntimeError(f"oracle baseline failed ({rc})")
+            return n.value, el.value
+        return run
+
+    radii = np.full((B, S, 2), 0.15)
+    if wl == "linear":
+        run = linear_runner(masks, vals, times, B, S)
         what = "solves (setupFromVertices + solveLinear + computeCost)"
-    elif wl == "time":
-        units, sec = pyoracle.bench_workload(1, N, D, r, S, K, masks, vals, times,
-                                             param_i=50, seconds=seconds)
-        what = "50-evaluation time optimisations (orc_time_optimize)"
-    elif wl == "tube":
-        radii = np.full((B, S, 2), 0.15)
-        units, sec = pyoracle.bench_workload(2, N, D, r, S, K, masks, vals, times, radii=radii,
-                                             seconds=seconds)
-        what = "tube QCQP solves (oracle primal-dual IPM, tol 1e-10)"
-    elif wl == "time-qcqp":
-        radii = np.full((B, S, 2), 0.15)
-        units, sec = pyoracle.bench_workload(5, N, D, r, S, K, masks, vals, times, radii=radii,
-                                             seconds=seconds)
-        what = ("time-objective evaluations with the QCQP inner solve and the central-"
-                "difference gradient (2S+1 oracle IPM solves each)")
-    elif wl == "extrema":
-        units, sec = pyoracle.bench_workload(4, N, D, r, S, K, masks, vals, times,
-                                             seconds=seconds)
-        what = ("soft-constraint evaluations (two computeMaximumOfMagnitude searches, "
-                "companion-matrix roots)")
     else:
-        dt, kmax = sample_args
-        units, sec = pyoracle.bench_workload(3, N, D, r, S, K, masks, vals, times, param_i=kmax,
-                                             param_d=dt, seconds=seconds)
-        what = f"samples (evaluateRange, derivatives 0..{kmax}, dt={dt})"
-    desc = (f"{units} {what} cycling over {B} of the same {S}-seg problems "
-            f"(seeds 105..{104 + B}), oracle C++ port, 1 thread, ~{seconds:.0f} s")
-    return units / sec, units, desc
+        kind, pi, pd, rad, what = {
+            "time": (1, 50, 0.0, None, "50-evaluation time optimisations (orc_time_optimize)"),
+            "tube": (2, 0, 0.0, radii, "tube QCQP solves (oracle primal-dual IPM, tol 1e-10)"),
+            "time-qcqp": (5, 0, 0.0, radii,
+                          "time-objective evaluations with the QCQP inner solve and the central-"
+                          "difference gradient (2S+1 oracle IPM solves each)"),
+            "extrema": (4, 0, 0.0, None, "soft-constraint evaluations (two "
+                        "computeMaximumOfMagnitude searches, companion-matrix roots)"),
+        }.get(wl, (3, None, None, None, None))
+        if kind == 3:
+            dt, kmax = sample_args
+            pi, pd = kmax, dt
+            what = f"samples (evaluateRange, derivatives 0..{kmax}, dt={dt})"
+
+        def run(threads, sec):
+            return pyoracle.bench_workload(kind, N, D, r, S, K, masks, vals, times, radii=rad,
+                                           param_i=pi, param_d=pd, threads=threads,
+                                           seconds=sec)
+    threads = _cpu_threads()
+    per_rep = seconds / (2 * reps + (1 if wl == "linear" else 0))
+    one, one_all = _median_rate(lambda s_: run(1, s_), reps, per_rep)
+    allc, allc_all = _median_rate(lambda s_: run(threads, s_), reps, per_rep)
+    out = {
+        "value": allc, "cores": threads, "kind": "port",
+        "single_core": {"value": one, "cores": 1, "reps": [round(x, 3) for x in one_all]},
+        "all_core_reps": [round(x, 3) for x in allc_all],
+        "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+        "method": (f"median of {reps} repetitions of ~{per_rep:.1f} s after a warm-up, "
+                   "std::chrono::steady_clock; the reference's stdout prints excluded"),
+        "sample": (f"{what} cycling over {B} of the same {S}-seg problems (seeds 105..{104 + B}),"
+                   f" oracle C++ port (-O3 -march=x86-64-v3); value = all {threads} threads"),
+    }
+    if wl == "linear":
+        # C1: a single 3-segment problem (BASELINE.json configs[0]), 1 thread.
+        _, m1, v1, t1 = _oracle_problems(N, D, 3, [105])
+        c1, _ = _median_rate(lambda s_: linear_runner(m1, v1, t1, 1, 3)(1, s_), reps,
+                             per_rep / reps)
+        out["c1_3seg_single"] = {"value": c1, "unit": "trajectories/s", "cores": 1,
+                                 "latency_us": 1e6 / c1}
+    return out
 
 
 def load_pmc_traffic(workload, config_key):
@@ -142,6 +198,38 @@ def load_pmc_traffic(workload, config_key):
     except (OSError, ValueError):
         pass
     return None
+
+
+def tube_flops_per_iter(N, S):
+    """FLOP per interior-point iteration of one tube QCQP:
+    m (2 v^2 + 2 v) constraint evaluation + m v^2 Hessian accumulation +
+    (S-1) (b^3/3 + b^3 + 2 b^3) block-tridiagonal KKT factorisation, with
+    m = (S-1) + 3 S (N-2) constraints, v = 3 N variables per constraint
+    stencil, b = 3 N/2 per block (0.79 MFLOP at S = 10, N = 10)."""
+    m = (S - 1) + 3 * S * (N - 2)
+    v = 3 * N
+    b = 3 * (N // 2)
+    return m * (2 * v * v + 2 * v) + m * v * v + (S - 1) * (b ** 3 / 3 + b ** 3 + 2 * b ** 3)
+
+
+def linear_flops(N, D, S, nf, np_):
+    """SURVEY.md 8(d) dense algorithmic FLOP count of one linear solve (81 032
+    at S = 10); the kernel's banded / time-scaled route does fewer."""
+    return (4 * N ** 3 * S + N ** 2 * S + np_ ** 3 / 3 + 2 * np_ * nf * D
+            + 2 * np_ ** 2 * D + 2 * N ** 2 * D * S + D * S * (2 * N ** 2 + 2 * N))
+
+
+def config_name(wl, B, world, S):
+    if wl == "linear" and S == 10:
+        if B * world == 65536:
+            return f"C4: 65536 x 10-segment sharded {world} way(s)"
+        if world == 1 and B == 1024:
+            return "C2: 1024 x 10-segment linear solve"
+    if wl == "tube" and S == 10 and B == 4096 and world == 1:
+        return "C3: 4096 x 10-segment tube QCQP"
+    if wl == "time" and S == 10 and B == 4096 and world == 1:
+        return "C5: 4096 x 50-evaluation time allocation"
+    return f"{wl}: {B} x {S}-segment per GPU"
 
 
 def main():
@@ -165,7 +253,7 @@ def main():
     wl = args.workload
     B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "time-qcqp": 1024,
                        "sample": 1024, "extrema": 1024}[wl]
-    from mav_tube_trajectory_generation_amd.shard import select_best, shard_range
+    from mav_tube_trajectory_generation_amd.shard import select_best_device, shard_range
     global_batch = B * world
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
     mask, fixed, times, pos = mtg.generate_random_problems(N, D, S, B, seed0=seed0)
@@ -175,20 +263,27 @@ def main():
     times_d = torch.from_numpy(times).to(dev)
     nf = plan.n_fixed
     stream = torch.cuda.current_stream(dev)
+    bound = "fp64_vector"
+    flops_per_step = None   # algorithmic FP64 work of one step (None: not FP64-bound)
+    flop_note = None
+    useful_per_step = None  # units that count towards `value` (converged solves)
+    metric_base = "trajectories/sec (10-seg, N=10, 3D minimum-snap) at 1/2/4/8 MI355X"
 
     if wl == "linear":
         out = plan.solve(fixed_d, times_d, free=False)
 
         def step():
             plan.solve(fixed_d, times_d, free=False, out=out)
-            if world > 1:  # RCCL all-gather of costs + global argmin
-                return select_best(out["cost"], global_batch)
+            if world > 1:  # RCCL all-gather of (cost, index) + global argmin, on device
+                return select_best_device(out["cost"], global_batch)
             return None
 
         bytes_per_traj = (D * nf + S) * 8 + (S * D * N + 1) * 8 + 4  # + status
-        metric = "trajectories/sec (10-seg, N=10, 3D minimum-snap) at 1/2/4/8 MI355X"
+        metric = metric_base
         unit = "trajectories/s"
         units_per_step = B
+        flops_per_step = linear_flops(N, D, S, nf, plan.n_free) * B
+        flop_note = "SURVEY 8(d) dense count per solve x B"
     elif wl == "time":
         max_evals = 50
 
@@ -197,12 +292,21 @@ def main():
         def step():
             return plan.time_optimize(fixed_d, times_d, max_evals=max_evals, soft=soft)
 
+        probe = step()
+        torch.cuda.synchronize(dev)
+        solves = int(probe["solves"].sum().item())
+        evals_mean = float(probe["evals"].float().mean().item())
         bytes_per_traj = (D * nf + S) * 8 + (S + 2) * 8
         metric = "time-allocation optimisations/sec (4096 traj x 50 evals, 10-seg, N=10, 3D)"
         if args.soft:
             metric += " + soft max|v|<=3, max|a|<=5"
+            bound = "fp64_vector (soft: extremum search not counted)"
         unit = "trajectories/s"
         units_per_step = B
+        flops_per_step = linear_flops(N, D, S, nf, plan.n_free) * solves
+        flop_note = (f"dense solve count x {solves} inner solves per launch (measured, gradient "
+                     f"points included; {solves / B:.1f} per trajectory, {evals_mean:.1f} "
+                     "counted evaluations)")
     elif wl == "sample":
         # Sampling of solved trajectories (evaluateRange for derivatives 0..4,
         # the [t, p, v, a, j, s] rows of printMatlabSampledTrajectory) at
@@ -224,6 +328,7 @@ def main():
         metric = "trajectory samples/sec (evaluateRange, dt=0.01, derivatives 0..4, 3D)"
         unit = "samples/s"
         units_per_step = n_total
+        bound = "hbm"
     elif wl == "extrema":
         # Soft-constraint cost of max |v| <= 3, max |a| <= 5 (v_max, a_max of
         # estimateSegmentTimes) on solved trajectories: two batched
@@ -241,6 +346,7 @@ def main():
         metric = "soft-constraint evaluations/sec (max |v|, |a| extremum search, 10-seg, N=10, 3D)"
         unit = "trajectories/s"
         units_per_step = B
+        bound = "hbm"
     else:  # tube, time-qcqp
         radii = torch.full((B, S, 2), 0.15, dtype=torch.float64, device=dev)
         pos_d = torch.from_numpy(pos).to(dev)
@@ -250,45 +356,80 @@ def main():
         tf[:, :, 0] = pos[:, 0, :]
         tf[:, :, M] = pos[:, S, :]
         tfix = torch.from_numpy(tf).to(dev)
+        # The same inputs every step, so the per-step status and iteration
+        # counts are those of this probe (read once, outside the timed loop).
+        probe = mtg.tube_solve(ctx, N, r, pos_d, tfix, times_d, times_d, radii)
+        torch.cuda.synchronize(dev)
+        conv = int((probe["status"] == 0).sum().item())
+        iters = int(probe["iters"].sum().item())
+        hist = {int(k): int(v) for k, v in zip(*np.unique(probe["status"].cpu().numpy(),
+                                                           return_counts=True))}
+        f_iter = tube_flops_per_iter(N, S)
 
         if wl == "tube":
             def step():
                 return mtg.tube_solve(ctx, N, r, pos_d, tfix, times_d, times_d, radii)
 
             bytes_per_traj = ((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8 + (S * 3 * N + 1) * 8
-            metric = "tube QCQP solves/sec (4096 x 10-seg, N=10, 3D)"
+            metric = "converged tube QCQP solves/sec (4096 x 10-seg, N=10, 3D)"
+            useful_per_step = conv
+            flops_per_step = f_iter * iters
+            flop_note = (f"SURVEY 8(d) C3: {f_iter:.0f} FLOP/iteration x {iters} IPM iterations "
+                         f"per launch (measured, {iters / B:.1f} per problem); status "
+                         f"histogram {hist}")
         else:
             # config 5's callback in the fork's form (solveQCQP inside
             # objectiveFunctionTime, nonlinear_impl:892) with the central-
             # difference gradient the optimiser uses: 2S+1 QCQPs per unit.
+            from mav_tube_trajectory_generation_amd._abi import make_time_params
+            tparams = make_time_params(500.0, 0.1, 0.1, 1.0, 2, None, 100.0)
+            ws = torch.empty(mtg.tube_time_workspace_bytes(N, S, B, tparams, False),
+                             dtype=torch.uint8, device=dev)
+
             def step():
                 return mtg.tube_time_cost(ctx, N, r, pos_d, tfix, times_d, times_d, radii,
-                                          grad=True)
+                                          grad=True, workspace=ws)
 
             # inputs once + cost and gradient out (scratch traffic not counted)
             bytes_per_traj = ((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8 + (S + 1) * 8 + 4
             metric = ("time-objective evaluations/sec with the QCQP inner solve + FD gradient "
                       "(1024 x 10-seg, N=10, 3D)")
+            flops_per_step = f_iter * iters * (2 * S + 1)
+            flop_note = (f"approximate: {f_iter:.0f} FLOP/iteration x the IPM iterations of the "
+                         f"base solves ({iters / B:.1f} per problem) x (2S+1) problems")
         unit = "trajectories/s"
         units_per_step = B
 
-    # World 1: the K timed steps are captured into one HIP graph and
-    # replayed, so launches are back to back (no host launch gaps) and the
-    # per-launch duration is (end - start) / K from two HIP events on the
-    # launch stream.  Otherwise (collective per step, or millisecond kernels)
-    # eager launches with one event pair per launch.
-    # (time-qcqp takes stream-ordered scratch inside the call: eager.)
-    use_graph = world == 1 and not args.no_graph and wl != "time-qcqp"
+    # World 1: the K timed steps are captured into one HIP graph and replayed,
+    # so launches are back to back (no host launch gaps) and the per-step
+    # device time is (end - start) / K from two HIP events on the launch
+    # stream.  World > 1 (linear): the step, RCCL all-gather included, is
+    # captured the same way after eager warm-up steps (the communicator is
+    # initialised outside the capture); if the capture fails the loop runs
+    # eagerly with one event pair per step.
+    use_graph = not args.no_graph
+    graph_note = ""
+    graphs = {}
+    if world > 1:
+        for _ in range(max(args.warmup, 2)):
+            step()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
     if use_graph:
-        graphs = {}
-        for name, n in (("warmup", args.warmup), ("timed", args.steps)):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(n):
-                    step()
-            graphs[name] = g
-        graphs["warmup"].replay()
-    else:
+        try:
+            for name, n in (("warmup", args.warmup), ("timed", args.steps)):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(n):
+                        step()
+                graphs[name] = g
+            graphs["warmup"].replay()
+        except Exception as exc:  # capture unsupported here: eager launches
+            use_graph = False
+            graph_note = f" (graph capture failed: {type(exc).__name__}; eager)"
+            torch.cuda.synchronize(dev)
+            print(f"bench: graph capture failed, eager: {exc}", file=sys.stderr)
+    if not use_graph:
         for _ in range(args.warmup):
             step()
     torch.cuda.synchronize(dev)
@@ -302,6 +443,9 @@ def main():
         ev0.record(stream)
         graphs["timed"].replay()
         ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
@@ -324,29 +468,42 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    fp64 = None
-    if wl == "linear":
-        # SURVEY.md 8(d) dense FLOP count per trajectory (81 032 at S=10);
-        # the kernel's banded / time-scaled route does fewer operations.
-        nf_, np_ = plan.n_fixed, plan.n_free
-        flops = (4 * N ** 3 * S + N ** 2 * S + np_ ** 3 / 3 + 2 * np_ * nf_ * D
-                 + 2 * np_ ** 2 * D + 2 * N ** 2 * D * S + D * S * (2 * N ** 2 + 2 * N))
-        tf = flops * B / (kernel_ms * 1e-3) / 1e12
-        fp64 = {"algorithmic_flops_per_traj": flops, "achieved_tflops": tf,
-                "peak_tflops": FP64_PEAK_TFLOPS, "frac": tf / FP64_PEAK_TFLOPS}
-    total_units = units_per_step * args.steps * world
+    counted = useful_per_step if useful_per_step is not None else units_per_step
+    total_units = counted * args.steps * world
     value = total_units / elapsed
     alg_bytes = bytes_per_traj * B
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
     config_key = f"{wl}:B{B}:S{S}"
     traffic = load_pmc_traffic(wl, config_key)
+    timing = ("HIP events around one graph replay of the K steps, / K" if use_graph else
+              "HIP event pair per step, mean") + graph_note
+    hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+           "alg_bytes_per_launch": alg_bytes, "traffic": traffic}
+    if flops_per_step is not None:
+        tfl = flops_per_step / (kernel_ms * 1e-3) / 1e12
+        roof = {"bound": bound, "achieved": tfl, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tfl / FP64_PEAK_TFLOPS, "traffic": traffic,
+                "alg_flops_per_launch": flops_per_step, "flop_count": flop_note,
+                "hbm": hbm}
+    else:
+        roof = {"bound": "hbm", **{k: hbm[k] for k in ("achieved", "peak", "unit", "frac")},
+                "traffic": traffic, "alg_bytes_per_launch": alg_bytes}
+    roof["kernel_ms"] = kernel_ms
+    roof["kernel_timing"] = timing
+    if world > 1:
+        roof["kernel_timing"] += "; per-step device time includes the all-gather and argmin"
 
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            rate, _, desc = cpu_baseline(wl, N, D, r, S, args.cpu_seconds,
-                                         sample_args=(0.01, 4) if wl == "sample" else None)
-            cpu = {"value": rate, "unit": unit, "cores": 1, "kind": "port", "sample": desc}
+            cpu = cpu_baseline(wl, N, D, r, S, args.cpu_seconds, args.cpu_reps,
+                               sample_args=(0.01, 4) if wl == "sample" else None)
+            cpu["unit"] = unit
+        cfg = {"workload": config_name(wl, B, world, S), "global_batch": global_batch,
+               "batch_per_gpu": B, "segments": S, "N": N, "D": D, "r": r,
+               "parallelism": f"shard{world}"}
+        if useful_per_step is not None:
+            cfg["converged_per_step"] = useful_per_step
         line = {
             "metric": metric,
             "value": value,
@@ -360,17 +517,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (createRandomVertices seeds 105+i, estimateSegmentTimes v=3 a=5)",
-            "config": {"workload": f"{wl}: {B} x {S}-segment N={N} D={D} r={r} per GPU",
-                       "batch_per_gpu": B, "segments": S, "N": N, "D": D,
-                       "parallelism": f"shard{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes,
-                         "kernel_timing": ("HIP events around one graph replay of the K "
-                                           "launches, / K" if use_graph else
-                                           "HIP event pair per launch, mean"),
-                         "fp64_vector": fp64},
+            "config": cfg,
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

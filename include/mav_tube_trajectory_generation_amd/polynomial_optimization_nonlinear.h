@@ -244,7 +244,8 @@ class PolynomialOptimizationNonLinear {
     const mtg_time_params p = timeParams(0);
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
     internal::checkStatus(mtg_time_optimize(planOf(), 1, d_df.get(), d_t.get(), &p, budget,
-                                            d_cost.get(), d_ev.get(), d_st.get(), nullptr),
+                                            d_cost.get(), d_ev.get(), nullptr, d_st.get(),
+                                            nullptr),
                           "mtg_time_optimize");
     internal::synchronize();
     d_t.download(times.data(), S);

@@ -200,11 +200,13 @@ int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
  *   times_io   B x S  in: initial times T0, out: optimised times
  *   cost       B      final objective
  *   evals      B      objective evaluations used (nullable)
+ *   solves     B      inner solves run, gradient points included (nullable;
+ *                     the work count behind the FP64 roofline of bench.py)
  */
 int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       double* times_io, const mtg_time_params* params,
                       int max_evals, double* cost, int32_t* evals,
-                      int32_t* status, void* stream);
+                      int32_t* solves, int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * Free-derivative objectives of PolynomialOptimizationNonLinear (the NLopt

@@ -75,7 +75,7 @@ SIGNATURES = {
                                      _vp, _vp, _vp, _vp]),
     "mtg_time_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp,
                                          ctypes.POINTER(TimeParams), ctypes.c_int, _vp, _vp,
-                                         _vp, _vp]),
+                                         _vp, _vp, _vp]),
     "mtg_tube_num_constraints": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "mtg_tube_residuals": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -167,7 +167,9 @@ class LinearPlan:
 
     def time_optimize(self, fixed_vals, times, max_evals=50, time_penalty=500.0, increment=0.1,
                       w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0):
-        """Optimise segment times in place on a copy; returns dict(times, cost, evals)."""
+        """Optimise segment times in place on a copy; returns dict(times, cost,
+        evals, solves, status); solves = inner solves run (gradient points
+        included)."""
         import torch
         B = times.shape[0]
         _require(times, (B, self.S), "times")
@@ -176,12 +178,13 @@ class LinearPlan:
         t = times.clone()
         cost = torch.empty(B, dtype=torch.float64, device=dev)
         evals = torch.empty(B, dtype=torch.int32, device=dev)
+        solves = torch.empty(B, dtype=torch.int32, device=dev)
         status = torch.empty(B, dtype=torch.int32, device=dev)
         p = make_time_params(time_penalty, increment, w_d, w_t, 2, soft, soft_weight)
         check(lib().mtg_time_optimize(self._h, B, _ptr(fixed_vals), _ptr(t), ctypes.byref(p),
-                                      max_evals, _ptr(cost), _ptr(evals), _ptr(status),
-                                      _stream(dev)), "mtg_time_optimize")
-        return dict(times=t, cost=cost, evals=evals, status=status)
+                                      max_evals, _ptr(cost), _ptr(evals), _ptr(solves),
+                                      _ptr(status), _stream(dev)), "mtg_time_optimize")
+        return dict(times=t, cost=cost, evals=evals, solves=solves, status=status)
 
     def free_cost(self, fixed_vals, free_vals, times, mode=0, time_penalty=500.0, soft=None,
                   soft_weight=100.0, grad=True):

@@ -488,14 +488,15 @@ int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
 
 int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       double* times_io, const mtg_time_params* params, int max_evals,
-                      double* cost, int32_t* evals, int32_t* status, void* stream) {
+                      double* cost, int32_t* evals, int32_t* solves, int32_t* status,
+                      void* stream) {
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
   if (!valid_soft(plan, params)) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   return from_hip(mtg::launch_time_optimize(plan->dev, B, fixed_vals, times_io, *params,
-                                            max_evals, cost, evals, status,
+                                            max_evals, cost, evals, solves, status,
                                             static_cast<hipStream_t>(stream)));
 }
 

@@ -283,7 +283,8 @@ template <int N, bool kSoft>
 __global__ __launch_bounds__(kWave) void time_optimize_kernel(
     PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ times_io,
     mtg_time_params p, int max_evals, double* __restrict__ cost,
-    int32_t* __restrict__ evals_out, int32_t* __restrict__ status) {
+    int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
+    int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int S = pl.S, D = pl.D, nf = pl.nf;
   const double* tab = pl.tab;
@@ -303,12 +304,13 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   }
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
-  int phase = kBase, gi = 0, evals = 0;
+  int phase = kBase, gi = 0, evals = 0, nsolve = 0;
   double f = 0.0, Jlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   int fl = 0;
   while (phase != kDone) {
     const double J = objective_at<N, kSoft>(t, tab, p, cbuf);  // at T()
+    ++nsolve;
     if (phase == kBase) {
       f = J;
       evals = 1;
@@ -365,6 +367,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   if (t.lane == 0) {
     if (cost) cost[b] = (fl & 1) ? NAN : f;
     if (evals_out) evals_out[b] = evals;
+    if (solves_out) solves_out[b] = nsolve;
     if (status)
       status[b] = (fl & 1) ? MTG_TRAJ_BAD_TIME
                            : ((fl & 2) ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
@@ -434,20 +437,22 @@ template <int N>
 static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* df,
                                     double* times, const mtg_time_params& p,
                                     int max_evals, double* cost, int32_t* evals,
-                                    int32_t* status, hipStream_t st) {
+                                    int32_t* solves, int32_t* status, hipStream_t st) {
   const Layout lay = make_layout(N, pl.S, pl.D);
   if (p.n_soft > 0) {
     const size_t bytes = soft_cbuf_offset(lay) + sizeof(double) * pl.S * pl.D * N;
     hipError_t e = prepare_lds(time_optimize_kernel<N, true>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_kernel<N, true>), dim3(static_cast<unsigned>(B)),
-                       dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, status);
+                       dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, solves,
+                       status);
   } else {
     const size_t bytes = lay.bytes();
     hipError_t e = prepare_lds(time_optimize_kernel<N, false>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_kernel<N, false>), dim3(static_cast<unsigned>(B)),
-                       dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, status);
+                       dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, solves,
+                       status);
   }
   return hipGetLastError();
 }
@@ -493,11 +498,13 @@ hipError_t launch_time_cost(const PlanDev& pl, int64_t B, const double* df,
 
 hipError_t launch_time_optimize(const PlanDev& pl, int64_t B, const double* df,
                                 double* times, const mtg_time_params& p, int max_evals,
-                                double* cost, int32_t* evals, int32_t* status,
-                                hipStream_t st) {
+                                double* cost, int32_t* evals, int32_t* solves,
+                                int32_t* status, hipStream_t st) {
   if (has_time_std(pl))
-    return launch_time_optimize_std(pl, B, df, times, p, max_evals, cost, evals, status, st);
-#define CALL(n) launch_time_opt_n<n>(pl, B, df, times, p, max_evals, cost, evals, status, st)
+    return launch_time_optimize_std(pl, B, df, times, p, max_evals, cost, evals, solves, status,
+                                    st);
+#define CALL(n) \
+  launch_time_opt_n<n>(pl, B, df, times, p, max_evals, cost, evals, solves, status, st)
   MTG_DISPATCH_N(pl.N, CALL)
 #undef CALL
 }

@@ -158,7 +158,8 @@ template <int N, int R, int D, bool kSoft>
 __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
     int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     double* __restrict__ times_io, mtg_time_params p, int max_evals,
-    double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ status) {
+    double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
+    int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int64_t b = blockIdx.x;
   StdSv<N, R, D> sv;
@@ -173,12 +174,13 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
   for (int i = lane; i < S; i += kWave) T[i] = Tcur[i] = T0[i] = times_io[b * S + i];
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
-  int phase = kBase, gi = 0, evals = 0;
+  int phase = kBase, gi = 0, evals = 0, nsolve = 0;
   double f = 0.0, Jlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   bool bad = false, not_spd = false;
   while (phase != kDone) {
     const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd);
+    ++nsolve;
     if (phase == kBase) {
       f = J;
       evals = 1;
@@ -232,6 +234,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
   if (lane == 0) {
     if (cost) cost[b] = bad ? NAN : f;
     if (evals_out) evals_out[b] = evals;
+    if (solves_out) solves_out[b] = nsolve;
     if (status)
       status[b] = bad ? MTG_TRAJ_BAD_TIME : (not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
   }
@@ -270,7 +273,7 @@ hipError_t time_cost_nrd(const PlanDev& pl, int64_t B, const double* df, const d
 template <int N, int R, int D>
 hipError_t time_opt_nrd(const PlanDev& pl, int64_t B, const double* df, double* times,
                         const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
-                        int32_t* status, hipStream_t st) {
+                        int32_t* solves, int32_t* status, hipStream_t st) {
   const bool soft = p.n_soft > 0;
   const size_t bytes = time_std_lds_bytes(N, pl.S, D, soft);
   if (soft) {
@@ -278,13 +281,13 @@ hipError_t time_opt_nrd(const PlanDev& pl, int64_t B, const double* df, double* 
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_std_kernel<N, R, D, true>),
                        dim3(static_cast<unsigned>(B)), dim3(kWave), bytes, st, pl.S, pl.tab,
-                       df, times, p, max_evals, cost, evals, status);
+                       df, times, p, max_evals, cost, evals, solves, status);
   } else {
     hipError_t e = prepare_lds_std(time_optimize_std_kernel<N, R, D, false>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_std_kernel<N, R, D, false>),
                        dim3(static_cast<unsigned>(B)), dim3(kWave), bytes, st, pl.S, pl.tab,
-                       df, times, p, max_evals, cost, evals, status);
+                       df, times, p, max_evals, cost, evals, solves, status);
   }
   return hipGetLastError();
 }
@@ -317,10 +320,11 @@ hipError_t launch_time_cost_std(const PlanDev& pl, int64_t B, const double* df,
 
 hipError_t launch_time_optimize_std(const PlanDev& pl, int64_t B, const double* df,
                                     double* times, const mtg_time_params& p, int max_evals,
-                                    double* cost, int32_t* evals, int32_t* status,
-                                    hipStream_t st) {
+                                    double* cost, int32_t* evals, int32_t* solves,
+                                    int32_t* status, hipStream_t st) {
   if (!has_time_std(pl)) return hipErrorInvalidValue;
-  MTG_TIME_STD_DISPATCH(time_opt_nrd, pl, B, df, times, p, max_evals, cost, evals, status, st)
+  MTG_TIME_STD_DISPATCH(time_opt_nrd, pl, B, df, times, p, max_evals, cost, evals, solves, status,
+                        st)
 }
 
 }  // namespace mtg

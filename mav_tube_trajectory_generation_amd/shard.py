@@ -2,10 +2,20 @@
 
 Trajectories are independent, so a global batch is split into contiguous
 shards, one per rank (one process per GPU), with no exchange during the
-solve.  The only collective is the all-gather of per-trajectory costs for
-selection (RCCL over xGMI when the process group is "nccl"; gloo on CPU in
-the tests), followed by a broadcast of the winning trajectory's
-coefficients from its owner.
+solve.  The only collective is the all-gather for selection (RCCL over xGMI
+when the process group is "nccl"; gloo on CPU in the tests), followed by a
+broadcast of the winning trajectory's coefficients from its owner.
+
+Two selection paths:
+  select_best_device  each rank reduces its shard to one (cost, global index,
+                      rank) triple on the device, the triples are all-gathered
+                      (24 B per rank) and reduced again on the device.  No host
+                      synchronisation, so it can sit inside a timed loop or a
+                      captured graph.
+  select_best         the same, returned as Python numbers (one sync).
+  gather_costs        every per-trajectory cost on every rank (the SURVEY's
+                      512 KiB all-gather at config 4), for callers that need
+                      the whole cost vector.
 """
 import torch
 import torch.distributed as dist
@@ -37,17 +47,52 @@ def gather_costs(local_costs, global_batch, group=None):
     return torch.cat(out)
 
 
+def local_best(local_costs, global_batch, group=None):
+    """This rank's (cost, global index, rank) triple as a float64 device
+    tensor [3]: the shard's smallest cost (NaN never wins; the first index on
+    ties).  An empty shard reports (+inf, -1, rank)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    start, count = shard_range(global_batch, world, rank)
+    # Only kernels with scalar arguments (no host->device copies), so the
+    # whole selection can be captured in a graph.
+    out = torch.full((3,), float(rank), dtype=torch.float64, device=local_costs.device)
+    if count == 0:
+        out[0] = float("inf")
+        out[1] = -1.0
+        return out
+    c = local_costs[:count].to(torch.float64)
+    c = torch.where(torch.isnan(c), torch.full_like(c, float("inf")), c)
+    i = torch.argmin(c)
+    out[0] = c[i]
+    out[1] = i.to(torch.float64) + float(start)
+    return out
+
+
+def select_best_device(local_costs, global_batch, group=None):
+    """Global argmin over all shards without a host sync.  Returns a float64
+    device tensor [3] = (cost, global index, owner rank), identical on every
+    rank.  Ties go to the lowest global index (shards are contiguous and in
+    rank order, so the first rank holding the minimum); if every cost is NaN
+    or +inf the winner is global index 0, as a single-process argmin."""
+    world = dist.get_world_size(group)
+    mine = local_best(local_costs, global_batch, group)
+    flat = torch.empty(world * 3, dtype=torch.float64, device=mine.device)
+    dist.all_gather_into_tensor(flat, mine, group=group)
+    allv = flat.view(world, 3)
+    # Empty shards (index -1) only win when every shard is empty.
+    key = torch.where(allv[:, 1] < 0, torch.full_like(allv[:, 0], float("nan")), allv[:, 0])
+    key = torch.where(torch.isnan(key), torch.full_like(key, float("inf")), key)
+    w = torch.argmin(key)
+    return allv[w]
+
+
 def select_best(local_costs, global_batch, group=None):
     """Global argmin over all shards (NaN costs never win).  Returns
-    (global index, cost, owner rank); identical on every rank."""
-    allc = gather_costs(local_costs, global_batch, group)
-    allc = torch.where(torch.isnan(allc), torch.full_like(allc, float("inf")), allc)
-    idx = int(torch.argmin(allc).item())
-    world = dist.get_world_size(group)
-    owner = next(r for r in range(world)
-                 if shard_range(global_batch, world, r)[0] <= idx <
-                 sum(shard_range(global_batch, world, r)))
-    return idx, float(allc[idx].item()), owner
+    (global index, cost, owner rank) as Python numbers; identical on every
+    rank (one host synchronisation)."""
+    cost, idx, owner = select_best_device(local_costs, global_batch, group).tolist()
+    return int(idx), float(cost), int(owner)
 
 
 def broadcast_best(local_coeffs, global_index, owner, global_batch, group=None):

@@ -38,13 +38,26 @@ def _worker(rank, world, port, global_batch, result_q):
     sys.path.insert(0, REPO)
     import torch.distributed as dist
     from mav_tube_trajectory_generation_amd.shard import (broadcast_best, select_best,
-                                                          shard_range)
+                                                          select_best_device, shard_range)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     start, count = shard_range(global_batch, world, rank)
     costs, coeffs = _solve_shard(range(105 + start, 105 + start + count))
     idx, cost, owner = select_best(torch.from_numpy(costs), global_batch)
     best = broadcast_best(torch.from_numpy(coeffs), idx, owner, global_batch)
-    result_q.put((rank, idx, cost, owner, best.numpy()))
+    # Device-side path (no host sync): the same triple as a tensor.
+    dev_triple = select_best_device(torch.from_numpy(costs), global_batch).tolist()
+    # NaN never wins, ties go to the lowest global index, an all-NaN batch
+    # selects index 0 (single-process argmin semantics).
+    nan_costs = costs.copy()
+    nan_costs[:] = np.nan
+    all_nan = select_best_device(torch.from_numpy(nan_costs), global_batch).tolist()
+    tie = np.full_like(costs, 7.0)
+    if rank == world - 1:
+        tie[-1] = np.nan
+    ties = select_best_device(torch.from_numpy(tie), global_batch).tolist()
+    # An empty shard (global batch smaller than the world) never wins.
+    tiny = select_best_device(torch.tensor([3.0] if rank == 0 else []), 1).tolist()
+    result_q.put((rank, idx, cost, owner, best.numpy(), dev_triple, all_nan, ties, tiny))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -71,7 +84,11 @@ def test_sharded_selection_matches_single_process(world, global_batch):
         assert p.exitcode == 0
     costs, coeffs = _solve_shard(range(105, 105 + global_batch))
     want = int(np.argmin(costs))
-    for rank, idx, cost, owner, best in results:
+    for rank, idx, cost, owner, best, dev_triple, all_nan, ties, tiny in results:
         assert idx == want
         assert cost == costs[want]
         assert np.array_equal(best, coeffs[want])
+        assert dev_triple == [costs[want], float(want), float(owner)]
+        assert all_nan[1:] == [0.0, 0.0]
+        assert ties == [7.0, 0.0, 0.0]
+        assert tiny == [3.0, 0.0, 0.0]

@@ -12,13 +12,21 @@ torch = pytest.importorskip("torch")
 N, D, R = 10, 3, 4
 
 
+@pytest.fixture(params=["auto", "generic"])
+def kernel(request):
+    """Every case runs with the kernel AUTO selects (time_*_std_kernel on the
+    standard pattern) and with the generic time_cost_kernel /
+    time_optimize_kernel forced."""
+    return request.param
+
+
 def _batch(S, B, seed0):
     import mav_tube_trajectory_generation_amd as mtg
     return mtg.generate_random_problems(N, D, S, B, seed0=seed0)
 
 
 @pytest.mark.parametrize("grad_mode", [0, 1, 2])
-def test_time_cost_vs_oracle(ctx, dev, oracle, grad_mode):
+def test_time_cost_vs_oracle(ctx, dev, oracle, grad_mode, kernel):
     """objectiveFunctionTime (nonlinear_impl:877-945) with the gradient forms
     of getCostAndGradientTime (:2495-2584)."""
     import mav_tube_trajectory_generation_amd as mtg
@@ -26,7 +34,7 @@ def test_time_cost_vs_oracle(ctx, dev, oracle, grad_mode):
     mask, fixed, times, _ = _batch(S, B, 500)
     times[3, 2] = 0.1   # exercise the clamp rule (nonlinear_impl:2529-2530)
     times[5, 0] = 0.07
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
     out = plan.time_cost(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev),
                          grad_mode=grad_mode, increment=0.1, w_d=0.1, w_t=1.0)
     cost = out["cost"].cpu().numpy()
@@ -87,11 +95,11 @@ def _grad_mode1_segmentwise(oracle, v, t, inc, w_d, w_t):
     return g
 
 
-def test_time_optimize_vs_reference_driver(ctx, dev, oracle):
+def test_time_optimize_vs_reference_driver(ctx, dev, oracle, kernel):
     import mav_tube_trajectory_generation_amd as mtg
     S, B, E = 6, 8, 20
     mask, fixed, times, _ = _batch(S, B, 900)
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
     out = plan.time_optimize(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev),
                              max_evals=E)
     T = out["times"].cpu().numpy()
@@ -107,13 +115,13 @@ def test_time_optimize_vs_reference_driver(ctx, dev, oracle):
         assert ec == evals[b] and np.max(np.abs(T[b] - Tc) / Tc) <= 1e-6, b
 
 
-def test_time_optimize_properties(ctx, dev, oracle):
+def test_time_optimize_properties(ctx, dev, oracle, kernel):
     """BASELINE config 5 shape (reduced batch): 50 evaluations, bounds
     [0.1, 2 T0] (nonlinear_impl:350-378), monotone objective."""
     import mav_tube_trajectory_generation_amd as mtg
     S, B = 10, 256
     mask, fixed, times, _ = _batch(S, B, 105)
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
     fd = torch.from_numpy(fixed).to(dev)
     td = torch.from_numpy(times).to(dev)
     c0 = plan.time_cost(fd, td)["cost"].cpu().numpy()
@@ -140,13 +148,13 @@ def _soft_limits(oracle, v, t):
 
 
 @pytest.mark.parametrize("grad_mode", [0, 2])
-def test_time_cost_soft_constraints_vs_oracle(ctx, dev, oracle, grad_mode):
+def test_time_cost_soft_constraints_vs_oracle(ctx, dev, oracle, grad_mode, kernel):
     """objectiveFunctionTime with use_soft_constraints (nonlinear_impl:907-913):
     J + sum_c min(1e12, exp((max_c - lim_c) / lim_c * 100))."""
     import mav_tube_trajectory_generation_amd as mtg
     S, B = 8, 8
     mask, fixed, times, _ = _batch(S, B, 540)
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
     fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
     for b in range(B):
         v = standard_vertices(N, S, D, 540 + b)
@@ -161,13 +169,13 @@ def test_time_cost_soft_constraints_vs_oracle(ctx, dev, oracle, grad_mode):
             assert np.max(np.abs(gg - g)) <= 1e-6 * np.max(np.abs(g)) + 1e-9, (b, gg, g)
 
 
-def test_time_optimize_soft_constraints_vs_oracle(ctx, dev, oracle):
+def test_time_optimize_soft_constraints_vs_oracle(ctx, dev, oracle, kernel):
     """The device optimiser on the soft-constrained objective takes the same
     steps as the oracle port (orc_time_optimize_soft)."""
     import mav_tube_trajectory_generation_amd as mtg
     S, B, E = 6, 6, 20
     mask, fixed, times, _ = _batch(S, B, 940)
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
     fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
     agree = 0
     for b in range(B):
@@ -187,12 +195,12 @@ def test_time_optimize_soft_constraints_vs_oracle(ctx, dev, oracle):
     assert agree >= B - 1
 
 
-def test_time_soft_rejects_bad_constraints(ctx, dev):
+def test_time_soft_rejects_bad_constraints(ctx, dev, kernel):
     import mav_tube_trajectory_generation_amd as mtg
     from mav_tube_trajectory_generation_amd._abi import MTGError
     S = 4
     mask, fixed, times, _ = _batch(S, 1, 5)
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
     fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
     for soft in ([(5, 1.0)], [(1, 0.0)], [(-1, 1.0)], [(1, 1.0)] * 9):
         with pytest.raises(MTGError):
