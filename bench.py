@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=5)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph)")
+    p.add_argument("--kernel", default="auto",
+                   choices=["auto", "generic", "standard", "lane"],
+                   help="linear-solve kernel (mtg_plan_set_kernel); auto picks by batch size")
     p.add_argument("--soft", action="store_true",
                    help="time workload: soft constraints max|v| <= 3, max|a| <= 5 in the objective")
     return p.parse_args()
@@ -258,7 +261,7 @@ def main():
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
     mask, fixed, times, pos = mtg.generate_random_problems(N, D, S, B, seed0=seed0)
     ctx = mtg.Context(local_rank)
-    plan = mtg.LinearPlan(ctx, N, D, r, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, r, S, mask).set_kernel(args.kernel)
     fixed_d = torch.from_numpy(fixed).to(dev)
     times_d = torch.from_numpy(times).to(dev)
     nf = plan.n_fixed
@@ -500,6 +503,7 @@ def main():
                                sample_args=(0.01, 4) if wl == "sample" else None)
             cpu["unit"] = unit
         cfg = {"workload": config_name(wl, B, world, S), "global_batch": global_batch,
+               "kernel": plan.kernel_for_batch(B) if wl == "linear" else None,
                "batch_per_gpu": B, "segments": S, "N": N, "D": D, "r": r,
                "parallelism": f"shard{world}"}
         if useful_per_step is not None:

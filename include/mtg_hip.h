@@ -87,16 +87,28 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S,
                     mtg_plan** out);
 int mtg_plan_destroy(mtg_plan* plan);
 /* Kernel selection for mtg_linear_solve.  AUTO (default) runs the
- * standard-pattern kernel when the pattern is the reference's standard one
+ * standard-pattern kernels when the pattern is the reference's standard one
  * (start and end vertex fully fixed, intermediate vertices position only:
  * createRandomVertices / makeStartOrEnd, vertex.cpp:27-82, 147-153) and
- * 2 <= S <= 64, else the generic kernel.  GENERIC forces the generic kernel
- * (parity cross-checks); STANDARD fails with MTG_ERR_UNSUPPORTED on other
- * patterns.  mtg_plan_kernel returns the kernel a solve will run
- * (GENERIC or STANDARD). */
-enum { MTG_KERNEL_AUTO = 0, MTG_KERNEL_GENERIC = 1, MTG_KERNEL_STANDARD = 2 };
+ * 2 <= S <= 64, else the generic kernel.  Among the standard-pattern kernels
+ * it picks by batch size: STANDARD (one wavefront per trajectory, lowest
+ * latency) below 4096 trajectories, LANE (one (trajectory, dimension) per
+ * lane, highest throughput) from 4096; LANE covers N = 10, r = 4, D = 3,
+ * 2 <= S <= 12.  GENERIC forces the generic kernel (parity cross-checks);
+ * STANDARD / LANE fail with MTG_ERR_UNSUPPORTED where they do not apply.
+ * mtg_plan_kernel returns the forced kernel, or for AUTO the wavefront
+ * kernel (GENERIC or STANDARD); mtg_plan_kernel_for_batch the kernel a
+ * solve of B trajectories runs.  The time, free-derivative and sampling
+ * entry points treat LANE like STANDARD. */
+enum {
+  MTG_KERNEL_AUTO = 0,
+  MTG_KERNEL_GENERIC = 1,
+  MTG_KERNEL_STANDARD = 2,
+  MTG_KERNEL_LANE = 3
+};
 int mtg_plan_set_kernel(mtg_plan* plan, int kernel);
 int mtg_plan_kernel(const mtg_plan* plan);
+int mtg_plan_kernel_for_batch(const mtg_plan* plan, int64_t B);
 
 /* n_fixed / n_free per dimension (getNumberFixedConstraints /
  * getNumberFreeConstraints, polynomial_optimization_linear.h:224-226). */

@@ -75,20 +75,30 @@ class LinearPlan:
         check(lib().mtg_plan_counts(self._h, ctypes.byref(nf), ctypes.byref(np_)), "counts")
         self.n_fixed, self.n_free = nf.value, np_.value
 
-    KERNELS = {"auto": 0, "generic": 1, "standard": 2}
+    KERNELS = {"auto": 0, "generic": 1, "standard": 2, "lane": 3}
+    _NAMES = {v: k for k, v in KERNELS.items()}
 
     def set_kernel(self, which):
-        """Select the linear-solve kernel: "auto" (default), "generic", or
-        "standard" (the standard-pattern kernel; MTGError on other patterns)."""
+        """Select the linear-solve kernel: "auto" (default), "generic",
+        "standard" (one wavefront per trajectory) or "lane" (one
+        (trajectory, dimension) per lane); MTGError where the pattern or
+        sizes do not allow it."""
         check(lib().mtg_plan_set_kernel(self._h, self.KERNELS[which]), "mtg_plan_set_kernel")
         return self
 
     @property
     def kernel(self):
-        """Kernel a solve runs: "generic" or "standard"."""
+        """The forced kernel, or for "auto" the wavefront kernel ("generic" or
+        "standard"); see kernel_for_batch."""
         k = lib().mtg_plan_kernel(self._h)
         check(min(k, 0), "mtg_plan_kernel")
-        return {1: "generic", 2: "standard"}[k]
+        return self._NAMES[k]
+
+    def kernel_for_batch(self, B):
+        """Kernel a solve of B trajectories runs."""
+        k = lib().mtg_plan_kernel_for_batch(self._h, B)
+        check(min(k, 0), "mtg_plan_kernel_for_batch")
+        return self._NAMES[k]
 
     def close(self):
         if self._h:

@@ -273,16 +273,27 @@ int mtg_plan_destroy(mtg_plan* plan) {
 }
 
 int mtg_plan_set_kernel(mtg_plan* plan, int kernel) {
-  if (!plan || kernel < MTG_KERNEL_AUTO || kernel > MTG_KERNEL_STANDARD)
+  if (!plan || kernel < MTG_KERNEL_AUTO || kernel > MTG_KERNEL_LANE)
     return MTG_ERR_INVALID_ARG;
   if (kernel == MTG_KERNEL_STANDARD && !plan->dev.std_pattern) return MTG_ERR_UNSUPPORTED;
+  if (kernel >= MTG_KERNEL_LANE) {
+    mtg::PlanDev probe = plan->dev;
+    probe.kernel = MTG_KERNEL_AUTO;
+    if (!mtg::has_linear_lane(probe)) return MTG_ERR_UNSUPPORTED;
+  }
   plan->dev.kernel = kernel;
   return MTG_OK;
 }
 
 int mtg_plan_kernel(const mtg_plan* plan) {
   if (!plan) return MTG_ERR_INVALID_ARG;
+  if (plan->dev.kernel >= MTG_KERNEL_LANE) return plan->dev.kernel;
   return mtg::use_std_kernel(plan->dev) ? MTG_KERNEL_STANDARD : MTG_KERNEL_GENERIC;
+}
+
+int mtg_plan_kernel_for_batch(const mtg_plan* plan, int64_t B) {
+  if (!plan || B < 0) return MTG_ERR_INVALID_ARG;
+  return mtg::linear_kernel_for_batch(plan->dev, B);
 }
 
 int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free) {

@@ -28,6 +28,17 @@ struct PlanDev {
 
 // Standard-pattern linear solve (mtg_linear_std.hip).
 constexpr int kMaxStdS = 64;
+// Lane linear solve for large batches (mtg_linear_lane.hip): one
+// (trajectory, dimension) per lane; standard pattern, N = 10, r = 4, D = 3,
+// 2 <= S <= kMaxLaneS.  AUTO runs it from kLaneMinBatch trajectories.
+constexpr int kMaxLaneS = 12;
+constexpr int64_t kLaneMinBatch = 4096;
+struct PlanDev;
+bool has_linear_lane(const PlanDev& pl);
+hipError_t launch_linear_solve_lane(const PlanDev& pl, int64_t B, const double* df,
+                                    const double* times, double* coeffs, double* cost,
+                                    double* free_vals, int32_t* status, hipStream_t st);
+int linear_kernel_for_batch(const PlanDev& pl, int64_t B);
 hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
                                    const double* times, double* coeffs, double* cost,
                                    double* free_vals, int32_t* status, hipStream_t st);

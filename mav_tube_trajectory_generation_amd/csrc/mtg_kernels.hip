@@ -467,9 +467,19 @@ static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* 
     default: return hipErrorInvalidValue; \
   }
 
+int linear_kernel_for_batch(const PlanDev& pl, int64_t B) {
+  if (pl.kernel != MTG_KERNEL_AUTO) return pl.kernel;
+  if (!pl.std_pattern) return MTG_KERNEL_GENERIC;
+  if (has_linear_lane(pl) && B >= kLaneMinBatch) return MTG_KERNEL_LANE;
+  return MTG_KERNEL_STANDARD;
+}
+
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,
                                double* free_vals, int32_t* status, hipStream_t st) {
+  const int k = linear_kernel_for_batch(pl, B);
+  if (k == MTG_KERNEL_LANE)
+    return launch_linear_solve_lane(pl, B, df, times, coeffs, cost, free_vals, status, st);
   if (use_std_kernel(pl))
     return launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st);
 #define CALL(n) launch_linear_n<n>(pl, B, df, times, coeffs, cost, free_vals, status, st)

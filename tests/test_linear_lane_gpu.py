@@ -1,0 +1,85 @@
+"""The lane linear kernel (mtg_linear_lane.hip, LANE: one (trajectory,
+dimension) per lane) against the wavefront standard-pattern kernel and the
+oracle, and AUTO's choice by batch size."""
+import numpy as np
+import pytest
+
+from helpers import REL_TOL, rel_err, rel_err_coeffs, standard_vertices
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+N, D, R = 10, 3, 4
+
+
+def _solve(ctx, dev, mask, fixed, times, kernel):
+    import mav_tube_trajectory_generation_amd as mtg
+    S = times.shape[1]
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
+    out = plan.solve(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev), free=True)
+    torch.cuda.synchronize()
+    return plan, {k: v.cpu().numpy() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("kernel", ["lane"])
+@pytest.mark.parametrize("S", [2, 3, 4, 7, 10, 12])
+def test_lane_kernels_match_wavefront_kernel(ctx, dev, oracle, kernel, S):
+    """Same inputs as the wavefront kernel, a batch that is not a multiple of
+    the trajectories per wavefront (21): coefficients, d_p and cost to
+    1e-9 (different elimination order: block Thomas vs twisted), oracle spot
+    checks at the 1e-6 parity bar."""
+    import mav_tube_trajectory_generation_amd as mtg
+    B = 203
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=2000 + S)
+    plan, out = _solve(ctx, dev, mask, fixed, times, kernel)
+    assert plan.kernel == kernel
+    _, ref = _solve(ctx, dev, mask, fixed, times, "standard")
+    assert (out["status"] == 0).all()
+    for b in range(B):
+        assert rel_err_coeffs(out["coeffs"][b], ref["coeffs"][b]) <= 1e-9, b
+        assert rel_err_coeffs(out["free"][b], ref["free"][b]) <= 1e-9, b
+        assert rel_err(out["cost"][b], ref["cost"][b]) <= 1e-8, b
+    for b in (0, 101, B - 1):
+        o = oracle.linear_solve(N, R, standard_vertices(N, S, D, 2000 + S + b), times[b])
+        assert rel_err_coeffs(out["coeffs"][b], o["coeffs"]) <= REL_TOL, b
+        assert rel_err(out["cost"][b], o["cost"]) <= REL_TOL, b
+
+
+@pytest.mark.parametrize("kernel", ["lane"])
+def test_lane_kernels_bad_time(ctx, dev, kernel):
+    import mav_tube_trajectory_generation_amd as mtg
+    S, B = 5, 70
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=31)
+    times[3, 1] = 0.0
+    times[64, 4] = -2.0
+    times[65, 0] = np.inf
+    _, out = _solve(ctx, dev, mask, fixed, times, kernel)
+    bad = {3, 64, 65}
+    for b in range(B):
+        if b in bad:
+            assert out["status"][b] == 1 and np.isnan(out["cost"][b])
+            assert np.isnan(out["coeffs"][b]).all()
+        else:
+            assert out["status"][b] == 0 and np.isfinite(out["cost"][b])
+
+
+def test_auto_selection_by_batch(ctx):
+    import mav_tube_trajectory_generation_amd as mtg
+    S = 10
+    mask, _, _, _ = mtg.generate_random_problems(N, D, S, 1, seed0=1)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    assert plan.kernel == "standard"
+    assert plan.kernel_for_batch(1024) == "standard"
+    assert plan.kernel_for_batch(4095) == "standard"
+    assert plan.kernel_for_batch(4096) == "lane"
+    assert plan.kernel_for_batch(65536) == "lane"
+    assert plan.set_kernel("standard").kernel_for_batch(65536) == "standard"
+    # outside the lane kernels' instantiations: the wavefront kernel
+    p2 = mtg.LinearPlan(ctx, N, 2, R, S, mask)
+    assert p2.kernel_for_batch(65536) == "standard"
+    with pytest.raises(mtg.MTGError):
+        p2.set_kernel("lane")
+    m20, _, _, _ = mtg.generate_random_problems(N, D, 20, 1, seed0=1)
+    p3 = mtg.LinearPlan(ctx, N, D, R, 20, m20)
+    assert p3.kernel_for_batch(65536) == "standard"
