@@ -220,15 +220,19 @@ class PolynomialOptimizationNonLinear {
     return freeCost(segment_times, free_constraints, 1, nullptr);
   }
 
-  // Runs the optimisation: kOptimizeTime, or kOptimizeFreeConstraints
-  // (optimizeFreeConstraints, nonlinear_impl:399-493, on the device).
-  // Returns a positive NLopt-style success code or a negative failure code.
+  // Runs the optimisation: kOptimizeTime, kOptimizeFreeConstraints
+  // (optimizeFreeConstraints, nonlinear_impl:399-493) or
+  // kOptimizeFreeConstraintsAndTime (optimizeTimeAndFreeConstraints,
+  // :610-706), each on the device.  Returns a positive NLopt-style success
+  // code or a negative failure code.
   int optimize() {
     if (params_.objective == NonlinearOptimizationParameters::kOptimizeFreeConstraints)
       return optimizeFreeConstraints();
+    if (params_.objective == NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndTime)
+      return optimizeTimeAndFreeConstraints();
     MTG_CHECK(params_.objective == NonlinearOptimizationParameters::kOptimizeTime,
-              "objective not part of this build: kOptimizeTime and kOptimizeFreeConstraints "
-              "(SURVEY.md 8a T1-T6, 8f rank 2)");
+              "objective not part of this build: kOptimizeTime, kOptimizeFreeConstraints and "
+              "kOptimizeFreeConstraintsAndTime (SURVEY.md 8a T1-T6, 8f rank 2)");
     warnCollision();
     if (params_.solve_time_with_qcqp) return optimizeTimeQCQP();
     const auto t0 = std::chrono::steady_clock::now();
@@ -457,6 +461,59 @@ class PolynomialOptimizationNonLinear {
     optimization_info_.cost_trajectory = 2.0 * poly_opt_.computeCost();  // J_d
     optimization_info_.cost_soft_constraints =
         soft_.empty() ? 0.0 : J - optimization_info_.cost_trajectory;
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
+    optimization_info_.optimization_time =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    free_optimized_ = true;
+    return optimization_info_.stopping_reason;
+  }
+
+  // optimizeTimeAndFreeConstraints (nonlinear_impl:610-706): initial
+  // solution from the tube QCQP (:617-622), x = [T; d_p] with the bounds of
+  // :660-677, then the device optimiser of mtg_time_free_optimize in place of
+  // NLopt (max_iterations objective evaluations of
+  // objectiveFunctionTimeAndConstraints, :947-1019).
+  int optimizeTimeAndFreeConstraints() {
+    warnCollision();
+    const auto t0 = std::chrono::steady_clock::now();
+    poly_opt_.solveQCQP();
+    poly_opt_.getTrajectory(&trajectory_initial_);
+    std::vector<VectorXd> free;
+    poly_opt_.getFreeConstraints(&free);
+    MTG_CHECK(!free.empty() && free.front().size() > 0, "no free constraints (:619-621)");
+    const std::vector<double> x0 = packFree(free);
+    std::vector<double> times = segmentTimesOfQcqp();
+    const size_t np = poly_opt_.getNumberFreeConstraints();
+    internal::DeviceBuffer<double> d_df, d_dp, d_t, d_cost(1);
+    internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
+    d_df.upload(packFixedQcqp());
+    d_dp.upload(x0);
+    d_t.upload(times);
+    const mtg_time_params p = timeParams(0);
+    const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
+    internal::checkStatus(mtg_time_free_optimize(poly_opt_.getPlan(), 1, d_df.get(), d_dp.get(),
+                                                 d_t.get(), &p, budget, d_cost.get(), d_ev.get(),
+                                                 d_st.get(), nullptr),
+                          "mtg_time_free_optimize");
+    internal::synchronize();
+    const std::vector<double> x = d_dp.download();
+    d_t.download(times.data(), times.size());
+    for (size_t d = 0; d < dimension_; ++d)
+      for (size_t i = 0; i < np; ++i) free[d][i] = x[d * np + i];
+    poly_opt_.updateSegmentTimes(times);
+    poly_opt_.setFreeConstraints(free);
+    int32_t evals = 0, st = 0;
+    d_ev.download(&evals, 1);
+    d_st.download(&st, 1);
+    double J = 0.0, tot = 0.0;
+    d_cost.download(&J, 1);
+    for (double t : times) tot += t;
+    optimization_info_.n_iterations = evals;
+    optimization_info_.cost_trajectory = poly_opt_.computeCost();
+    optimization_info_.cost_time = tot * tot * params_.time_penalty;
+    optimization_info_.cost_soft_constraints =
+        soft_.empty() ? 0.0
+                      : J - optimization_info_.cost_trajectory - optimization_info_.cost_time;
     optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
     optimization_info_.optimization_time =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

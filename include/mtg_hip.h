@@ -259,6 +259,26 @@ int mtg_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       const double* upper, const mtg_time_params* params, int max_evals,
                       double* cost, int32_t* evals, int32_t* status, void* stream);
 
+/* Batched optimisation over segment times AND free derivatives
+ * (optimizeTimeAndFreeConstraints, nonlinear_impl:610-706, objective mode 1
+ * of mtg_free_cost = objectiveFunctionTimeAndConstraints, :947-1019) with
+ * the reference's bounds T in [0.1, 2 |T0|], d_p in [-2 |d0|, 2 |d0|]
+ * (:660-677).  NLopt's SBPLX is not available; the device optimiser
+ * alternates projected steps, each trial one counted evaluation: a scaled
+ * steepest-descent step in T (central-difference gradient in T with d_p held,
+ * step params->increment, clamp rule of :2529-2530, not counted) and a
+ * Newton step of the quadratic J in d_p toward the linear solve at the
+ * current T; step sizes x1.5 (capped at 1) on a decrease of J, x0.5
+ * otherwise (T starts at 0.1, d_p at 1); stops at `max_evals` evaluations,
+ * both steps below 1e-9, or a round in which neither moves.
+ *   free_io   B x D x n_free   in: d0 (the start solution), out: optimised d_p
+ *   times_io  B x S            in: T0, out: optimised times
+ *   cost B, evals B, status B (nullable) */
+int mtg_time_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                           double* free_io, double* times_io, const mtg_time_params* params,
+                           int max_evals, double* cost, int32_t* evals, int32_t* status,
+                           void* stream);
+
 /* ------------------------------------------------------------------------
  * Tube QCQP (PolynomialOptimizationConstrained<N>, qcqp_impl).  The tube
  * pattern is fixed by the reference: start and end vertices fully fixed

@@ -63,6 +63,9 @@ SIGNATURES = {
     "mtg_free_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp,
                                          ctypes.POINTER(TimeParams), ctypes.c_int, _vp, _vp,
                                          _vp, _vp]),
+    "mtg_time_free_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp,
+                                              ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
+                                              _vp, _vp, _vp]),
     "mtg_plan_kernel": (ctypes.c_int, [_vp]),
     "mtg_plan_kernel_for_batch": (ctypes.c_int, [_vp, ctypes.c_int64]),
     "mtg_linear_solve": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -241,6 +241,28 @@ class LinearPlan:
               "mtg_free_optimize")
         return dict(free=d, cost=cost, evals=evals, status=status)
 
+    def time_free_optimize(self, fixed_vals, free_vals, times, max_evals=50, time_penalty=500.0,
+                           increment=0.1, soft=None, soft_weight=100.0):
+        """Optimise segment times and free derivatives together
+        (mtg_time_free_optimize, optimizeTimeAndFreeConstraints) on copies;
+        returns dict(times, free, cost, evals, status)."""
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        _require(free_vals, (B, self.D, self.n_free), "free_vals")
+        dev = times.device
+        t = times.clone()
+        d = free_vals.clone()
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        evals = torch.empty(B, dtype=torch.int32, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        p = make_time_params(time_penalty, increment, 0.1, 1.0, 0, soft, soft_weight)
+        check(lib().mtg_time_free_optimize(self._h, B, _ptr(fixed_vals), _ptr(d), _ptr(t),
+                                           ctypes.byref(p), max_evals, _ptr(cost), _ptr(evals),
+                                           _ptr(status), _stream(dev)), "mtg_time_free_optimize")
+        return dict(times=t, free=d, cost=cost, evals=evals, status=status)
+
     # -- host (numpy) API ---------------------------------------------------
     def solve_host(self, fixed_vals, times):
         fixed_vals = np.ascontiguousarray(fixed_vals, dtype=np.float64)

@@ -15,6 +15,9 @@
 //
 // free_optimize_kernel: the device optimiser of mtg_free_optimize on the
 // mode-0 objective (oracle restatement: orc_free_optimize).
+// time_free_optimize_kernel: the device optimiser of mtg_time_free_optimize
+// over [T; d_p] on the mode-1 objective (optimizeTimeAndFreeConstraints,
+// nonlinear_impl:610-706; oracle restatement: orc_time_free_optimize).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -28,7 +31,7 @@ namespace mtg {
 namespace {
 
 // LDS after the generic layout: [cbuf S*D*N (kSoft)] [gv (S+1)*M*D]
-// [free-optimiser state 3*D*np].
+// [free-optimiser state 3*D*np] [time state 4*S (time_free_optimize)].
 struct FreeLds {
   size_t cbuf, gv, opt, bytes;
 };
@@ -43,6 +46,7 @@ __host__ __device__ inline FreeLds free_lds(int N, int S, int D, int np, bool so
   o += sizeof(double) * (S + 1) * (N / 2) * D;
   f.opt = o;
   o += sizeof(double) * 3 * D * (np > 0 ? np : 1);
+  o += sizeof(double) * 4 * S;
   f.bytes = o;
   return f;
 }
@@ -257,6 +261,208 @@ __global__ __launch_bounds__(kWave) void free_optimize_kernel(
   }
 }
 
+// Device optimiser of the kOptimizeFreeConstraintsAndTime objective (mode 1,
+// objectiveFunctionTimeAndConstraints, nonlinear_impl:947-1019) over
+// x = [T; d_p] with the reference's bounds (optimizeTimeAndFreeConstraints,
+// nonlinear_impl:610-706): T in [0.1, 2 |T0|], d_p in [-2 |d0|, 2 |d0|].
+// NLopt's SBPLX is replaced by block-alternating projected steps, each trial
+// one counted evaluation (NLopt maxeval, :101):
+//   T block: scaled steepest descent, T' = clamp(T - aT T0 (g T0) / max|g T0|),
+//     g = central differences of J in T with d_p held (step `increment`,
+//     clamp rule of :2529-2530; not counted, as the time optimiser's);
+//   d block: Newton step of the quadratic J in d_p toward d* = argmin_d J at
+//     the current T (the linear solve), d' = clamp(d + ad (d* - d));
+//   a step size grows x1.5 (capped at 1) on a decrease of J and halves
+//   otherwise (aT starts at initial_stepsize_rel = 0.1, ad at 1).
+// The round repeats (gradient only after an accepted step) until max_evals
+// evaluations, both step sizes below 1e-9, or a round in which neither trial
+// moves.  A state machine with one objective call site.
+template <int N, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_free_optimize_kernel(
+    PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ free_io,
+    double* __restrict__ times_io, mtg_time_params p, int max_evals, double* __restrict__ cost,
+    int32_t* __restrict__ evals_out, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf, np = pl.np, n = D * np;
+  const Layout lay = make_layout(N, S, D);
+  const FreeLds fl = free_lds(N, S, D, np, kSoft);
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
+  const int64_t b = blockIdx.x;
+  double* cbuf = lds_at<double>(smem, fl.cbuf);
+  double* dstar = lds_at<double>(smem, fl.opt);  // [d][p]
+  double* dcur = dstar + (n > 0 ? n : 1);
+  double* dtry = dcur + (n > 0 ? n : 1);
+  double* Tcur = dtry + (n > 0 ? n : 1);
+  double* T0 = Tcur + S;
+  double* Ttry = T0 + S;
+  double* g = Ttry + S;
+  const bool bad = free_setup(t, pl, fixed_vals + b * D * nf, nullptr, times_io + b * S);
+  int evals = 0;
+  double f = NAN;
+  bool not_spd = false;
+  auto slot_of = [&](int i) { return pl.free_map[i % np] * D + i / np; };
+  if (!bad) {
+    for (int i = t.lane; i < S; i += kWave) Tcur[i] = T0[i] = t.T()[i];
+    for (int i = t.lane; i < n; i += kWave) {
+      const double d0 = free_io[b * n + i];
+      dcur[i] = d0;
+      t.dv()[slot_of(i)] = d0;
+    }
+    __syncthreads();
+    constexpr double kLower = 0.1;  // nonlinear_impl:675-677
+    enum { kBase, kGrad, kTTrial, kDTrial };               // evaluation kinds
+    enum { kEval, kDone, kRound, kTStep, kDStep, kEnd };  // transitions
+    int phase = kBase, gi = 0;
+    double aT = 0.1, ad = 1.0, Jlo = 0.0;
+    bool stale = true, dstar_ok = false, moved_round = false;
+    // Evaluation point: times src (powers recomputed), free values dsrc.
+    auto set_point = [&](const double* src, const double* dsrc) {
+      for (int i = t.lane; i < S; i += kWave) t.T()[i] = src[i];
+      for (int i = t.lane; i < n; i += kWave) t.dv()[slot_of(i)] = dsrc[i];
+      __syncthreads();
+      t.compute_powers();
+      __syncthreads();
+    };
+    for (;;) {
+      const double J = free_objective<N, kSoft>(t, pl.tab, p, 1, cbuf);
+      int go;
+      if (phase == kBase) {
+        f = J;
+        evals = 1;
+        go = kRound;
+      } else if (phase == kGrad) {
+        if (gi & 1) {
+          if (t.lane == 0) g[gi >> 1] = (J - Jlo) / (2.0 * p.increment);
+        } else {
+          Jlo = J;
+        }
+        ++gi;
+        go = gi < 2 * S ? kEval : kTStep;
+      } else if (phase == kTTrial) {
+        ++evals;
+        if (J < f) {
+          f = J;
+          for (int i = t.lane; i < S; i += kWave) Tcur[i] = Ttry[i];
+          aT = fmin(aT * 1.5, 1.0);
+          stale = true;
+          dstar_ok = false;
+        } else {
+          aT *= 0.5;
+        }
+        go = kDStep;
+      } else {  // kDTrial
+        ++evals;
+        if (J < f) {
+          f = J;
+          for (int i = t.lane; i < n; i += kWave) dcur[i] = dtry[i];
+          ad = fmin(ad * 1.5, 1.0);
+          stale = true;
+        } else {
+          ad *= 0.5;
+        }
+        go = kEnd;
+      }
+      __syncthreads();
+      while (go != kEval && go != kDone) {
+        if (go == kRound) {
+          moved_round = false;
+          if (stale) {
+            stale = false;
+            phase = kGrad;
+            gi = 0;
+            go = kEval;
+          } else {
+            go = kTStep;
+          }
+        } else if (go == kTStep) {
+          go = kDStep;
+          if (!(evals < max_evals)) {
+            go = kDone;
+          } else if (aT > 1e-9) {
+            double gmax = 0.0;
+            for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(g[i] * T0[i]));
+            bool moved = false;
+            if (gmax > 0.0) {
+              for (int i = 0; i < S; ++i) {
+                double tn = Tcur[i] - aT * T0[i] * (g[i] * T0[i]) / gmax;
+                tn = fmin(fmax(tn, kLower), 2.0 * fabs(T0[i]));
+                moved = moved || tn != Tcur[i];
+                if (t.lane == 0) Ttry[i] = tn;
+              }
+            }
+            __syncthreads();
+            if (moved) {
+              moved_round = true;
+              phase = kTTrial;
+              go = kEval;
+            }
+          }
+        } else if (go == kDStep) {
+          go = kEnd;
+          if (!(evals < max_evals)) {
+            go = kDone;
+          } else if (ad > 1e-9) {
+            if (!dstar_ok) {
+              // d* = argmin_d J at Tcur (solveLinear, linear_impl:337-379).
+              set_point(Tcur, dcur);
+              t.clear_free();  // assemble() sums over dv with free entries zero
+              __syncthreads();
+              t.solve();
+              not_spd = not_spd || (t.flag()[0] & 2) != 0;
+              for (int i = t.lane; i < n; i += kWave) dstar[i] = t.dv()[slot_of(i)];
+              __syncthreads();
+              dstar_ok = true;
+            }
+            bool moved = false;
+            for (int i = t.lane; i < n; i += kWave) {
+              const double d = dcur[i];
+              const double bnd = 2.0 * fabs(free_io[b * n + i]);  // nonlinear_impl:665-668
+              double x = __dadd_rn(d, __dmul_rn(ad, __dsub_rn(dstar[i], d)));
+              x = fmin(fmax(x, -bnd), bnd);
+              dtry[i] = x;
+              moved = moved || fabs(x - d) > 1e-13 * (1.0 + fabs(d));
+            }
+            __syncthreads();
+            if (__any(moved)) {
+              moved_round = true;
+              phase = kDTrial;
+              go = kEval;
+            }
+          }
+        } else {  // kEnd
+          go = (evals < max_evals && moved_round) ? kRound : kDone;
+        }
+      }
+      if (go == kDone) break;
+      // Load the evaluation point of `phase`.
+      if (phase == kGrad) {
+        const int nn = gi >> 1;
+        for (int i = t.lane; i < S; i += kWave) {
+          const double Tn = Tcur[i];
+          Ttry[i] = i != nn ? Tn
+                            : (Tn <= 0.1 ? 0.1 : ((gi & 1) ? Tn + p.increment : Tn - p.increment));
+        }
+        __syncthreads();
+        set_point(Ttry, dcur);
+      } else if (phase == kTTrial) {
+        set_point(Ttry, dcur);
+      } else {
+        set_point(Tcur, dtry);
+      }
+    }
+    __syncthreads();
+    for (int i = t.lane; i < S; i += kWave) times_io[b * S + i] = Tcur[i];
+    for (int i = t.lane; i < n; i += kWave) free_io[b * n + i] = dcur[i];
+  }
+  if (t.lane == 0) {
+    if (cost) cost[b] = f;
+    if (evals_out) evals_out[b] = evals;
+    if (status)
+      status[b] = bad ? MTG_TRAJ_BAD_TIME : (not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
+  }
+}
+
 namespace {
 template <typename K>
 hipError_t prepare_lds_free(K kernel, size_t bytes) {
@@ -311,6 +517,28 @@ hipError_t free_opt_n(const PlanDev& pl, int64_t B, const double* df, double* dp
 }
 }  // namespace
 
+template <int N>
+hipError_t time_free_opt_n(const PlanDev& pl, int64_t B, const double* df, double* dp,
+                           double* times, const mtg_time_params& p, int max_evals, double* cost,
+                           int32_t* evals, int32_t* status, hipStream_t st) {
+  const bool soft = p.n_soft > 0;
+  const size_t bytes = free_lds(N, pl.S, pl.D, pl.np, soft).bytes;
+  if (soft) {
+    hipError_t e = prepare_lds_free(time_free_optimize_kernel<N, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_free_optimize_kernel<N, true>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, dp, times, p, max_evals, cost, evals,
+                       status);
+  } else {
+    hipError_t e = prepare_lds_free(time_free_optimize_kernel<N, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_free_optimize_kernel<N, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, dp, times, p, max_evals, cost, evals,
+                       status);
+  }
+  return hipGetLastError();
+}
+
 size_t free_lds_bytes(int N, int S, int D, int np, bool soft) {
   return free_lds(N, S, D, np, soft).bytes;
 }
@@ -329,6 +557,13 @@ hipError_t launch_free_cost(const PlanDev& pl, int64_t B, const double* df, cons
                             const double* times, const mtg_time_params& p, int mode,
                             double* cost, double* grad, int32_t* status, hipStream_t st) {
   MTG_FREE_DISPATCH(free_cost_n, pl, B, df, dp, times, p, mode, cost, grad, status, st)
+}
+
+hipError_t launch_time_free_optimize(const PlanDev& pl, int64_t B, const double* df, double* dp,
+                                     double* times, const mtg_time_params& p, int max_evals,
+                                     double* cost, int32_t* evals, int32_t* status,
+                                     hipStream_t st) {
+  MTG_FREE_DISPATCH(time_free_opt_n, pl, B, df, dp, times, p, max_evals, cost, evals, status, st)
 }
 
 hipError_t launch_free_optimize(const PlanDev& pl, int64_t B, const double* df, double* dp,

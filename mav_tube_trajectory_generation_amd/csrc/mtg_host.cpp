@@ -467,6 +467,25 @@ int mtg_free_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                                         static_cast<hipStream_t>(stream)));
 }
 
+int mtg_time_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                           double* free_io, double* times_io, const mtg_time_params* params,
+                           int max_evals, double* cost, int32_t* evals, int32_t* status,
+                           void* stream) {
+  if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
+    return MTG_ERR_INVALID_ARG;
+  if ((plan->dev.nf > 0 && !fixed_vals) || plan->dev.np < 1 || !free_io)
+    return MTG_ERR_INVALID_ARG;
+  if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
+  if (!valid_soft(plan, params)) return MTG_ERR_INVALID_ARG;
+  if (mtg::free_lds_bytes(plan->dev.N, plan->dev.S, plan->dev.D, plan->dev.np,
+                          params->n_soft > 0) > static_cast<size_t>(mtg::kMaxLdsBytes))
+    return MTG_ERR_UNSUPPORTED;
+  if (B == 0) return MTG_OK;
+  return from_hip(mtg::launch_time_free_optimize(plan->dev, B, fixed_vals, free_io, times_io,
+                                                 *params, max_evals, cost, evals, status,
+                                                 static_cast<hipStream_t>(stream)));
+}
+
 int mtg_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       double* free_io, const double* times, const double* lower,
                       const double* upper, const mtg_time_params* params, int max_evals,

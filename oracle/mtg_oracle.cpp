@@ -2198,4 +2198,114 @@ int orc_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
   return 0;
 }
 
+// The mtg_time_free_optimize algorithm (time_free_optimize_kernel) restated on
+// the oracle objective: optimizeTimeAndFreeConstraints (nonlinear_impl:
+// 610-706) with objectiveFunctionTimeAndConstraints (:947-1019, mode 1 of
+// freeCostImpl), bounds T in [0.1, 2|T0|], d in [-2|d0|, 2|d0|] (:660-677);
+// block-alternating projected steps (see include/mtg_hip.h).  dp_io: D x np
+// (in d0, out optimised), times_io: S (in T0, out optimised).
+int orc_time_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, double* dp_io, double* times_io,
+                           double time_penalty, double increment, int n_soft,
+                           const int* soft_derivatives, const double* soft_limits,
+                           double soft_weight, double soft_maximum_cost, int max_evals,
+                           double* cost, int* evals) {
+  if (!dp_io || !times_io || max_evals < 1) return -1;
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times_io, &lp);
+  if (rc) return rc;
+  const int np = lp.np, n = D * np;
+  if (np < 1) return -1;
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  auto objective = [&](const std::vector<double>& t, const std::vector<double>& d) {
+    lp.updateSegmentTimes(t);
+    double J = 0.0;
+    freeCostImpl(lp, d.data(), 1, time_penalty, n_soft > 0 ? &soft : nullptr, &J, nullptr);
+    return J;
+  };
+  const std::vector<double> T0(times_io, times_io + S), d0(dp_io, dp_io + n);
+  std::vector<double> T = T0, d = d0, g(S), Ttry(S), dtry(n), dstar(n);
+  double f = objective(T, d);
+  int n_eval = 1;
+  double aT = 0.1, ad = 1.0;
+  bool stale = true, dstar_ok = false;
+  for (;;) {
+    bool moved_round = false;
+    if (stale) {
+      stale = false;
+      for (int k = 0; k < S; ++k) {
+        std::vector<double> ts = T, tb = T;
+        ts[k] = T[k] <= 0.1 ? 0.1 : T[k] - increment;
+        tb[k] = T[k] <= 0.1 ? 0.1 : T[k] + increment;
+        const double Js = objective(ts, d);
+        const double Jb = objective(tb, d);
+        g[k] = (Jb - Js) / (2.0 * increment);
+      }
+    }
+    if (!(n_eval < max_evals)) break;
+    if (aT > 1e-9) {  // T block
+      double gmax = 0.0;
+      for (int k = 0; k < S; ++k) gmax = std::max(gmax, std::fabs(g[k] * T0[k]));
+      bool moved = false;
+      if (gmax > 0.0)
+        for (int k = 0; k < S; ++k) {
+          const double x = T[k] - aT * T0[k] * (g[k] * T0[k]) / gmax;
+          Ttry[k] = std::min(std::max(x, 0.1), 2.0 * std::fabs(T0[k]));
+          moved = moved || Ttry[k] != T[k];
+        }
+      if (moved) {
+        moved_round = true;
+        const double ft = objective(Ttry, d);
+        ++n_eval;
+        if (ft < f) {
+          f = ft;
+          T = Ttry;
+          aT = std::min(aT * 1.5, 1.0);
+          stale = true;
+          dstar_ok = false;
+        } else {
+          aT *= 0.5;
+        }
+      }
+    }
+    if (!(n_eval < max_evals)) break;
+    if (ad > 1e-9) {  // d block
+      if (!dstar_ok) {
+        lp.updateSegmentTimes(T);
+        lp.solveLinear();
+        for (int k = 0; k < D; ++k)
+          for (int i = 0; i < np; ++i) dstar[k * np + i] = lp.dp[k][i];
+        dstar_ok = true;
+      }
+      bool moved = false;
+      for (int i = 0; i < n; ++i) {
+        const double bnd = 2.0 * std::fabs(d0[i]);
+        double x = d[i] + ad * (dstar[i] - d[i]);
+        x = std::min(std::max(x, -bnd), bnd);
+        dtry[i] = x;
+        moved = moved || std::fabs(x - d[i]) > 1e-13 * (1.0 + std::fabs(d[i]));
+      }
+      if (moved) {
+        moved_round = true;
+        const double ft = objective(T, dtry);
+        ++n_eval;
+        if (ft < f) {
+          f = ft;
+          d = dtry;
+          ad = std::min(ad * 1.5, 1.0);
+          stale = true;
+        } else {
+          ad *= 0.5;
+        }
+      }
+    }
+    if (!(n_eval < max_evals) || !moved_round) break;
+  }
+  std::memcpy(times_io, T.data(), sizeof(double) * S);
+  std::memcpy(dp_io, d.data(), sizeof(double) * n);
+  if (cost) *cost = f;
+  if (evals) *evals = n_eval;
+  return 0;
+}
+
 }  // extern "C"

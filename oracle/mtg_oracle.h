@@ -244,6 +244,15 @@ int orc_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
                       double soft_weight, double soft_maximum_cost, int max_evals, double* cost,
                       int* evals);
 
+// The mtg_time_free_optimize algorithm restated (optimizeTimeAndFreeConstraints
+// with projected block-alternating steps).  dp_io: D x np, times_io: S.
+int orc_time_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, double* dp_io, double* times_io,
+                           double time_penalty, double increment, int n_soft,
+                           const int* soft_derivatives, const double* soft_limits,
+                           double soft_weight, double soft_maximum_cost, int max_evals,
+                           double* cost, int* evals);
+
 #ifdef __cplusplus
 }
 #endif

@@ -464,3 +464,25 @@ def free_optimize(N, r, vertices, times, dp0, max_evals, lower=None, upper=None,
                                soft_maximum_cost, max_evals, _d(cost), ctypes.byref(evals)),
            "free_optimize")
     return dp, float(cost[0]), evals.value
+
+
+def time_free_optimize(N, r, vertices, times, dp0, max_evals, time_penalty=500.0, increment=0.1,
+                       soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """orc_time_free_optimize: the mtg_time_free_optimize algorithm on the
+    oracle.  Returns (times, dp, J, evals)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    t = np.ascontiguousarray(times, dtype=np.float64).copy()
+    dp = np.ascontiguousarray(dp0, dtype=np.float64).copy()
+    cost = np.zeros(1)
+    evals = ctypes.c_int()
+    ns, der, lim = _soft_arrays(soft)
+    L = lib()
+    L.orc_time_free_optimize.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, ctypes.c_double, ctypes.c_double, ctypes.c_int, _ip, _dp,
+        ctypes.c_double, ctypes.c_double, ctypes.c_int, _dp, ctypes.POINTER(ctypes.c_int)]
+    _check(L.orc_time_free_optimize(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                    _d(vertices.vals), _d(dp), _d(t), time_penalty, increment,
+                                    ns, der.ctypes.data_as(_ip), _d(lim), soft_weight,
+                                    soft_maximum_cost, max_evals, _d(cost), ctypes.byref(evals)),
+           "time_free_optimize")
+    return t, dp, float(cost[0]), evals.value

@@ -759,6 +759,51 @@ TEST(gpu, FreeConstraintsObjective) {
   EXPECT_TRUE(traj.K() == 4);
 }
 
+// kOptimizeFreeConstraintsAndTime (optimizeTimeAndFreeConstraints,
+// nonlinear_impl:610-706): the shim runs mtg_time_free_optimize from the tube
+// QCQP start; the same steps as the oracle port, a lower objective, bounds
+// held.
+TEST(gpu, OptimizeTimeAndFreeConstraints) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> times = estimateSegmentTimes(vs, 2.0, 2.0);
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndTime;
+  p.weights.w_c = 0.0;
+  p.max_iterations = 30;
+  PolynomialOptimizationNonLinear<10> opt(3, p);
+  opt.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(4, {0.15, 0.15}), 4);
+  EXPECT_TRUE(opt.solveQCQP() == 0);
+  std::vector<VectorXd> fc;
+  opt.getConstrainedOptimizationRef().getFreeConstraints(&fc);
+  const double J0 = opt.evaluateTimeAndFreeConstraintsCost(times, fc);
+  EXPECT_TRUE(opt.optimize() > 0);
+  const OptimizationInfo info = opt.getOptimizationInfo();
+  EXPECT_TRUE(info.n_iterations >= 2 && info.n_iterations <= 30);
+  std::vector<double> t1;
+  opt.getConstrainedOptimizationRef().getSegmentTimes(&t1);
+  std::vector<VectorXd> f1;
+  opt.getConstrainedOptimizationRef().getFreeConstraints(&f1);
+  const double J1 = opt.evaluateTimeAndFreeConstraintsCost(t1, f1);
+  EXPECT_TRUE(J1 < J0);
+  EXPECT_LE(relErr(J1, info.cost_trajectory + info.cost_time), 1e-9);
+  for (size_t i = 0; i < t1.size(); ++i) EXPECT_TRUE(t1[i] >= 0.1 && t1[i] <= 2.0 * times[i]);
+  // Oracle port from the same start.
+  Dense d = toDense(vs, 5);
+  for (int v = 1; v < d.S; ++v)
+    for (int k = 0; k < 5; ++k) d.mask[v * 5 + k] = 0;
+  std::vector<double> x, ot = times;
+  for (const VectorXd& v : fc)
+    for (long i = 0; i < v.size(); ++i) x.push_back(v[i]);
+  double oJ = 0.0;
+  int oev = 0;
+  EXPECT_TRUE(orc_time_free_optimize(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), x.data(),
+                                     ot.data(), p.time_penalty, p.increment_time, 0, nullptr,
+                                     nullptr, 100.0, 1e12, 30, &oJ, &oev) == 0);
+  EXPECT_TRUE(oev == info.n_iterations);
+  EXPECT_LE(relErr(J1, oJ), 1e-6);
+  EXPECT_LE(relErr(t1, ot), 1e-6);
+}
+
 int main(int argc, char** argv) {
   const std::string group = argc > 1 ? argv[1] : "host";
   int run = 0, failed_tests = 0;

@@ -166,3 +166,40 @@ def test_free_rejects_bad_arguments(ctx, dev, oracle):
     with pytest.raises(MTGError):
         plan.free_optimize(_T(dev, df[None]), _T(dev, dp[None]), _T(dev, times[None]),
                            max_evals=0)
+
+
+@pytest.mark.parametrize("pattern", ["tube", "standard"])
+def test_time_free_optimize_vs_oracle(ctx, dev, oracle, pattern):
+    """mtg_time_free_optimize (optimizeTimeAndFreeConstraints,
+    nonlinear_impl:610-706, with the device optimiser in place of SBPLX --
+    parity vs NLopt unpinned) takes the same steps as the oracle port from
+    the linear-solve start: same evaluation count, times, d_p and objective to
+    1e-6; bounds T in [0.1, 2 T0], d in [-2|d0|, 2|d0|] hold; J decreases."""
+    S, D, E = 6, 3, 40
+    agree = 0
+    for seed in range(700, 706):
+        v, times = _problem(oracle, S, D, seed, pattern)
+        plan, df = _plan(ctx, v)
+        d0 = oracle.linear_solve(N, R, v, times)["dp"]
+        out = plan.time_free_optimize(_T(dev, df[None]), _T(dev, d0[None]), _T(dev, times[None]),
+                                      max_evals=E)
+        T = out["times"].cpu().numpy()[0]
+        dp = out["free"].cpu().numpy()[0]
+        J = float(out["cost"][0])
+        ev = int(out["evals"][0])
+        assert int(out["status"][0]) == 0
+        assert np.all(T >= 0.1 - 1e-15) and np.all(T <= 2 * times + 1e-12)
+        assert np.all(np.abs(dp) <= 2 * np.abs(d0) + 1e-12)
+        J0, _ = oracle.free_cost(N, R, v, times, d0, mode=1)
+        assert J <= J0
+        # the reported cost is the objective at the returned point
+        chk = plan.free_cost(_T(dev, df[None]), _T(dev, dp[None]), out["times"], mode=1,
+                             grad=False)["cost"]
+        assert rel_err(float(chk[0]), J) <= 1e-12
+        To, dpo, Jo, evo = oracle.time_free_optimize(N, R, v, times, d0, E)
+        if evo == ev and np.max(np.abs(T - To) / To) <= 1e-6:
+            assert rel_err(J, Jo) <= 1e-6
+            scale = np.maximum(np.abs(dpo), 1e-6 * np.max(np.abs(dpo)))
+            assert np.max(np.abs(dp - dpo) / scale) <= 1e-5
+            agree += 1
+    assert agree >= 5, agree
