@@ -111,6 +111,151 @@ class Polynomial {
     return true;
   }
 
+  // Extrema of p^(derivative) on [t_start, t_end] (polynomial.cpp:32-143):
+  // candidates are t_start, t_end and the real roots of p^(derivative+1) in
+  // the interval; the first candidate with the smallest / largest value wins
+  // (selectMinMaxFromCandidates, :118-143).  The reference finds ALL complex
+  // roots by Jenkins-Traub (rpoly_ak1.cpp) and drops those outside the
+  // interval; only the real roots inside matter, so this build isolates them
+  // by Bernstein subdivision (Descartes' rule of signs) and bisects each to
+  // full precision.  Results: (time, value).
+  bool computeMinMaxCandidates(double t_start, double t_end, int derivative,
+                               std::vector<double>* candidates) const {
+    MTG_CHECK(candidates != nullptr, "candidates must not be null");
+    candidates->clear();
+    if (N_ - derivative - 1 < 0) {
+      internal::warn("N - derivative - 1 has to be at least 0.");
+      return false;
+    }
+    if (t_start > t_end) {
+      internal::warn("t_start is greater than t_end.");
+      return false;
+    }
+    candidates->push_back(t_start);
+    candidates->push_back(t_end);
+    const VectorXd q = getCoefficients(derivative + 1);
+    for (double r : realRootsIn(q, N_ - derivative - 1, t_start, t_end)) candidates->push_back(r);
+    return true;
+  }
+  bool selectMinMaxFromCandidates(const std::vector<double>& candidates, int derivative,
+                                  std::pair<double, double>* minimum,
+                                  std::pair<double, double>* maximum) const {
+    MTG_CHECK(minimum != nullptr && maximum != nullptr, "outputs must not be null");
+    if (candidates.empty()) {
+      internal::warn("Cannot find extrema from an empty candidates vector.");
+      return false;
+    }
+    minimum->first = maximum->first = candidates[0];
+    minimum->second = std::numeric_limits<double>::max();
+    maximum->second = std::numeric_limits<double>::lowest();
+    for (double t : candidates) {
+      const double v = evaluate(t, derivative);
+      if (v < minimum->second) *minimum = std::make_pair(t, v);
+      if (v > maximum->second) *maximum = std::make_pair(t, v);
+    }
+    return true;
+  }
+  bool computeMinMax(double t_start, double t_end, int derivative,
+                     std::pair<double, double>* minimum,
+                     std::pair<double, double>* maximum) const {
+    std::vector<double> candidates;
+    if (!computeMinMaxCandidates(t_start, t_end, derivative, &candidates)) return false;
+    return selectMinMaxFromCandidates(candidates, derivative, minimum, maximum);
+  }
+
+  // Real roots in [a, b] of sum_{k<n} q_k t^k, ascending.  Bernstein
+  // coefficients on the interval, depth-first dyadic subdivision: no sign
+  // variation -> no root, one -> exactly one root (bisected to the rounding
+  // floor), more -> split (a cluster narrower than 2^-50 of the interval
+  // reports its midpoint).  Long double throughout.
+  static std::vector<double> realRootsIn(const VectorXd& q, int n, double a, double b) {
+    typedef long double ld;
+    std::vector<double> roots;
+    int deg = n - 1;
+    while (deg > 0 && q[deg] == 0.0) --deg;
+    if (deg < 1 || !(b > a)) return roots;
+    // Coefficients of s(u) = p(a + (b - a) u), u in [0, 1] (Taylor shift, scale).
+    std::vector<ld> c(deg + 1);
+    for (int i = 0; i <= deg; ++i) c[i] = q[i];
+    for (int i = 0; i < deg; ++i)  // shift by a (repeated synthetic division)
+      for (int j = deg - 1; j >= i; --j) c[j] += static_cast<ld>(a) * c[j + 1];
+    ld w = 1;
+    for (int i = 0; i <= deg; ++i) {
+      c[i] *= w;
+      w *= static_cast<ld>(b) - static_cast<ld>(a);
+    }
+    auto binom = [](int nn, int k) {
+      ld r = 1;
+      for (int i = 1; i <= k; ++i) r = r * (nn - k + i) / i;
+      return r;
+    };
+    std::vector<ld> bern(deg + 1);
+    for (int i = 0; i <= deg; ++i) {
+      ld acc = 0;
+      for (int j = 0; j <= i; ++j) acc += binom(i, j) / binom(deg, j) * c[j];
+      bern[i] = acc;
+    }
+    auto horner = [&](ld u) {
+      ld v = c[deg];
+      for (int j = deg - 1; j >= 0; --j) v = v * u + c[j];
+      return v;
+    };
+    struct Node {
+      std::vector<ld> bb;
+      ld lo, hi;
+      int depth;
+    };
+    std::vector<Node> stack{{bern, 0.0L, 1.0L, 0}};
+    std::vector<ld> found;
+    while (!stack.empty()) {
+      Node nd = stack.back();
+      stack.pop_back();
+      int var = 0;
+      ld last = 0;
+      for (ld x : nd.bb) {
+        if (x == 0) continue;
+        if (last != 0 && ((x > 0) != (last > 0))) ++var;
+        last = x;
+      }
+      if (nd.bb.front() == 0 && nd.lo > 0) found.push_back(nd.lo);
+      if (var == 0) continue;
+      if (var == 1 || nd.depth >= 50) {
+        ld lo = nd.lo, hi = nd.hi;
+        if (var == 1) {
+          const bool pos_lo = horner(lo) > 0;
+          for (int it = 0; it < 200 && hi - lo > 0; ++it) {
+            const ld mid = 0.5L * (lo + hi);
+            if (mid <= lo || mid >= hi) break;
+            const ld fm = horner(mid);
+            if (fm == 0) {
+              lo = hi = mid;
+              break;
+            }
+            if ((fm > 0) == pos_lo) lo = mid; else hi = mid;
+          }
+        }
+        found.push_back(0.5L * (lo + hi));
+        continue;
+      }
+      // de Casteljau split at the midpoint.
+      const int m = static_cast<int>(nd.bb.size()) - 1;
+      std::vector<ld> left(m + 1), right(m + 1), tmp = nd.bb;
+      for (int r = 0; r <= m; ++r) {
+        left[r] = tmp[0];
+        right[m - r] = tmp[m - r];
+        for (int i = 0; i < m - r; ++i) tmp[i] = 0.5L * (tmp[i] + tmp[i + 1]);
+      }
+      const ld mid = 0.5L * (nd.lo + nd.hi);
+      stack.push_back({right, mid, nd.hi, nd.depth + 1});
+      stack.push_back({left, nd.lo, mid, nd.depth + 1});
+    }
+    for (ld u : found) {
+      const double t = static_cast<double>(static_cast<ld>(a) + u * (static_cast<ld>(b) - a));
+      if (t >= a && t <= b) roots.push_back(t);
+    }
+    return roots;
+  }
+
   // Row `derivative` of the derivative basis at t (polynomial.h:201-219).
   static void baseCoeffsWithTime(int N, int derivative, double t, VectorXd* coeffs) {
     MTG_CHECK(derivative < N, "derivative must be < N");

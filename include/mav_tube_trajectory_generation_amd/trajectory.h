@@ -4,8 +4,11 @@
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_TRAJECTORY_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_TRAJECTORY_H_
 
+#include <limits>
 #include <vector>
 
+#include "mav_tube_trajectory_generation_amd/device.h"
+#include "mav_tube_trajectory_generation_amd/extremum.h"
 #include "mav_tube_trajectory_generation_amd/segment.h"
 #include "mav_tube_trajectory_generation_amd/vertex.h"
 
@@ -106,6 +109,102 @@ class Trajectory {
       tin += dt;
       acc += dt;
     }
+  }
+
+  // trajectory.cpp:136-152.
+  Trajectory getTrajectoryWithSingleDimension(int dimension) const {
+    MTG_CHECK(dimension >= 0 && dimension < D_, "dimension out of range");
+    Segment::Vector segments;
+    segments.reserve(segments_.size());
+    for (const Segment& s : segments_) {
+      Segment one(N_, 1);
+      one[0] = s[dimension];
+      segments.push_back(one);  // time 0, as the reference (segment time not copied)
+    }
+    Trajectory traj;
+    traj.setSegments(segments);
+    return traj;
+  }
+
+  // trajectory.cpp:154-182.
+  bool getTrajectoryWithAppendedDimension(const Trajectory& to_append,
+                                          Trajectory* new_trajectory) const {
+    MTG_CHECK(new_trajectory != nullptr, "new_trajectory must not be null");
+    if (N_ == 0 || D_ == 0) {
+      *new_trajectory = to_append;
+      return true;
+    }
+    if (to_append.N() == 0 || to_append.D() == 0) {
+      *new_trajectory = *this;
+      return true;
+    }
+    MTG_CHECK(K() == to_append.K(), "segment counts differ");
+    Segment::Vector segments;
+    segments.reserve(segments_.size());
+    for (size_t k = 0; k < segments_.size(); ++k) {
+      Segment s(0, 0);
+      if (!segments_[k].getSegmentWithAppendedDimension(to_append.segments()[k], &s))
+        return false;
+      segments.push_back(s);
+    }
+    new_trajectory->setSegments(segments);
+    return true;
+  }
+
+  // trajectory.cpp:230-251: this trajectory followed by `trajectories`
+  // (same D and N, else false).
+  bool addTrajectories(const std::vector<Trajectory>& trajectories, Trajectory* merged) const {
+    MTG_CHECK(merged != nullptr, "merged must not be null");
+    merged->clear();
+    *merged = *this;
+    for (const Trajectory& t : trajectories) {
+      if (t.D() != D_ || t.N() != N_) return false;
+      merged->addSegments(t.segments());
+    }
+    return true;
+  }
+
+  // Minimum and maximum of |p^(derivative)| over the given dimensions and
+  // every segment (trajectory.cpp:184-220) by the device candidate search
+  // (mtg_min_max_magnitude): the selected dimensions are packed and sent
+  // once.  Extremum times are relative to the segment start.
+  bool computeMinMaxMagnitude(int derivative, const std::vector<int>& dimensions,
+                              Extremum* minimum, Extremum* maximum) const {
+    MTG_CHECK(minimum != nullptr && maximum != nullptr, "outputs must not be null");
+    if (dimensions.empty()) {
+      internal::warn("No dimensions specified.");
+      return false;
+    }
+    for (int d : dimensions)
+      if (d < 0 || d >= D_) {
+        internal::warn("Specified dimension out of bounds.");
+        return false;
+      }
+    if (segments_.empty() || N_ - derivative - 1 <= 0 || derivative < 0) return false;
+    const int S = K(), Dn = static_cast<int>(dimensions.size());
+    std::vector<double> coeffs(static_cast<size_t>(S) * Dn * N_), times(S);
+    for (int s = 0; s < S; ++s) {
+      times[s] = segments_[s].getTime();
+      for (int j = 0; j < Dn; ++j) {
+        const VectorXd c = segments_[s][dimensions[j]].getCoefficients(0);
+        for (int k = 0; k < N_; ++k) coeffs[(static_cast<size_t>(s) * Dn + j) * N_ + k] = c[k];
+      }
+    }
+    internal::DeviceBuffer<double> d_c, d_t, d_out(4);
+    internal::DeviceBuffer<int32_t> d_seg(2);
+    d_c.upload(coeffs);
+    d_t.upload(times);
+    internal::checkStatus(
+        mtg_min_max_magnitude(N_, Dn, S, 1, d_c.get(), d_t.get(), derivative, d_out.get(),
+                              d_out.get() + 1, d_seg.get(), d_out.get() + 2, d_out.get() + 3,
+                              d_seg.get() + 1, nullptr),
+        "mtg_min_max_magnitude");
+    internal::synchronize();
+    const std::vector<double> o = d_out.download();
+    const std::vector<int32_t> sg = d_seg.download();
+    *minimum = Extremum(o[0], o[1], sg[0]);
+    *maximum = Extremum(o[2], o[3], sg[1]);
+    return true;
   }
 
   // Vertex at time t with derivatives 0..max_derivative_order

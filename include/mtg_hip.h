@@ -413,6 +413,23 @@ int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                       const double* times, int derivative, double* max_time,
                       double* max_value, int32_t* max_segment, void* stream);
 
+/* Minimum and maximum of the magnitude: Trajectory::computeMinMaxMagnitude
+ * (src/trajectory.cpp:184-220, candidates of Segment::
+ * computeMinMaxMagnitudeCandidates, src/segment.cpp:82-161) over all D
+ * dimensions of the coefficients given (a caller selecting dimensions passes
+ * only those).  Same candidate search as mtg_max_magnitude; the minimum is
+ * the first candidate with the smallest |p^(derivative)| (strict '<' from
+ * +max in segment order, trajectory.cpp:201-214).  For D = 1 the candidates
+ * include the zeros of p^(derivative) (the real minimum of |p|), where the
+ * reference takes only the roots of p^(derivative+1) (segment.cpp:123-129),
+ * so a 1-D minimum can be lower than the reference's; maxima agree.  Outputs
+ * (device, each nullable): min_time / max_time B (relative to the segment
+ * start), min_value / max_value B, min_segment / max_segment B. */
+int mtg_min_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
+                          const double* times, int derivative, double* min_time,
+                          double* min_value, int32_t* min_segment, double* max_time,
+                          double* max_value, int32_t* max_segment, void* stream);
+
 /* Soft-constraint cost of PolynomialOptimizationNonLinear
  * (evaluateMaximumMagnitudeAsSoftConstraint, nonlinear_impl:2735-2766; the
  * constraints of addMaximumMagnitudeConstraint, :847-875):

@@ -8,11 +8,12 @@ package is the batched front end used by tests and bench.py.
 """
 from ._abi import LIB_PATH, MTGError, lib  # noqa: F401
 from .batch import (Context, LinearPlan, generate_random_problems, max_magnitude,  # noqa: F401
-                    sample_trajectories, segment_matrices, soft_constraint_cost,
+                    min_max_magnitude, sample_trajectories, segment_matrices, soft_constraint_cost,
                     tube_num_constraints, tube_residuals, tube_solve, tube_time_cost,
                     tube_time_optimize, tube_time_workspace_bytes)
 
 __all__ = ["Context", "LinearPlan", "MTGError", "generate_random_problems", "max_magnitude",
+           "min_max_magnitude",
            "sample_trajectories", "segment_matrices", "soft_constraint_cost",
            "tube_num_constraints", "tube_residuals", "tube_solve", "tube_time_cost",
            "tube_time_optimize", "tube_time_workspace_bytes", "lib", "LIB_PATH"]

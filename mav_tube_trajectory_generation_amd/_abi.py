@@ -67,6 +67,9 @@ SIGNATURES = {
                                               ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
                                               _vp, _vp, _vp]),
     "mtg_plan_kernel": (ctypes.c_int, [_vp]),
+    "mtg_min_max_magnitude": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp, _vp,
+                                             _vp, _vp, _vp, _vp, _vp]),
     "mtg_plan_kernel_for_batch": (ctypes.c_int, [_vp, ctypes.c_int64]),
     "mtg_linear_solve": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mtg_linear_solve_host": (ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, _dp, _dp,

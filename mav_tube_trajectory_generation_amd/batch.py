@@ -486,6 +486,28 @@ def max_magnitude(coeffs, times, derivative, out=None):
     return out
 
 
+def min_max_magnitude(coeffs, times, derivative):
+    """Batched Trajectory::computeMinMaxMagnitude (trajectory.cpp:184-220;
+    mtg_min_max_magnitude) over all D dimensions of coeffs [B, S, D, N].
+    Returns a dict of min_time, min_value, min_segment, max_time, max_value,
+    max_segment [B]."""
+    import torch
+    B, S, D, N = coeffs.shape
+    _require(coeffs, (B, S, D, N), "coeffs")
+    _require(times, (B, S), "times")
+    dev = times.device
+    out = {k: torch.empty(B, dtype=torch.float64, device=dev)
+           for k in ("min_time", "min_value", "max_time", "max_value")}
+    out["min_segment"] = torch.empty(B, dtype=torch.int32, device=dev)
+    out["max_segment"] = torch.empty(B, dtype=torch.int32, device=dev)
+    check(lib().mtg_min_max_magnitude(N, D, S, B, _ptr(coeffs), _ptr(times), derivative,
+                                      _ptr(out["min_time"]), _ptr(out["min_value"]),
+                                      _ptr(out["min_segment"]), _ptr(out["max_time"]),
+                                      _ptr(out["max_value"]), _ptr(out["max_segment"]),
+                                      _stream(dev)), "mtg_min_max_magnitude")
+    return out
+
+
 def soft_constraint_cost(coeffs, times, derivatives, limits, weight=100.0, maximum_cost=1.0e12,
                          out=None):
     """Batched evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:

@@ -37,14 +37,16 @@ namespace mtg {
 
 constexpr int kExtBlock = 256;
 
-template <int N, int K>
+template <int N, int K, bool kMin>
 __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
     int D, int S, int64_t B, int parts, int log2parts, const double* __restrict__ coeffs,
     const double* __restrict__ times, double* __restrict__ max_time,
     double* __restrict__ max_value, int32_t* __restrict__ max_segment, int value_stride,
-    int value_offset, SoftCostArgs soft) {
+    int value_offset, SoftCostArgs soft, MinOut mino) {
   __shared__ double val_s[kExtBlock];
   __shared__ double time_s[kExtBlock];
+  __shared__ double mval_s[kMin ? kExtBlock : 1];
+  __shared__ double mtime_s[kMin ? kExtBlock : 1];
   // The block's trajectories (coefficients, then segment times), staged
   // once with coalesced loads: every magnitude evaluation reads LDS.
   extern __shared__ double traj_s[];
@@ -69,13 +71,19 @@ __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
   __syncthreads();
 
   double best_v = -1.0, best_t = 0.0;  // |p|^2 and time of this lane's best
+  double min_v = HUGE_VAL, min_t = 0.0;
   if (active) {
     const double T = traj_s[traj_per_block * S * D * N + bl * S + s];
     const double* c = traj_s + (bl * S + s) * D * N;
-    ext_segment_search<N, K>(c, D, T, part, parts, log2parts, best_v, best_t);
+    ext_segment_search<N, K, kMin>(c, D, T, part, parts, log2parts, best_v, best_t, min_v,
+                                   min_t);
   }
   val_s[tid] = best_v;
   time_s[tid] = best_t;
+  if constexpr (kMin) {
+    mval_s[tid] = min_v;
+    mtime_s[tid] = min_t;
+  }
   __syncthreads();
   // Reduction in candidate order: segment ascending, part ascending; strict
   // '>' keeps the first maximum (Extremum::operator<, extremum.h:35-36;
@@ -109,26 +117,43 @@ __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
     }
     if (max_time) max_time[b] = t;
     if (max_segment) max_segment[b] = seg;
+    if constexpr (kMin) {
+      // Same order, strict '<' from +max (trajectory.cpp:191-215).
+      double mv = HUGE_VAL, mt = 0.0;
+      int mseg = 0;
+      for (int i = 0; i < lanes_per_traj; ++i) {
+        const double x = mval_s[tid + i];
+        if (x < mv) {
+          mv = x;
+          mt = mtime_s[tid + i];
+          mseg = i >> log2parts;
+        }
+      }
+      if (mino.value) mino.value[b] = sqrt(mv);
+      if (mino.time) mino.time[b] = mt;
+      if (mino.segment) mino.segment[b] = mseg;
+    }
   }
 }
 
-template <int N>
+template <int N, bool kMin>
 static hipError_t launch_max_n(int K, int D, int S, int64_t B, int parts, int log2parts,
                                const double* coeffs, const double* times, double* tmax,
                                double* vmax, int32_t* smax, int stride, int offset,
-                               const SoftCostArgs& soft, hipStream_t st) {
+                               const SoftCostArgs& soft, const MinOut& mino, hipStream_t st) {
   const int tpb = kExtBlock / (S * parts);
   const dim3 grid(static_cast<unsigned>((B + tpb - 1) / tpb));
   const size_t lds = sizeof(double) * static_cast<size_t>(tpb) * S * (D * N + 1);
 #define CALL(k)                                                                                \
   if (lds > 65536) {                                                                           \
     const hipError_t e = hipFuncSetAttribute(                                                  \
-        reinterpret_cast<const void*>(max_magnitude_kernel<N, k>),                             \
+        reinterpret_cast<const void*>(max_magnitude_kernel<N, k, kMin>),                       \
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));                     \
     if (e != hipSuccess) return e;                                                             \
   }                                                                                            \
-  hipLaunchKernelGGL((max_magnitude_kernel<N, k>), grid, dim3(kExtBlock), lds, st, D, S, B,      \
-                     parts, log2parts, coeffs, times, tmax, vmax, smax, stride, offset, soft)
+  hipLaunchKernelGGL((max_magnitude_kernel<N, k, kMin>), grid, dim3(kExtBlock), lds, st, D, S,    \
+                     B, parts, log2parts, coeffs, times, tmax, vmax, smax, stride, offset, soft,  \
+                     mino)
   switch (K) {
     case 0: CALL(0); break;
     case 1: CALL(1); break;
@@ -148,7 +173,8 @@ static hipError_t launch_max_n(int K, int D, int S, int64_t B, int parts, int lo
 hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
                                 const double* coeffs, const double* times, double* max_time,
                                 double* max_value, int32_t* max_segment, int value_stride,
-                                int value_offset, const SoftCostArgs& soft, hipStream_t st) {
+                                int value_offset, const SoftCostArgs& soft, hipStream_t st,
+                                const MinOut* mino) {
   if (S < 1 || S > kExtBlock || derivative < 0 || derivative > kMaxExtremaDerivative ||
       N - derivative - 1 <= 0)
     return hipErrorInvalidValue;
@@ -157,9 +183,14 @@ hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
     parts >>= 1;
     --log2parts;
   }
-#define CALL(n)                                                                           \
-  launch_max_n<n>(derivative, D, S, B, parts, log2parts, coeffs, times, max_time, max_value, \
-                  max_segment, value_stride, value_offset, soft, st)
+  const MinOut none{};
+#define CALL(n)                                                                               \
+  (mino ? launch_max_n<n, true>(derivative, D, S, B, parts, log2parts, coeffs, times,          \
+                                max_time, max_value, max_segment, value_stride, value_offset, \
+                                soft, *mino, st)                                              \
+        : launch_max_n<n, false>(derivative, D, S, B, parts, log2parts, coeffs, times,         \
+                                 max_time, max_value, max_segment, value_stride, value_offset, \
+                                 soft, none, st))
   switch (N) {
     case 4: return CALL(4);
     case 6: return CALL(6);

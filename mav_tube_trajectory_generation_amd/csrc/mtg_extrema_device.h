@@ -49,10 +49,26 @@ __device__ inline double ext_mag2(const double* c, int D, double t) {
 // last part: t = T) and the real roots of f = sum_d p_d^(K) p_d^(K+1) in its
 // dyadic part [part / 2^log2parts, (part + 1) / 2^log2parts) of the segment.
 // c: the segment's D x N coefficients (LDS), T: its time.  Updates best_v
-// (|p^(K)|^2) and best_t with strict '>' in candidate order.
-template <int N, int K>
+// (|p^(K)|^2) and best_t with strict '>' in candidate order; with kMin also
+// min_v / min_t with strict '<' (the minimum of Trajectory::
+// computeMinMaxMagnitude, trajectory.cpp:184-220; caller starts min_v at
+// +inf).
+template <int N, int K, bool kMin = false>
 __device__ inline void ext_segment_search(const double* c, int D, double T, int part, int parts,
-                                          int log2parts, double& best_v, double& best_t) {
+                                          int log2parts, double& best_v, double& best_t,
+                                          double& min_v, double& min_t) {
+  auto take = [&](double v, double t) {
+    if (v > best_v) {
+      best_v = v;
+      best_t = t;
+    }
+    if constexpr (kMin) {
+      if (v < min_v) {
+        min_v = v;
+        min_t = t;
+      }
+    }
+  };
   constexpr int ND = N - K;        // terms of p^(K)
   constexpr int NDD = ND - 1;      // terms of p^(K+1)
   constexpr int M = ND + NDD - 2;  // degree of f
@@ -60,14 +76,12 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
   if (part == 0) {
     best_v = ext_mag2<N, K>(c, D, 0.0);
     best_t = 0.0;
-  }
-  if (part == parts - 1) {
-    const double v = ext_mag2<N, K>(c, D, T);
-    if (v > best_v) {
-      best_v = v;
-      best_t = T;
+    if constexpr (kMin) {
+      min_v = best_v;
+      min_t = 0.0;
     }
   }
+  if (part == parts - 1) take(ext_mag2<N, K>(c, D, T), T);
   // f(t) = sum_d conv(p_d^(K), p_d^(K+1)), then q(u) = f(T u) on [0, 1].
   double q[M + 1];
 #pragma unroll
@@ -149,13 +163,8 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
         last = nz ? x : last;
       }
       double root = -1.0;
-      if (bb[0] == 0.0 && a > 0.0) {  // root exactly at the node's left end
-        const double v = ext_mag2<N, K>(c, D, a * T);
-        if (v > best_v) {
-          best_v = v;
-          best_t = a * T;
-        }
-      }
+      if (bb[0] == 0.0 && a > 0.0)  // root exactly at the node's left end
+        take(ext_mag2<N, K>(c, D, a * T), a * T);
       bool descend = false;
       if (var == 1) {
         // Laguerre's method safeguarded by the bracket (bisection when a
@@ -193,14 +202,7 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
         if (level >= kExtMaxLevel) root = 0.5 * (a + e);  // unresolved cluster
         else descend = true;
       }
-      if (root >= 0.0) {
-        const double t = root * T;
-        const double v = ext_mag2<N, K>(c, D, t);
-        if (v > best_v) {
-          best_v = v;
-          best_t = t;
-        }
-      }
+      if (root >= 0.0) take(ext_mag2<N, K>(c, D, root * T), root * T);
       if (descend) {
         ++level;
         idx *= 2;
@@ -230,8 +232,9 @@ __device__ inline double ext_trajectory_max_wave(const double* coeffs, const dou
   double best = 0.0;
   for (int item = lane; item < S * parts; item += 64) {
     const int s = item >> log2parts, part = item & (parts - 1);
-    double v = -1.0, t = 0.0;
-    ext_segment_search<N, K>(coeffs + s * D * N, D, times[s], part, parts, log2parts, v, t);
+    double v = -1.0, t = 0.0, mv = 0.0, mt = 0.0;
+    ext_segment_search<N, K>(coeffs + s * D * N, D, times[s], part, parts, log2parts, v, t, mv,
+                             mt);
     best = fmax(best, v);
   }
 #pragma unroll

@@ -392,6 +392,22 @@ int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                                             static_cast<hipStream_t>(stream)));
 }
 
+int mtg_min_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
+                          const double* times, int derivative, double* min_time,
+                          double* min_value, int32_t* min_segment, double* max_time,
+                          double* max_value, int32_t* max_segment, void* stream) {
+  if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > 256 || B < 0 || derivative < 0 ||
+      derivative > mtg::kMaxExtremaDerivative || N - derivative - 1 <= 0)
+    return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  if (!coeffs || !times) return MTG_ERR_INVALID_ARG;
+  const mtg::SoftCostArgs none{};
+  const mtg::MinOut mino{min_time, min_value, min_segment};
+  return from_hip(mtg::launch_max_magnitude(N, D, S, B, derivative, coeffs, times, max_time,
+                                            max_value, max_segment, 1, 0, none,
+                                            static_cast<hipStream_t>(stream), &mino));
+}
+
 int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeffs,
                              const double* times, int n_constraints, const int* derivatives,
                              const double* limits, double weight, double maximum_cost,

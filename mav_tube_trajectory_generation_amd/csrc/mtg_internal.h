@@ -155,9 +155,16 @@ struct SoftCostArgs {
   SoftLimits lim;
   double weight, maximum_cost;
 };
+// Minimum outputs of mtg_min_max_magnitude (each nullable).
+struct MinOut {
+  double* time;
+  double* value;
+  int32_t* segment;
+};
 hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
                                 const double* coeffs, const double* times, double* max_time,
                                 double* max_value, int32_t* max_segment, int value_stride,
-                                int value_offset, const SoftCostArgs& soft, hipStream_t st);
+                                int value_offset, const SoftCostArgs& soft, hipStream_t st,
+                                const MinOut* mino = nullptr);
 
 }  // namespace mtg

@@ -10,6 +10,9 @@
 //   test_polynomial_optimization gpu    -> the parity tests proper
 #define MTG_CHECK_THROWS 1
 
+#include <fstream>
+#include <random>
+#include <sstream>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -757,6 +760,166 @@ TEST(gpu, FreeConstraintsObjective) {
   Trajectory traj;
   opt.getTrajectory(&traj);
   EXPECT_TRUE(traj.K() == 4);
+}
+
+// FindMinMax (test/test_polynomial.cpp:81-137): roots-based extrema of a
+// random polynomial and its derivatives vs dense sampling (1e-2 there; the
+// candidate search is exact, so 1e-6 of the range here).
+TEST(host, PolynomialMinMax) {
+  std::mt19937 gen(7);
+  std::uniform_real_distribution<double> u(-1.0, 1.0);
+  for (int trial = 0; trial < 20; ++trial) {
+    VectorXd c(10);
+    for (int k = 0; k < 10; ++k) c[k] = u(gen);
+    const Polynomial p(c);
+    const double t0 = -1.5 + 0.1 * trial, t1 = t0 + 3.0;
+    for (int der = 0; der < 4; ++der) {
+      std::pair<double, double> mn, mx;
+      EXPECT_TRUE(p.computeMinMax(t0, t1, der, &mn, &mx));
+      double smin = 1e300, smax = -1e300;
+      for (double t = t0; t <= t1; t += 1e-4) {
+        const double v = p.evaluate(t, der);
+        smin = std::min(smin, v);
+        smax = std::max(smax, v);
+      }
+      const double tol = 1e-6 * std::max(1.0, smax - smin);
+      EXPECT_LE(mn.second, smin + tol);
+      EXPECT_LE(smax, mx.second + tol);
+      EXPECT_LE(smin - 1e-3 * std::max(1.0, smax - smin), mn.second);  // a real value
+      EXPECT_LE(std::fabs(p.evaluate(mn.first, der) - mn.second), 1e-12 * (1.0 + smax - smin));
+      EXPECT_TRUE(mn.first >= t0 && mn.first <= t1 && mx.first >= t0 && mx.first <= t1);
+    }
+  }
+  // constant derivative: only the end points are candidates
+  VectorXd lc(2);
+  lc[0] = 1.0;
+  lc[1] = 2.0;
+  const Polynomial lin(lc);
+  std::vector<double> cand;
+  EXPECT_TRUE(lin.computeMinMaxCandidates(0.0, 1.0, 0, &cand));
+  EXPECT_TRUE(cand.size() == 2);
+}
+
+// Trajectory container operations (trajectory.cpp:136-251).
+TEST(host, TrajectoryContainers) {
+  Segment::Vector segs;
+  for (int s = 0; s < 3; ++s) {
+    Segment seg(10, 3);
+    seg.setTime(1.0 + s);
+    for (int d = 0; d < 3; ++d) {
+      VectorXd c(10);
+      for (int k = 0; k < 10; ++k) c[k] = (d + s) + k * (2.0 * d - s - d - s) / 9.0;
+      seg[d] = Polynomial(c);
+    }
+    segs.push_back(seg);
+  }
+  Trajectory traj;
+  traj.setSegments(segs);
+  const Trajectory y = traj.getTrajectoryWithSingleDimension(1);
+  EXPECT_TRUE(y.D() == 1 && y.K() == 3);
+  for (int s = 0; s < 3; ++s) EXPECT_TRUE(y.segments()[s][0] == segs[s][1]);
+  Trajectory x = traj.getTrajectoryWithSingleDimension(0), xy;
+  EXPECT_TRUE(x.getTrajectoryWithAppendedDimension(y, &xy));
+  EXPECT_TRUE(xy.D() == 2 && xy.K() == 3);
+  for (int s = 0; s < 3; ++s) {
+    EXPECT_TRUE(xy.segments()[s][0] == segs[s][0]);
+    EXPECT_TRUE(xy.segments()[s][1] == segs[s][1]);
+  }
+  Trajectory empty, same;
+  EXPECT_TRUE(empty.getTrajectoryWithAppendedDimension(traj, &same));
+  EXPECT_TRUE(same == traj);
+  Trajectory merged;
+  EXPECT_TRUE(traj.addTrajectories({traj, traj}, &merged));
+  EXPECT_TRUE(merged.K() == 9);
+  EXPECT_LE(std::fabs(merged.getMaxTime() - 18.0), 1e-12);
+  EXPECT_TRUE(!traj.addTrajectories({y}, &merged));  // D differs
+}
+
+// ExtremaOfMagnitude (test_polynomial_optimization.cpp:307-406): the device
+// min / max of |p^(k)| over all dimensions or a subset vs dense sampling, and
+// the maximum vs computeMaximumOfMagnitude.
+TEST(gpu, TrajectoryMinMaxMagnitude) {
+  const Fixture& f = kSeg10Dim3;
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+  PolynomialOptimization<10> opt(3);
+  opt.setupFromVertices(vs, times, 4);
+  opt.solveLinear();
+  Trajectory traj;
+  opt.getTrajectory(&traj);
+  for (int der = 0; der < 4; ++der)
+    for (const std::vector<int>& dims : {std::vector<int>{0, 1, 2}, std::vector<int>{0, 2}}) {
+      Extremum mn, mx;
+      EXPECT_TRUE(traj.computeMinMaxMagnitude(der, dims, &mn, &mx));
+      double smin = 1e300, smax = -1.0;
+      for (int s = 0; s < traj.K(); ++s)
+        for (double t = 0.0; t <= traj.segments()[s].getTime(); t += 1e-3) {
+          const VectorXd v = traj.segments()[s].evaluate(t, der);
+          double m2 = 0.0;
+          for (int d : dims) m2 += v[d] * v[d];
+          smin = std::min(smin, std::sqrt(m2));
+          smax = std::max(smax, std::sqrt(m2));
+        }
+      EXPECT_LE(std::fabs(mx.value - smax), 1e-2 * std::max(1.0, smax));
+      EXPECT_LE(smax, mx.value * (1 + 1e-12) + 1e-12);
+      EXPECT_LE(mn.value, smin + 1e-12);
+      EXPECT_LE(std::fabs(mn.value - smin), 1e-2 * std::max(1.0, smax));
+      const VectorXd at = traj.segments()[mx.segment_idx].evaluate(mx.time, der);
+      double m2 = 0.0;
+      for (int d : dims) m2 += at[d] * at[d];
+      EXPECT_LE(std::fabs(std::sqrt(m2) - mx.value), 1e-9 * std::max(1.0, mx.value));
+      if (dims.size() == 3)
+        EXPECT_LE(relErr(mx.value, opt.computeMaximumOfMagnitude(der, nullptr).value), 1e-12);
+    }
+}
+
+// printMatlabSampledTrajectory (nonlinear_impl:2907-3003): row count, column
+// layout and values against host evaluation at the 6 printed digits.
+TEST(gpu, PrintMatlabSampledTrajectory) {
+  const Fixture& f = kSeg10Dim3;
+  const Vertex::Vector all = fixtureVertices(f, 10);
+  Vertex::Vector vs(all.begin(), all.begin() + 4);
+  vs.back().makeStartOrEnd(VectorXd::Constant(3, 1.0), 4);
+  const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.weights.w_c = 0.0;
+  p.max_iterations = 5;
+  PolynomialOptimizationNonLinear<10> opt(3, p);
+  opt.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(3, {0.15, 0.15}), 4);
+  opt.optimize();
+  const std::string path = "/tmp/mtg_matlab_test.txt";
+  opt.printMatlabSampledTrajectory(path);
+  Trajectory traj;
+  opt.getTrajectory(&traj);
+  const std::vector<double> T = traj.getSegmentTimes();
+  int rows = 0;
+  for (double t : T) rows += static_cast<int>(std::ceil(t / 0.01)) + 1;
+  std::ifstream in(path);
+  std::vector<std::vector<double>> m;
+  std::string line;
+  while (std::getline(in, line)) {
+    std::istringstream is(line);
+    std::vector<double> r;
+    double v;
+    while (is >> v) r.push_back(v);
+    m.push_back(r);
+  }
+  EXPECT_TRUE(static_cast<int>(m.size()) == rows);
+  EXPECT_TRUE(m.front().size() == 17u);
+  double acc = 0.0;
+  for (size_t s = 0; s < T.size(); ++s) {
+    acc += T[s];
+    EXPECT_LE(std::fabs(m[s][16] - acc), 1e-5 * acc);
+  }
+  // row 150 lies in the first segment (T_0 > 1.5 s at these limits)
+  const int r = std::min(150, static_cast<int>(std::ceil(T[0] / 0.01)) - 1);
+  EXPECT_LE(std::fabs(m[r][0] - r * 0.01), 1e-9 + 1e-5 * r * 0.01);
+  for (int k = 0; k <= 4; ++k) {
+    const VectorXd v = traj.segments()[0].evaluate(r * 0.01, k);
+    for (int d = 0; d < 3; ++d)
+      EXPECT_LE(std::fabs(m[r][1 + 3 * k + d] - v[d]), 1e-5 * std::max(1e-3, std::fabs(v[d])));
+  }
 }
 
 // kOptimizeFreeConstraintsAndTime (optimizeTimeAndFreeConstraints,

@@ -181,3 +181,34 @@ def test_max_magnitude_random_polynomials(ctx, dev, oracle, N, D, S, K):
         ref = oracle.max_magnitude(N, coeffs[b], times[b], K)
         assert abs(float(out["value"][b]) - ref["value"]) <= 1e-10 * ref["value"]
         _check_argmax(float(out["time"][b]), int(out["segment"][b]), ref, coeffs[b], times[b], K)
+
+
+@pytest.mark.parametrize("N,D,S", [(10, 3, 10), (10, 2, 4), (8, 3, 6)])
+def test_min_max_magnitude(ctx, dev, oracle, N, D, S):
+    """mtg_min_max_magnitude (Trajectory::computeMinMaxMagnitude,
+    trajectory.cpp:184-220): the maximum is mtg_max_magnitude's bit for bit;
+    the minimum is attained at its reported (segment, time), is no larger than
+    the minimum over 2000 samples per segment, and no smaller by more than
+    the sampling resolution (the test_polynomial_optimization.cpp:307-406
+    check, 1e-2 there)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    seeds = list(range(900, 908))
+    coeffs, times = _problems(oracle, N, D, S, seeds)
+    c_d = torch.from_numpy(coeffs).to(dev)
+    t_d = torch.from_numpy(times).to(dev)
+    for k in range(0, 4):
+        mm = {key: v.cpu().numpy() for key, v in mtg.min_max_magnitude(c_d, t_d, k).items()}
+        mx = {key: v.cpu().numpy() for key, v in mtg.max_magnitude(c_d, t_d, k).items()}
+        assert np.array_equal(mm["max_value"], mx["value"])
+        assert np.array_equal(mm["max_time"], mx["time"])
+        assert np.array_equal(mm["max_segment"], mx["segment"])
+        for b in range(len(seeds)):
+            smin = min(np.min(_magnitude(coeffs[b, s], np.linspace(0, times[b, s], 2000), k))
+                       for s in range(S))
+            vmax = mm["max_value"][b]
+            s_, t_ = int(mm["min_segment"][b]), mm["min_time"][b]
+            assert 0.0 <= t_ <= times[b, s_]
+            got = _magnitude(coeffs[b, s_], t_, k)
+            assert abs(got - mm["min_value"][b]) <= 1e-9 * max(vmax, 1.0)
+            assert mm["min_value"][b] <= smin + 1e-12 * max(vmax, 1.0)
+            assert smin - mm["min_value"][b] <= 1e-2 * max(vmax, 1.0)
