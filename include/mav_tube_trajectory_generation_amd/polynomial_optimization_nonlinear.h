@@ -29,9 +29,14 @@
 //     adds the soft cost of evaluateMaximumMagnitudeAsSoftConstraint
 //     (:2735-2766) to the objective, evaluated on the device after every
 //     inner solve (extremum search of mtg_max_magnitude); at most 8
-//     constraints, derivatives POSITION..SNAP.  The NLopt hard inequality
-//     constraints used when use_soft_constraints is false (:861-872) have no
-//     counterpart in the device optimiser: that call returns false.
+//     constraints, derivatives POSITION..SNAP.  With use_soft_constraints =
+//     false they are the NLopt inequality constraints of :861-872
+//     (max |p^(k)| - value <= inequality_constraint_tolerance,
+//     evaluateMaximumMagnitudeConstraint, :2687-2733): kOptimizeTime's
+//     device optimiser then accepts only feasible improving trials
+//     (feasibility first from an infeasible start, mtg_time_params
+//     hard_constraints); the other objectives' device optimisers ignore hard
+//     constraints with a warning.
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
 
@@ -162,12 +167,6 @@ class PolynomialOptimizationNonLinear {
   bool addMaximumMagnitudeConstraint(int derivative_order, double maximum_value) {
     MTG_CHECK(derivative_order >= 0, "derivative must be >= 0");
     MTG_CHECK(maximum_value >= 0.0, "maximum_value must be >= 0");
-    if (!params_.use_soft_constraints) {
-      internal::warn(
-          "addMaximumMagnitudeConstraint: hard (NLopt) inequality constraints are not "
-          "available in the device optimiser; set use_soft_constraints");
-      return false;
-    }
     if (soft_.size() >= 8 || derivative_order > derivative_order::SNAP ||
         N - derivative_order - 1 <= 0) {
       internal::warn("addMaximumMagnitudeConstraint: unsupported constraint ignored");
@@ -198,7 +197,7 @@ class PolynomialOptimizationNonLinear {
     internal::DeviceBuffer<double> d_df, d_t, d_cost(1), d_g(S);
     d_df.upload(packFixed());
     d_t.upload(segment_times);
-    const mtg_time_params p = timeParams(grad_mode);
+    const mtg_time_params p = timeParams(grad_mode, true);
     internal::checkStatus(mtg_time_cost(planOf(), 1, d_df.get(), d_t.get(), &p, d_cost.get(),
                                         grad_mode ? d_g.get() : nullptr, nullptr, nullptr),
                           "mtg_time_cost");
@@ -250,7 +249,7 @@ class PolynomialOptimizationNonLinear {
     internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
     d_df.upload(packFixed());
     d_t.upload(times);
-    const mtg_time_params p = timeParams(0);
+    const mtg_time_params p = timeParams(0, true);
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
     internal::checkStatus(mtg_time_optimize(planOf(), 1, d_df.get(), d_t.get(), &p, budget,
                                             d_cost.get(), d_ev.get(), nullptr, d_st.get(),
@@ -604,14 +603,22 @@ class PolynomialOptimizationNonLinear {
     return optimization_info_.stopping_reason;
   }
 
-  mtg_time_params timeParams(int grad_mode) const {
+  // hard_ok: the entry point takes hard constraints (mtg_time_cost /
+  // mtg_time_optimize); elsewhere hard constraints are dropped with a warning.
+  mtg_time_params timeParams(int grad_mode, bool hard_ok = false) const {
     mtg_time_params p;
     p.time_penalty = params_.time_penalty;
     p.increment = params_.increment_time;
     p.w_d = params_.weights.w_d;
     p.w_t = params_.weights.w_t;
     p.grad_mode = grad_mode;
-    p.n_soft = params_.use_soft_constraints ? static_cast<int>(soft_.size()) : 0;
+    const bool hard = !params_.use_soft_constraints;
+    if (hard && !hard_ok && !soft_.empty())
+      internal::warn("hard magnitude constraints are only applied by kOptimizeTime with the "
+                     "linear inner solve; ignored here");
+    p.n_soft = (!hard || hard_ok) ? static_cast<int>(soft_.size()) : 0;
+    p.hard_constraints = hard && hard_ok ? 1 : 0;
+    p.hard_tolerance = params_.inequality_constraint_tolerance;
     for (int c = 0; c < 8; ++c) {
       p.soft_derivative[c] = c < p.n_soft ? soft_[c].first : 0;
       p.soft_limit[c] = c < p.n_soft ? soft_[c].second : 1.0;

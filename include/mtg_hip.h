@@ -175,6 +175,14 @@ int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n,
  * exp((max_t |p^(soft_derivative[c])| - soft_limit[c]) / soft_limit[c] *
  * soft_weight)), with the maxima from the device extremum search of
  * mtg_max_magnitude.
+ * hard_constraints = 1 (use_soft_constraints = false): the constraints are
+ * the reference's NLopt inequality constraints g_c(T) = max_t
+ * |p^(soft_derivative[c])| - soft_limit[c] <= hard_tolerance
+ * (evaluateMaximumMagnitudeConstraint, :2687-2733); J carries no soft term
+ * and mtg_time_optimize accepts a trial only if it is feasible and lowers J,
+ * or, from an infeasible point, lowers the largest violation (feasibility
+ * first).  Only mtg_time_cost / mtg_time_optimize accept it; every other
+ * entry point returns MTG_ERR_INVALID_ARG for hard_constraints != 0.
  * grad_mode (grad may be NULL when 0):
  *   0  no gradient (objectiveFunctionTime is gradient-free, :881-882)
  *   1  getCostAndGradientTime (nonlinear_impl:2495-2584):
@@ -197,6 +205,11 @@ typedef struct mtg_time_params {
   double soft_limit[8];     /* maximum_value of constraint c, > 0 */
   double soft_weight;       /* ::soft_constraint_weight (100) */
   double soft_maximum_cost; /* maximum_cost (1e12, header :576) */
+  int hard_constraints;     /* 0: the n_soft constraints are soft costs
+                               (use_soft_constraints = true, the default);
+                               1: hard inequalities (use_soft_constraints =
+                               false, nonlinear_impl:861-872) */
+  double hard_tolerance;    /* ::inequality_constraint_tolerance (0.1) */
 } mtg_time_params;
 
 int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,

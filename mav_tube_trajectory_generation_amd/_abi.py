@@ -24,13 +24,17 @@ class TimeParams(ctypes.Structure):
                 ("w_d", ctypes.c_double), ("w_t", ctypes.c_double),
                 ("grad_mode", ctypes.c_int), ("n_soft", ctypes.c_int),
                 ("soft_derivative", ctypes.c_int * 8), ("soft_limit", ctypes.c_double * 8),
-                ("soft_weight", ctypes.c_double), ("soft_maximum_cost", ctypes.c_double)]
+                ("soft_weight", ctypes.c_double), ("soft_maximum_cost", ctypes.c_double),
+                ("hard_constraints", ctypes.c_int), ("hard_tolerance", ctypes.c_double)]
 
 
 def make_time_params(time_penalty=500.0, increment=0.1, w_d=0.1, w_t=1.0, grad_mode=0,
-                     soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12):
+                     soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12, hard=False,
+                     hard_tolerance=0.1):
     """soft: list of (derivative, maximum_value) magnitude constraints
-    (addMaximumMagnitudeConstraint), evaluated as soft costs."""
+    (addMaximumMagnitudeConstraint), evaluated as soft costs, or with
+    hard=True as hard inequalities max - value <= hard_tolerance
+    (use_soft_constraints = false)."""
     p = TimeParams(time_penalty, increment, w_d, w_t, grad_mode)
     soft = list(soft or [])
     if len(soft) > 8:
@@ -41,6 +45,8 @@ def make_time_params(time_penalty=500.0, increment=0.1, w_d=0.1, w_t=1.0, grad_m
         p.soft_limit[i] = float(v)
     p.soft_weight = soft_weight
     p.soft_maximum_cost = soft_maximum_cost
+    p.hard_constraints = 1 if hard else 0
+    p.hard_tolerance = hard_tolerance
     return p
 
 

@@ -158,7 +158,8 @@ class LinearPlan:
         return coeffs, cost, status
 
     def time_cost(self, fixed_vals, times, time_penalty=500.0, grad_mode=0, increment=0.1,
-                  w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0):
+                  w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0, hard=False,
+                  hard_tolerance=0.1):
         """objectiveFunctionTime per trajectory (mtg_time_cost); soft: list of
         (derivative, maximum_value) soft magnitude constraints."""
         import torch
@@ -169,14 +170,16 @@ class LinearPlan:
         cost = torch.empty(B, dtype=torch.float64, device=dev)
         grad = torch.empty((B, self.S), dtype=torch.float64, device=dev) if grad_mode else None
         status = torch.empty(B, dtype=torch.int32, device=dev)
-        p = make_time_params(time_penalty, increment, w_d, w_t, grad_mode, soft, soft_weight)
+        p = make_time_params(time_penalty, increment, w_d, w_t, grad_mode, soft, soft_weight,
+                             hard=hard, hard_tolerance=hard_tolerance)
         check(lib().mtg_time_cost(self._h, B, _ptr(fixed_vals), _ptr(times), ctypes.byref(p),
                                   _ptr(cost), _ptr(grad), _ptr(status), _stream(dev)),
               "mtg_time_cost")
         return dict(cost=cost, grad=grad, status=status)
 
     def time_optimize(self, fixed_vals, times, max_evals=50, time_penalty=500.0, increment=0.1,
-                      w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0):
+                      w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0, hard=False,
+                      hard_tolerance=0.1):
         """Optimise segment times in place on a copy; returns dict(times, cost,
         evals, solves, status); solves = inner solves run (gradient points
         included)."""
@@ -190,7 +193,8 @@ class LinearPlan:
         evals = torch.empty(B, dtype=torch.int32, device=dev)
         solves = torch.empty(B, dtype=torch.int32, device=dev)
         status = torch.empty(B, dtype=torch.int32, device=dev)
-        p = make_time_params(time_penalty, increment, w_d, w_t, 2, soft, soft_weight)
+        p = make_time_params(time_penalty, increment, w_d, w_t, 2, soft, soft_weight,
+                             hard=hard, hard_tolerance=hard_tolerance)
         check(lib().mtg_time_optimize(self._h, B, _ptr(fixed_vals), _ptr(t), ctypes.byref(p),
                                       max_evals, _ptr(cost), _ptr(evals), _ptr(solves),
                                       _ptr(status), _stream(dev)), "mtg_time_optimize")

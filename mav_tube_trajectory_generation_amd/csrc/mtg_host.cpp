@@ -455,8 +455,13 @@ int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* ti
 // CHECK_GE(derivative, 0), CHECK_GE(maximum_value, 0) (nonlinear_impl:849-850),
 // the POSITION..SNAP switch (:2697-2724), N - derivative - 1 > 0
 // (linear_impl:400) and a nonzero limit (the cost divides by it, :2754).
-static bool valid_soft(const mtg_plan* plan, const mtg_time_params* p) {
+// allow_hard: the entry point implements hard_constraints (mtg_time_cost /
+// mtg_time_optimize); elsewhere hard_constraints must be 0.
+static bool valid_soft(const mtg_plan* plan, const mtg_time_params* p, bool allow_hard = false) {
   if (p->n_soft < 0 || p->n_soft > mtg::kMaxSoftConstraints) return false;
+  if (p->hard_constraints != 0 && (!allow_hard || p->hard_constraints != 1)) return false;
+  if (p->hard_constraints && !(p->hard_tolerance >= 0.0 && p->hard_tolerance < 1e300))
+    return false;
   if (p->n_soft > 0 && plan->dev.S > 256) return false;
   for (int c = 0; c < p->n_soft; ++c) {
     const int k = p->soft_derivative[c];
@@ -526,7 +531,7 @@ int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times) return MTG_ERR_INVALID_ARG;
   if (params->grad_mode < 0 || params->grad_mode > 2) return MTG_ERR_INVALID_ARG;
   if (params->grad_mode && !(params->increment > 0)) return MTG_ERR_INVALID_ARG;
-  if (!valid_soft(plan, params)) return MTG_ERR_INVALID_ARG;
+  if (!valid_soft(plan, params, true)) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   return from_hip(mtg::launch_time_cost(plan->dev, B, fixed_vals, times, *params, cost, grad,
                                         status, static_cast<hipStream_t>(stream)));
@@ -539,7 +544,7 @@ int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
-  if (!valid_soft(plan, params)) return MTG_ERR_INVALID_ARG;
+  if (!valid_soft(plan, params, true)) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   return from_hip(mtg::launch_time_optimize(plan->dev, B, fixed_vals, times_io, *params,
                                             max_evals, cost, evals, solves, status,
@@ -602,6 +607,7 @@ int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* p
 
 static bool valid_tube_time_params(int N, int S, const mtg_time_params* p) {
   if (!p || p->n_soft < 0 || p->n_soft > mtg::kMaxSoftConstraints) return false;
+  if (p->hard_constraints != 0) return false;
   if (p->n_soft > 0 && S > 256) return false;
   for (int c = 0; c < p->n_soft; ++c) {
     const int k = p->soft_derivative[c];

@@ -145,7 +145,8 @@ __global__ void segment_matrices_kernel(int N, int r, int64_t n,
 // (objectiveFunctionTime, nonlinear_impl:877-945) with optional gradient.
 template <int N, bool kSoft>
 __device__ double objective_at(Traj<N>& t, const double* __restrict__ tab,
-                               const mtg_time_params& p, double* cbuf) {
+                               const mtg_time_params& p, double* cbuf, double* viol) {
+  *viol = 0.0;
   // Assumes T() holds the times; recomputes powers and re-solves.
   __syncthreads();
   t.compute_powers();
@@ -177,8 +178,12 @@ __device__ double objective_at(Traj<N>& t, const double* __restrict__ tab,
           lim = p.soft_limit[cc];
         }
       const double m = ext_trajectory_max_wave_k<N>(K, cbuf, t.T(), t.S, t.D, t.lane);
-      const double relative_violation = (m - lim) / lim;
-      soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
+      if (p.hard_constraints) {  // evaluateMaximumMagnitudeConstraint (:2687-2733)
+        *viol = fmax(*viol, m - lim - p.hard_tolerance);
+      } else {
+        const double relative_violation = (m - lim) / lim;
+        soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
+      }
     }
     J += soft;
   }
@@ -248,7 +253,8 @@ __global__ __launch_bounds__(kWave) void time_cost_kernel(
   int fl = 0;
   for (int e = 0; e < nevals; ++e) {
     if (e > 0) set_fd_point(t, Tb, e - 1, p.increment);
-    const double J = objective_at<N, kSoft>(t, tab, p, cbuf);
+    double viol;
+    const double J = objective_at<N, kSoft>(t, tab, p, cbuf, &viol);
     if (e == 0) {
       J0 = J;
       fl = t.flag()[0];
@@ -305,14 +311,16 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
   int phase = kBase, gi = 0, evals = 0, nsolve = 0;
-  double f = 0.0, Jlo = 0.0;
+  double f = 0.0, fv = 0.0, Jlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   int fl = 0;
   while (phase != kDone) {
-    const double J = objective_at<N, kSoft>(t, tab, p, cbuf);  // at T()
+    double viol;
+    const double J = objective_at<N, kSoft>(t, tab, p, cbuf, &viol);  // at T()
     ++nsolve;
     if (phase == kBase) {
       f = J;
+      fv = viol;
       evals = 1;
       fl = t.flag()[0];
       if (fl & 1) break;
@@ -327,8 +335,10 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
       if (++gi == 2 * S) phase = kTrial;
     } else {  // trial point
       ++evals;
-      if (J < f) {
+      // Feasibility first (hard constraints; viol is 0 otherwise).
+      if (viol == 0.0 ? (fv > 0.0 || J < f) : viol < fv) {
         f = J;
+        fv = viol;
         if (t.lane == 0)
           for (int i = 0; i < S; ++i) Tcur[i] = t.T()[i];
         alpha = fmin(alpha * 1.5, 1.0);

@@ -24,11 +24,15 @@ using StdSv = stdp::Solver<N, R, D>;
 // times T (LDS, S values).  Every lane calls it; returns the wave-uniform J
 // (NaN and *bad set when a time is invalid).  kSoft: the coefficients go to
 // cbuf (LDS) and evaluateMaximumMagnitudeAsSoftConstraint
-// (nonlinear_impl:2735-2766) runs one extremum search per constraint.
+// (nonlinear_impl:2735-2766) runs one extremum search per constraint; with
+// p.hard_constraints the searches give *viol = max(0, max_c (max_c - limit_c
+// - tolerance)) (evaluateMaximumMagnitudeConstraint, :2687-2733) instead of
+// a cost term.
 template <int N, int R, int D, bool kSoft>
 __device__ double std_objective(StdSv<N, R, D>& sv, const double* __restrict__ tab,
                                 const double* T, const mtg_time_params& p, double* cbuf,
-                                bool* bad, bool* not_spd) {
+                                bool* bad, bool* not_spd, double* viol) {
+  *viol = 0.0;
   __syncthreads();
   const bool b = sv.powers_from(T);
   __syncthreads();
@@ -56,8 +60,12 @@ __device__ double std_objective(StdSv<N, R, D>& sv, const double* __restrict__ t
           lim = p.soft_limit[cc];
         }
       const double m = ext_trajectory_max_wave_k<N>(K, cbuf, T, sv.S, D, sv.lane);
-      const double relative_violation = (m - lim) / lim;
-      soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
+      if (p.hard_constraints) {
+        *viol = fmax(*viol, m - lim - p.hard_tolerance);
+      } else {
+        const double relative_violation = (m - lim) / lim;
+        soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
+      }
     }
     J += soft;
   }
@@ -113,7 +121,8 @@ __global__ __launch_bounds__(kWave) void time_cost_std_kernel(
   bool bad = false, not_spd = false;
   for (int e = 0; e < nevals; ++e) {
     if (e > 0) std_set_fd_point(T, Tb, S, e - 1, p.increment, lane);
-    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd);
+    double viol;
+    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd, &viol);
     if (e == 0) {
       J0 = J;
       if (bad) break;
@@ -175,14 +184,16 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
   int phase = kBase, gi = 0, evals = 0, nsolve = 0;
-  double f = 0.0, Jlo = 0.0;
+  double f = 0.0, fv = 0.0, Jlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   bool bad = false, not_spd = false;
   while (phase != kDone) {
-    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd);
+    double viol;
+    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd, &viol);
     ++nsolve;
     if (phase == kBase) {
       f = J;
+      fv = viol;
       evals = 1;
       if (bad) break;
       phase = kGrad;
@@ -196,8 +207,10 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
       if (++gi == 2 * S) phase = kTrial;
     } else {  // trial point
       ++evals;
-      if (J < f) {
+      // Feasibility first (hard constraints; viol is 0 otherwise).
+      if (viol == 0.0 ? (fv > 0.0 || J < f) : viol < fv) {
         f = J;
+        fv = viol;
         for (int i = lane; i < S; i += kWave) Tcur[i] = T[i];
         alpha = fmin(alpha * 1.5, 1.0);
         phase = kGrad;

@@ -1177,6 +1177,8 @@ struct SoftSpec {
   const int* derivatives;
   const double* limits;
   double weight, maximum_cost;
+  bool hard = false;       // use_soft_constraints = false: inequality constraints
+  double tolerance = 0.0;  // inequality_constraint_tolerance
 };
 
 static int timeCostImpl(int N, int D, int r, int S, int K, const uint8_t* mask,
@@ -1745,13 +1747,25 @@ static int timeOptimizeImpl(int N, int D, int r, int S, int K, const uint8_t* ma
   LinearProblem lp;
   int rc = setupLinear(N, D, r, S, K, mask, vals, times_io, &lp);
   if (rc) return rc;
+  // Violation of the hard constraints at the last objective point:
+  // max(0, max_c (computeMaximumOfMagnitude - value - tolerance))
+  // (evaluateMaximumMagnitudeConstraint, nonlinear_impl:2687-2733).
+  double viol = 0.0;
   auto objective = [&](const std::vector<double>& t) {
     lp.updateSegmentTimes(t);
     lp.solveLinear();
     double total = 0.0;
     for (double v : t) total += v;
     double J = lp.computeCost() + total * total * time_penalty;
-    if (soft && soft->n > 0) {
+    viol = 0.0;
+    if (soft && soft->n > 0 && soft->hard) {
+      std::vector<double> mx(soft->n);
+      orc_soft_constraint_cost(N, D, S, lp.coeffs.data(), t.data(), soft->n, soft->derivatives,
+                               soft->limits, soft->weight, soft->maximum_cost, mx.data(),
+                               nullptr);
+      for (int c = 0; c < soft->n; ++c)
+        viol = std::max(viol, mx[c] - soft->limits[c] - soft->tolerance);
+    } else if (soft && soft->n > 0) {
       double c = 0.0;
       orc_soft_constraint_cost(N, D, S, lp.coeffs.data(), t.data(), soft->n, soft->derivatives,
                                soft->limits, soft->weight, soft->maximum_cost, nullptr, &c);
@@ -1773,6 +1787,7 @@ static int timeOptimizeImpl(int N, int D, int r, int S, int K, const uint8_t* ma
   const std::vector<double> T0(times_io, times_io + S);
   std::vector<double> T = T0, g(S), trial(S);
   double f = objective(T);
+  double fv = viol;
   gradient(T, &g);
   int n_eval = 1;
   double alpha = 0.1;
@@ -1788,10 +1803,13 @@ static int timeOptimizeImpl(int N, int D, int r, int S, int K, const uint8_t* ma
     }
     if (same) break;
     const double ft = objective(trial);
+    const double vt = viol;
     ++n_eval;
-    if (ft < f) {
+    // Feasibility first (hard constraints; the violation is 0 otherwise).
+    if (vt == 0.0 ? (fv > 0.0 || ft < f) : vt < fv) {
       T = trial;
       f = ft;
+      fv = vt;
       alpha = std::min(alpha * 1.5, 1.0);
       gradient(T, &g);
     } else {
@@ -1809,6 +1827,17 @@ int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
                       double increment, int max_evals, double* cost, int* evals) {
   return timeOptimizeImpl(N, D, r, S, K, mask, vals, times_io, time_penalty, increment,
                           max_evals, nullptr, cost, evals);
+}
+
+int orc_time_optimize_hard(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, double* times_io, double time_penalty,
+                           double increment, int max_evals, int n_con, const int* derivatives,
+                           const double* limits, double tolerance, double* cost, int* evals) {
+  SoftSpec hard{n_con, derivatives, limits, 100.0, 1.0e12};
+  hard.hard = true;
+  hard.tolerance = tolerance;
+  return timeOptimizeImpl(N, D, r, S, K, mask, vals, times_io, time_penalty, increment,
+                          max_evals, &hard, cost, evals);
 }
 
 int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mask,

@@ -204,6 +204,13 @@ int orc_time_cost_soft(int N, int D, int r, int S, int K, const uint8_t* mask,
                        const int* soft_derivatives, const double* soft_limits,
                        double soft_weight, double soft_maximum_cost, double* cost,
                        double* grad);
+// The optimiser with hard inequality constraints (use_soft_constraints =
+// false, nonlinear_impl:861-872): g_c = max |p^(derivatives[c])| - limits[c]
+// <= tolerance, accepted trials feasible-and-lower or less infeasible.
+int orc_time_optimize_hard(int N, int D, int r, int S, int K, const uint8_t* mask,
+                           const double* vals, double* times_io, double time_penalty,
+                           double increment, int max_evals, int n_con, const int* derivatives,
+                           const double* limits, double tolerance, double* cost, int* evals);
 int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mask,
                            const double* vals, double* times_io, double time_penalty,
                            double increment, int max_evals, int n_soft,

@@ -187,15 +187,27 @@ def time_cost(N, r, vertices, times, time_penalty=500.0, grad_mode=0, increment=
 
 
 def time_optimize(N, r, vertices, times, max_evals, time_penalty=500.0, increment=0.1,
-                  soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12):
-    """orc_time_optimize(_soft): the mtg_time_optimize algorithm on the oracle
-    objective.  Returns (times, cost, evals)."""
+                  soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12, hard=False,
+                  hard_tolerance=0.1):
+    """orc_time_optimize(_soft / _hard): the mtg_time_optimize algorithm on
+    the oracle objective.  Returns (times, cost, evals)."""
     S, D, K = vertices.S, vertices.D, vertices.K
     t = np.array(times, dtype=np.float64)
     cost = np.zeros(1)
     evals = ctypes.c_int()
     L = lib()
-    if soft:
+    if soft and hard:
+        der = np.ascontiguousarray([d for d, _ in soft], dtype=np.int32)
+        lim = np.ascontiguousarray([v for _, v in soft], dtype=np.float64)
+        L.orc_time_optimize_hard.argtypes = [ctypes.c_int] * 5 + [
+            _u8p, _dp, _dp, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int, _ip,
+            _dp, ctypes.c_double, _dp, _ip]
+        _check(L.orc_time_optimize_hard(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                        _d(vertices.vals), _d(t), time_penalty, increment,
+                                        max_evals, len(der), der.ctypes.data_as(_ip), _d(lim),
+                                        hard_tolerance, _d(cost), ctypes.byref(evals)),
+               "time_optimize_hard")
+    elif soft:
         der = np.ascontiguousarray([d for d, _ in soft], dtype=np.int32)
         lim = np.ascontiguousarray([v for _, v in soft], dtype=np.float64)
         L.orc_time_optimize_soft.argtypes = [ctypes.c_int] * 5 + [

@@ -696,11 +696,27 @@ TEST(gpu, SoftConstraintTimeCost) {
   EXPECT_LE(relErr(J1, info.cost_trajectory + info.cost_time + info.cost_soft_constraints),
             1e-9);
   EXPECT_TRUE(info.maxima.count(derivative_order::VELOCITY) == 1);
-  // Hard constraints are not available.
+  // Hard constraints (use_soft_constraints = false, nonlinear_impl:861-872):
+  // the objective has no soft term, a feasible start stays feasible.
   NonlinearOptimizationParameters hard = p;
   hard.use_soft_constraints = false;
   PolynomialOptimizationNonLinear<10> opt2(f.D, hard);
-  EXPECT_TRUE(!opt2.addMaximumMagnitudeConstraint(derivative_order::VELOCITY, 3.0));
+  opt2.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}),
+                         4);
+  opt2.solveLinear();
+  const double vmax0 =
+      opt2.getPolynomialOptimizationRef().computeMaximumOfMagnitude(1, nullptr).value;
+  EXPECT_TRUE(opt2.addMaximumMagnitudeConstraint(derivative_order::VELOCITY, 1.01 * vmax0));
+  double Jplain = 0.0;
+  EXPECT_TRUE(orc_time_cost(10, f.D, f.r, f.S, 5, d.mask.data(), d.vals.data(), times.data(),
+                            p.time_penalty, 0, p.increment_time, p.weights.w_d, p.weights.w_t,
+                            &Jplain, nullptr) == 0);
+  EXPECT_LE(relErr(opt2.evaluateTimeCost(times), Jplain), 1e-9);
+  EXPECT_TRUE(opt2.optimize() > 0);
+  const double vmax1 =
+      opt2.getPolynomialOptimizationRef().computeMaximumOfMagnitude(1, nullptr).value;
+  EXPECT_LE(vmax1, 1.01 * vmax0 + hard.inequality_constraint_tolerance + 1e-9);
+  EXPECT_TRUE(opt2.getOptimizationInfo().cost_soft_constraints == 0.0);
 }
 
 }  // namespace

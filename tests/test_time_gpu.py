@@ -205,3 +205,64 @@ def test_time_soft_rejects_bad_constraints(ctx, dev, kernel):
     for soft in ([(5, 1.0)], [(1, 0.0)], [(-1, 1.0)], [(1, 1.0)] * 9):
         with pytest.raises(MTGError):
             plan.time_cost(fd, td, soft=soft)
+
+
+@pytest.mark.parametrize("start", ["feasible", "infeasible"])
+def test_time_optimize_hard_constraints_vs_oracle(ctx, dev, oracle, kernel, start):
+    """use_soft_constraints = false (nonlinear_impl:861-872): the magnitude
+    constraints are inequalities max |p^(k)| - limit <= tolerance
+    (evaluateMaximumMagnitudeConstraint, :2687-2733).  The device optimiser
+    takes the oracle port's steps (orc_time_optimize_hard: feasible trials
+    must lower J; from an infeasible start the largest violation must drop);
+    a feasible start stays feasible.  The cost carries no soft term."""
+    import mav_tube_trajectory_generation_amd as mtg
+    S, B, E, tol = 6, 6, 20, 0.1
+    scale = 1.02 if start == "feasible" else 0.9
+    mask, fixed, times, _ = _batch(S, B, 960)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    agree = 0
+    for b in range(B):
+        v = standard_vertices(N, S, D, 960 + b)
+        c0 = oracle.linear_solve(N, R, v, times[b])["coeffs"]
+        lims = [(1, scale * oracle.max_magnitude(N, c0, times[b], 1)["value"]),
+                (2, scale * oracle.max_magnitude(N, c0, times[b], 2)["value"])]
+        J0 = plan.time_cost(fd[b:b + 1], td[b:b + 1], soft=lims, hard=True,
+                            hard_tolerance=tol)["cost"].cpu().numpy()[0]
+        Jp, _ = oracle.time_cost(N, R, v, times[b])
+        assert rel_err(J0, Jp) <= 1e-9  # no soft term
+        out = plan.time_optimize(fd[b:b + 1], td[b:b + 1], max_evals=E, soft=lims, hard=True,
+                                 hard_tolerance=tol)
+        T = out["times"].cpu().numpy()[0]
+        Tc, fc, ec = oracle.time_optimize(N, R, v, times[b], E, soft=lims, hard=True,
+                                          hard_tolerance=tol)
+        c1 = oracle.linear_solve(N, R, v, T)["coeffs"]
+        viol = max(oracle.max_magnitude(N, c1, T, k)["value"] - lim - tol for k, lim in lims)
+        if start == "feasible":
+            assert viol <= 1e-9, viol
+        if int(out["evals"][0]) == ec and np.max(np.abs(T - Tc) / Tc) <= 1e-6:
+            assert rel_err(float(out["cost"][0]), fc) <= 1e-6
+            agree += 1
+    assert agree >= B - 1, agree
+
+
+def test_hard_constraints_only_where_implemented(ctx, dev):
+    import mav_tube_trajectory_generation_amd as mtg
+    from mav_tube_trajectory_generation_amd._abi import MTGError
+    S = 4
+    mask, fixed, times, _ = _batch(S, 1, 5)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    dp = torch.zeros((1, D, plan.n_free), dtype=torch.float64, device=dev)
+    from mav_tube_trajectory_generation_amd._abi import check, lib, make_time_params
+    import ctypes
+    p = make_time_params(soft=[(1, 3.0)], hard=True)
+    cost = torch.empty(1, dtype=torch.float64, device=dev)
+    rc = lib().mtg_free_cost(plan._h, 1, ctypes.c_void_p(fd.data_ptr()),
+                             ctypes.c_void_p(dp.data_ptr()), ctypes.c_void_p(td.data_ptr()),
+                             ctypes.byref(p), 1, ctypes.c_void_p(cost.data_ptr()), None, None,
+                             None)
+    assert rc == -1  # MTG_ERR_INVALID_ARG
+    with pytest.raises(MTGError):
+        plan.time_cost(fd, td, soft=[(1, 3.0)], hard=True, hard_tolerance=-1.0)
+    check(0, "ok")
