@@ -384,6 +384,73 @@ class PolynomialOptimizationNonLinear {
     }
   }
 
+  // Occupancy map for the collision cost (build extension standing in for
+  // setOctree, polynomial_optimization_nonlinear.h:357-363; supereight is
+  // absent): a dense grid of log-odds, voxel (x, y, z) at (z*ny + y)*nx + x,
+  // occupied iff >= 0, uploaded once.
+  void setOccupancyGrid(const std::vector<float>& occupancy, int nx, int ny, int nz) {
+    MTG_CHECK(static_cast<size_t>(nx) * ny * nz == occupancy.size(), "grid size mismatch");
+    occ_dims_[0] = nx;
+    occ_dims_[1] = ny;
+    occ_dims_[2] = nz;
+    occupancy_.upload(occupancy);
+  }
+
+  // getCostAndGradientCollision (nonlinear_impl:1609-1780) of the tube-pattern
+  // problem's current solution (poly_opt_, as the reference) on the device
+  // (mtg_collision_cost); gradient (nullable) w.r.t. its free derivatives.
+  double getCostAndGradientCollision(std::vector<VectorXd>* gradients, bool* is_collision) {
+    MTG_CHECK(is_collision != nullptr, "is_collision must not be null");
+    MTG_CHECK(occupancy_.size() > 0 || occ_dims_[0] == 0, "setOccupancyGrid first");
+    Trajectory traj;
+    poly_opt_.getTrajectory(&traj);
+    const int S = traj.K(), D = traj.D();
+    MTG_CHECK(D == 3, "the collision cost is 3-D (nonlinear_impl:1796-1797)");
+    std::vector<double> coeffs(static_cast<size_t>(S) * D * N);
+    for (int s = 0; s < S; ++s)
+      for (int d = 0; d < D; ++d) {
+        const VectorXd c = traj.segments()[s][d].getCoefficients(0);
+        for (int k = 0; k < N; ++k) coeffs[(static_cast<size_t>(s) * D + d) * N + k] = c[k];
+      }
+    mtg_collision_params cp;
+    cp.map_resolution = params_.map_resolution;
+    for (int k = 0; k < 3; ++k) {
+      cp.min_bound[k] = params_.min_bound[k];
+      cp.max_bound[k] = params_.max_bound[k];
+    }
+    cp.epsilon = params_.epsilon;
+    cp.robot_radius = params_.robot_radius;
+    cp.coll_pot_multiplier = params_.coll_pot_multiplier;
+    cp.coll_check_time_increment = params_.coll_check_time_increment;
+    cp.box_side = 20;
+    const size_t np = poly_opt_.getNumberFreeConstraints();
+    internal::DeviceBuffer<double> d_c, d_t, d_cost(1), d_g(np ? D * np : 1);
+    internal::DeviceBuffer<int32_t> d_coll(1);
+    d_c.upload(coeffs);
+    d_t.upload(traj.getSegmentTimes());
+    internal::checkStatus(
+        mtg_collision_cost(poly_opt_.getPlan(), 1, d_c.get(), d_t.get(), occupancy_.get(),
+                           occ_dims_[0], occ_dims_[1], occ_dims_[2], &cp, d_cost.get(),
+                           d_coll.get(), nullptr, (gradients && np) ? d_g.get() : nullptr,
+                           nullptr),
+        "mtg_collision_cost");
+    internal::synchronize();
+    double J = 0.0;
+    int32_t coll = 0;
+    d_cost.download(&J, 1);
+    d_coll.download(&coll, 1);
+    *is_collision = coll != 0;
+    if (gradients) {
+      gradients->assign(D, VectorXd(static_cast<long>(np)));
+      if (np) {
+        const std::vector<double> g = d_g.download();
+        for (int d = 0; d < D; ++d)
+          for (size_t i = 0; i < np; ++i) (*gradients)[d][i] = g[d * np + i];
+      }
+    }
+    return J;
+  }
+
   // nonlinear_impl:2768-2774.
   static double computeTotalTrajectoryTime(const std::vector<double>& segment_times) {
     double t = 0.0;
@@ -649,6 +716,8 @@ class PolynomialOptimizationNonLinear {
   Trajectory trajectory_initial_;
   OptimizationInfo optimization_info_;
   std::vector<std::pair<int, double>> soft_;  // (derivative, maximum_value)
+  internal::DeviceBuffer<float> occupancy_;
+  int occ_dims_[3] = {0, 0, 0};
   bool free_optimized_ = false;
   bool qcqp_time_optimized_ = false;
 };

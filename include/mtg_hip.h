@@ -457,6 +457,40 @@ int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeff
                              double* maxima, double* cost, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Collision cost over an occupancy map: getCostAndGradientCollision
+ * (nonlinear_impl:1609-1780) with getCostAndGradientPotentialOctree
+ * (:1782-1917), the nearest-occupied-voxel search of findOccupiedVoxels /
+ * getDistanceOctree (:1920-2043) and getCostPotential (:2660-2684).  The
+ * reference reads a supereight octree (absent; parity unpinned); here the
+ * map is a caller-supplied dense grid `occupancy` (device, nx*ny*nz floats,
+ * voxel (x, y, z) at (z*ny + y)*nx + x, occupied iff the log-odds value is
+ * >= 0; voxels outside the grid are free).  A position maps to voxel
+ * (position / map_resolution) truncated toward zero (:1815).
+ * Per trajectory (D = 3): sample every coll_check_time_increment from each
+ * segment's start; once the path length since the last evaluation reaches
+ * map_resolution, add c(p) |v| time_sum, c = getCostPotential(distance to
+ * the nearest occupied voxel in the box_side^3 box around p - robot_radius).
+ * A collision (that distance <= 0, or p within one voxel of
+ * [min_bound, max_bound]) stops the walk: cost 0, collision 1, zero
+ * gradient.  Outputs (device, each nullable): cost B, collision B,
+ * grad_coeffs B x S x 3 x N (dJ_c/dc, the eq. (14) terms per coefficient),
+ * grad_free B x 3 x n_free (dJ_c/dd_p through L = A^-1 M, :1650-1656).
+ * coeffs B x S x 3 x N and times B x S as mtg_linear_solve writes them. */
+typedef struct mtg_collision_params {
+  double map_resolution;            /* ::map_resolution (voxel edge, m) */
+  double min_bound[3], max_bound[3]; /* ::min_bound / ::max_bound (m) */
+  double epsilon;                   /* ::epsilon (0.5) obstacle clearance */
+  double robot_radius;              /* ::robot_radius (0.5) */
+  double coll_pot_multiplier;       /* ::coll_pot_multiplier (1.0) */
+  double coll_check_time_increment; /* ::coll_check_time_increment (0.1) */
+  int box_side;                     /* findOccupiedVoxels side (20, :1797) */
+} mtg_collision_params;
+int mtg_collision_cost(const mtg_plan* plan, int64_t B, const double* coeffs,
+                       const double* times, const float* occupancy, int nx, int ny, int nz,
+                       const mtg_collision_params* params, double* cost, int32_t* collision,
+                       double* grad_coeffs, double* grad_free, void* stream);
+
+/* ------------------------------------------------------------------------
  * Host-side input generation (vertex.cpp:27-82, 228-269) for batches:
  * trajectory b uses createRandomVertices(max_derivative = M-1, S, +/-pos_bound,
  * seed = seed0 + b) and estimateSegmentTimes(v_max, a_max) (Nfabian, 6.5).

@@ -18,6 +18,23 @@ _ip = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
 
 
+class CollisionParams(ctypes.Structure):
+    """mtg_collision_params (include/mtg_hip.h)."""
+    _fields_ = [("map_resolution", ctypes.c_double), ("min_bound", ctypes.c_double * 3),
+                ("max_bound", ctypes.c_double * 3), ("epsilon", ctypes.c_double),
+                ("robot_radius", ctypes.c_double), ("coll_pot_multiplier", ctypes.c_double),
+                ("coll_check_time_increment", ctypes.c_double), ("box_side", ctypes.c_int)]
+
+
+def make_collision_params(map_resolution, min_bound, max_bound, epsilon=0.5, robot_radius=0.5,
+                          coll_pot_multiplier=1.0, coll_check_time_increment=0.1, box_side=20):
+    """NonlinearOptimizationParameters' collision fields (defaults of
+    polynomial_optimization_nonlinear.h:46-84; side 20 of :1797)."""
+    return CollisionParams(map_resolution, (ctypes.c_double * 3)(*min_bound),
+                           (ctypes.c_double * 3)(*max_bound), epsilon, robot_radius,
+                           coll_pot_multiplier, coll_check_time_increment, box_side)
+
+
 class TimeParams(ctypes.Structure):
     """mtg_time_params (include/mtg_hip.h)."""
     _fields_ = [("time_penalty", ctypes.c_double), ("increment", ctypes.c_double),
@@ -73,6 +90,10 @@ SIGNATURES = {
                                               ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
                                               _vp, _vp, _vp]),
     "mtg_plan_kernel": (ctypes.c_int, [_vp]),
+    "mtg_collision_cost": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(CollisionParams), _vp, _vp, _vp, _vp,
+                                          _vp]),
     "mtg_min_max_magnitude": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp, _vp,
                                              _vp, _vp, _vp, _vp, _vp]),

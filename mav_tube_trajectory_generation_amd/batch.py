@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import MTGError, check, lib, make_time_params
+from ._abi import MTGError, check, lib, make_collision_params, make_time_params  # noqa: F401
 
 
 def _ptr(t):
@@ -266,6 +266,33 @@ class LinearPlan:
                                            ctypes.byref(p), max_evals, _ptr(cost), _ptr(evals),
                                            _ptr(status), _stream(dev)), "mtg_time_free_optimize")
         return dict(times=t, free=d, cost=cost, evals=evals, status=status)
+
+    def collision_cost(self, coeffs, times, occupancy, params, grad=True):
+        """Collision cost over a dense occupancy grid (mtg_collision_cost,
+        getCostAndGradientCollision): coeffs [B, S, 3, N], times [B, S],
+        occupancy float32 CUDA tensor [nz, ny, nx] (occupied iff >= 0),
+        params from make_collision_params.  Returns dict(cost, collision,
+        grad_coeffs, grad_free)."""
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(coeffs, (B, self.S, self.D, self.N), "coeffs")
+        if not (isinstance(occupancy, torch.Tensor) and occupancy.is_cuda and
+                occupancy.dtype == torch.float32 and occupancy.dim() == 3 and
+                occupancy.is_contiguous()):
+            raise MTGError("occupancy must be a contiguous float32 CUDA tensor [nz, ny, nx]")
+        nz, ny, nx = occupancy.shape
+        dev = times.device
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        coll = torch.empty(B, dtype=torch.int32, device=dev)
+        gc = torch.empty((B, self.S, self.D, self.N), dtype=torch.float64, device=dev) \
+            if grad else None
+        gf = torch.empty((B, self.D, self.n_free), dtype=torch.float64, device=dev) \
+            if grad else None
+        check(lib().mtg_collision_cost(self._h, B, _ptr(coeffs), _ptr(times), _ptr(occupancy),
+                                       nx, ny, nz, ctypes.byref(params), _ptr(cost), _ptr(coll),
+                                       _ptr(gc), _ptr(gf), _stream(dev)), "mtg_collision_cost")
+        return dict(cost=cost, collision=coll, grad_coeffs=gc, grad_free=gf)
 
     # -- host (numpy) API ---------------------------------------------------
     def solve_host(self, fixed_vals, times):

@@ -392,6 +392,25 @@ int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                                             static_cast<hipStream_t>(stream)));
 }
 
+int mtg_collision_cost(const mtg_plan* plan, int64_t B, const double* coeffs,
+                       const double* times, const float* occupancy, int nx, int ny, int nz,
+                       const mtg_collision_params* params, double* cost, int32_t* collision,
+                       double* grad_coeffs, double* grad_free, void* stream) {
+  if (!plan || !params || B < 0 || B > 0x7fffffff || plan->dev.D != 3) return MTG_ERR_INVALID_ARG;
+  const mtg_collision_params& p = *params;
+  if (!(p.map_resolution > 0.0) || !(p.epsilon > 0.0) || !(p.coll_check_time_increment > 0.0) ||
+      !(p.robot_radius >= 0.0) || p.box_side < 1 || p.box_side > 256 || nx < 0 || ny < 0 ||
+      nz < 0)
+    return MTG_ERR_INVALID_ARG;
+  if (mtg::collision_lds_bytes(plan->dev.N, plan->dev.S) > 65536) return MTG_ERR_UNSUPPORTED;
+  if (B == 0) return MTG_OK;
+  if (!coeffs || !times || (!occupancy && static_cast<int64_t>(nx) * ny * nz > 0))
+    return MTG_ERR_INVALID_ARG;
+  return from_hip(mtg::launch_collision_cost(plan->dev, B, coeffs, times, occupancy, nx, ny, nz,
+                                             p, cost, collision, grad_coeffs, grad_free,
+                                             static_cast<hipStream_t>(stream)));
+}
+
 int mtg_min_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                           const double* times, int derivative, double* min_time,
                           double* min_value, int32_t* min_segment, double* max_time,

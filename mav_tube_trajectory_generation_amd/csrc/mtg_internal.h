@@ -155,6 +155,13 @@ struct SoftCostArgs {
   SoftLimits lim;
   double weight, maximum_cost;
 };
+// Collision cost over a dense occupancy grid (mtg_collision.hip).
+size_t collision_lds_bytes(int N, int S);
+hipError_t launch_collision_cost(const PlanDev& pl, int64_t B, const double* coeffs,
+                                 const double* times, const float* occ, int nx, int ny, int nz,
+                                 const mtg_collision_params& p, double* cost, int32_t* coll,
+                                 double* grad_coeffs, double* grad_free, hipStream_t st);
+
 // Minimum outputs of mtg_min_max_magnitude (each nullable).
 struct MinOut {
   double* time;

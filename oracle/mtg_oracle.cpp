@@ -9,6 +9,7 @@
 #include "mtg_oracle.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <thread>
@@ -2334,6 +2335,183 @@ int orc_time_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mas
   std::memcpy(dp_io, d.data(), sizeof(double) * n);
   if (cost) *cost = f;
   if (evals) *evals = n_eval;
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// Collision cost over a dense occupancy grid, restating
+// getCostAndGradientCollision (nonlinear_impl:1609-1780) and
+// getCostAndGradientPotentialOctree (:1782-1917) with the supereight octree
+// replaced by a dense grid (occupied iff value >= 0, :2022-2027):
+// findOccupiedVoxels (:1920-2018) keeps the voxels whose unit box overlaps the
+// side^3 box at position_voxel - side/2 (supereight aabb_aabb_collision, the
+// inclusive half-plane test !((a + a_edge < b) || (b + b_edge < a)));
+// getDistanceOctree (:2031-2043) and getCostPotential (:2660-2684) as written.
+// Coefficients from d_f and the given d_p (L = A^-1 M, :1650-1656), T and V
+// by explicit powers and the derivative map (:1686-1706), eq. (14) gradient
+// with T_all L_pp and T_all V_all L_pp (:1729-1747).
+namespace {
+struct CollMap {
+  const float* occ;
+  int nx, ny, nz;
+  const double* prm;  // res, min[3], max[3], eps, radius, mult, dt
+  int side;
+  bool occupied(int x, int y, int z) const {
+    if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) return false;
+    return occ[(static_cast<size_t>(z) * ny + y) * nx + x] >= 0.0f;
+  }
+};
+
+double costPotential(double d, const double* prm, bool* coll) {
+  const double eps = prm[7], radius = prm[8], mult = prm[9];
+  *coll = false;
+  d -= radius;
+  if (d <= 0.0) {
+    *coll = true;
+    return mult * (-d) + 0.5 * eps;
+  }
+  if (d <= eps) return 0.5 * 1.0 / eps * (d - eps) * (d - eps);
+  return 0.0;
+}
+
+bool axisOverlap(int a, int a_edge, int b, int b_edge) {
+  return !((a + a_edge < b) || (b + b_edge < a));
+}
+
+// getCostAndGradientPotentialOctree on the dense map.
+double potentialAt(const CollMap& mp, const double pos[3], double grad[3], bool* coll) {
+  const double res = mp.prm[0];
+  bool valid = true;
+  for (int k = 0; k < 3; ++k)
+    if (pos[k] < mp.prm[1 + k] + res || pos[k] > mp.prm[4 + k] - res) valid = false;
+  int v[3];
+  for (int k = 0; k < 3; ++k) v[k] = static_cast<int>(pos[k] / res);
+  std::vector<std::array<int, 3>> occupied;
+  const int half = mp.side / 2;
+  for (int z = v[2] - half - 1; z <= v[2] - half + mp.side; ++z)
+    for (int y = v[1] - half - 1; y <= v[1] - half + mp.side; ++y)
+      for (int x = v[0] - half - 1; x <= v[0] - half + mp.side; ++x) {
+        if (!(axisOverlap(v[0] - half, mp.side, x, 1) && axisOverlap(v[1] - half, mp.side, y, 1) &&
+              axisOverlap(v[2] - half, mp.side, z, 1)))
+          continue;
+        if (mp.occupied(x, y, z)) occupied.push_back({x, y, z});
+      }
+  auto distance = [&](const int c[3]) {
+    double m = std::numeric_limits<double>::max();
+    for (const auto& o : occupied) {
+      const double dx = o[0] - c[0], dy = o[1] - c[1], dz = o[2] - c[2];
+      const double l = std::sqrt(dx * dx + dy * dy + dz * dz);
+      if (l < m) m = l;
+    }
+    return m * res;
+  };
+  double dist = 0.0;
+  if (valid) dist = distance(v);
+  const double J = costPotential(dist, mp.prm, coll);
+
+  if (!*coll && grad)
+    for (int k = 0; k < 3; ++k) {
+      int lo[3] = {v[0], v[1], v[2]}, hi[3] = {v[0], v[1], v[2]};
+      lo[k] -= 1;
+      hi[k] += 1;
+      bool cl, cr;
+      const double l = costPotential(valid ? distance(lo) : 0.0, mp.prm, &cl);
+      const double r = costPotential(valid ? distance(hi) : 0.0, mp.prm, &cr);
+      grad[k] = (r - l) / (2.0 * res);
+    }
+  return J;
+}
+}  // namespace
+
+int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times, const double* dp,
+                       const float* occupancy, int nx, int ny, int nz, const double* params,
+                       int box_side, double* cost, int* collision, double* grad_coeffs,
+                       double* grad_free) {
+  if (D != 3 || !params) return -1;
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
+  if (rc) return rc;
+  const int nf = lp.nf, np = lp.np, nall = nf + np;
+  if (np > 0 && !dp) return -1;
+  for (int d = 0; d < D; ++d)
+    for (int i = 0; i < np; ++i) lp.dp[d][i] = dp[d * np + i];
+  lp.updateSegmentsFromCompactConstraints();
+  // L = blockdiag(A_s^-1) M (n_all x (nf + np)).
+  Mat L(S * N, nall);
+  for (int s = 0; s < S; ++s)
+    for (int a = 0; a < N; ++a)
+      for (int j = 0; j < nall; ++j) {
+        double v = 0.0;
+        for (int b = 0; b < N; ++b) v += lp.Ainv[s](a, b) * lp.M(s * N + b, j);
+        L(s * N + a, j) = v;
+      }
+  const CollMap mp{occupancy, nx, ny, nz, params, box_side};
+  const double res = params[0], dt = params[10];
+  std::vector<double> gc(static_cast<size_t>(S) * D * N, 0.0), gf(static_cast<size_t>(D) * np, 0.0);
+  double J = 0.0;
+  bool is_coll = false;
+  double prev[3] = {0, 0, 0}, time_sum = -1.0, dist_sum = 0.0, t = 0.0;
+  for (int i = 0; i < S && !is_coll; ++i) {
+    for (t = 0.0; t < times[i]; t += dt) {
+      double T[32], pos[3] = {0, 0, 0}, vel[3] = {0, 0, 0};
+      for (int n = 0; n < N; ++n) T[n] = std::pow(t, n);
+      for (int k = 0; k < D; ++k) {
+        const double* c = lp.coeffs.data() + (static_cast<size_t>(i) * D + k) * N;
+        for (int n = 0; n < N; ++n) pos[k] += T[n] * c[n];
+        for (int n = 0; n + 1 < N; ++n) vel[k] += T[n] * (n + 1) * c[n + 1];  // T V p
+      }
+      if (time_sum < 0) {
+        time_sum = 0.0;
+        for (int k = 0; k < 3; ++k) prev[k] = pos[k];
+        continue;
+      }
+      time_sum += dt;
+      double dd = 0.0;
+      for (int k = 0; k < 3; ++k) dd += (pos[k] - prev[k]) * (pos[k] - prev[k]);
+      dist_sum += std::sqrt(dd);
+      for (int k = 0; k < 3; ++k) prev[k] = pos[k];
+      if (dist_sum < res) continue;
+      bool pc = false;
+      double gpot[3] = {0, 0, 0};
+      const double c = potentialAt(mp, pos, gpot, &pc);
+      if (pc) {
+        is_coll = true;
+        break;
+      }
+      const double vn = std::sqrt(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
+      J += c * vn * time_sum;
+      if (vn > 1e-6) {
+        // rows T_all L_pp and T_all V_all L_pp of eq. (14)
+        std::vector<double> rT(np, 0.0), rV(np, 0.0);
+        for (int p2 = 0; p2 < np; ++p2)
+          for (int n = 0; n < N; ++n) {
+            rT[p2] += T[n] * L(i * N + n, nf + p2);
+            if (n + 1 < N) rV[p2] += T[n] * (n + 1) * L(i * N + n + 1, nf + p2);
+          }
+        for (int k = 0; k < D; ++k) {
+          const double a = vn * time_sum * gpot[k], bc = time_sum * c * vel[k] / vn;
+          for (int p2 = 0; p2 < np; ++p2) gf[k * np + p2] += a * rT[p2] + bc * rV[p2];
+          for (int n = 0; n < N; ++n)
+            gc[(static_cast<size_t>(i) * D + k) * N + n] +=
+                a * T[n] + bc * (n > 0 ? n * T[n - 1] : 0.0);
+        }
+      }
+      dist_sum = 0.0;
+      time_sum = 0.0;
+    }
+    if (is_coll) break;
+    time_sum += -dt + (times[i] - t);
+  }
+  if (is_coll) {
+    J = 0.0;
+    std::fill(gc.begin(), gc.end(), 0.0);
+    std::fill(gf.begin(), gf.end(), 0.0);
+  }
+  if (cost) *cost = J;
+  if (collision) *collision = is_coll ? 1 : 0;
+  if (grad_coeffs) std::memcpy(grad_coeffs, gc.data(), sizeof(double) * gc.size());
+  if (grad_free) std::memcpy(grad_free, gf.data(), sizeof(double) * gf.size());
   return 0;
 }
 

@@ -260,6 +260,17 @@ int orc_time_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mas
                            double soft_weight, double soft_maximum_cost, int max_evals,
                            double* cost, int* evals);
 
+// Collision cost of getCostAndGradientCollision (nonlinear_impl:1609-1780)
+// over a dense occupancy grid (see mtg_oracle.cpp).  dp: D x np (D = 3);
+// params: res, min_bound[3], max_bound[3], epsilon, robot_radius,
+// coll_pot_multiplier, coll_check_time_increment.  grad_coeffs S x D x N,
+// grad_free D x np (nullable).
+int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times, const double* dp,
+                       const float* occupancy, int nx, int ny, int nz, const double* params,
+                       int box_side, double* cost, int* collision, double* grad_coeffs,
+                       double* grad_free);
+
 #ifdef __cplusplus
 }
 #endif

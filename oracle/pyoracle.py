@@ -498,3 +498,33 @@ def time_free_optimize(N, r, vertices, times, dp0, max_evals, time_penalty=500.0
                                     soft_maximum_cost, max_evals, _d(cost), ctypes.byref(evals)),
            "time_free_optimize")
     return t, dp, float(cost[0]), evals.value
+
+
+def collision_cost(N, r, vertices, times, dp, occupancy, params, box_side=20):
+    """orc_collision_cost: getCostAndGradientCollision on a dense grid.
+    occupancy: float32 [nz, ny, nx]; params: dict of map_resolution,
+    min_bound[3], max_bound[3], epsilon, robot_radius, coll_pot_multiplier,
+    coll_check_time_increment.  Returns (J, collision, grad_coeffs [S, D, N],
+    grad_free [D, np])."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    occ = np.ascontiguousarray(occupancy, dtype=np.float32)
+    nz, ny, nx = occ.shape
+    prm = np.array([params["map_resolution"], *params["min_bound"], *params["max_bound"],
+                    params["epsilon"], params["robot_radius"], params["coll_pot_multiplier"],
+                    params["coll_check_time_increment"]], dtype=np.float64)
+    dp = np.ascontiguousarray(dp, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    cost = np.zeros(1)
+    coll = ctypes.c_int()
+    gc = np.zeros((S, D, N))
+    gf = np.zeros(dp.shape)
+    L = lib()
+    L.orc_collision_cost.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int,
+        ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.POINTER(ctypes.c_int), _dp, _dp]
+    _check(L.orc_collision_cost(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                _d(vertices.vals), _d(times), _d(dp),
+                                occ.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), nx, ny, nz,
+                                _d(prm), box_side, _d(cost), ctypes.byref(coll), _d(gc), _d(gf)),
+           "collision_cost")
+    return float(cost[0]), coll.value, gc, gf

@@ -938,6 +938,53 @@ TEST(gpu, PrintMatlabSampledTrajectory) {
   }
 }
 
+// getCostAndGradientCollision (nonlinear_impl:1609-1780) through the shim on
+// a dense occupancy grid (setOccupancyGrid) vs the oracle restatement.
+TEST(gpu, CollisionCostMatchesOracle) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> times = estimateSegmentTimes(vs, 2.0, 2.0);
+  NonlinearOptimizationParameters p;
+  p.map_resolution = 0.05;
+  p.min_bound = VectorXd::Constant(3, 0.0);
+  p.max_bound = VectorXd::Constant(3, 16.0);
+  p.robot_radius = 0.1;
+  PolynomialOptimizationNonLinear<10> opt(3, p);
+  opt.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(4, {0.15, 0.15}), 4);
+  EXPECT_TRUE(opt.solveQCQP() == 0);
+  const int n = 320;
+  std::vector<float> occ(static_cast<size_t>(n) * n * n, -1.0f);
+  std::mt19937 gen(11);
+  std::uniform_int_distribution<int> u(0, n - 1);
+  for (int i = 0; i < 200000; ++i) occ[(static_cast<size_t>(u(gen)) * n + u(gen)) * n + u(gen)] = 0.5f;
+  opt.setOccupancyGrid(occ, n, n, n);
+  std::vector<VectorXd> g;
+  bool coll = true;
+  const double J = opt.getCostAndGradientCollision(&g, &coll);
+  std::vector<VectorXd> fc;
+  opt.getConstrainedOptimizationRef().getFreeConstraints(&fc);
+  std::vector<double> x;
+  for (const VectorXd& v : fc)
+    for (long i = 0; i < v.size(); ++i) x.push_back(v[i]);
+  Dense d = toDense(vs, 5);
+  for (int v = 1; v < d.S; ++v)
+    for (int k = 0; k < 5; ++k) d.mask[v * 5 + k] = 0;
+  const double prm[11] = {0.05, 0, 0, 0, 16, 16, 16, p.epsilon, 0.1, p.coll_pot_multiplier,
+                          p.coll_check_time_increment};
+  double oJ = 0.0;
+  int oc = 0;
+  std::vector<double> og(x.size());
+  EXPECT_TRUE(orc_collision_cost(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), times.data(),
+                                 x.data(), occ.data(), n, n, n, prm, 20, &oJ, &oc, nullptr,
+                                 og.data()) == 0);
+  EXPECT_TRUE((coll ? 1 : 0) == oc);
+  EXPECT_LE(std::fabs(J - oJ), 1e-9 * std::max(1.0, std::fabs(oJ)));
+  std::vector<double> gx;
+  for (const VectorXd& v : g)
+    for (long i = 0; i < v.size(); ++i) gx.push_back(v[i]);
+  if (!oc && oJ > 0) EXPECT_LE(relErr(gx, og), 1e-7);
+  std::printf("  collision cost %.6g (oracle %.6g), collision %d\n", J, oJ, oc);
+}
+
 // kOptimizeFreeConstraintsAndTime (optimizeTimeAndFreeConstraints,
 // nonlinear_impl:610-706): the shim runs mtg_time_free_optimize from the tube
 // QCQP start; the same steps as the oracle port, a lower objective, bounds
