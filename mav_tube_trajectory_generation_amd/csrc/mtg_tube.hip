@@ -10,8 +10,9 @@
 namespace mtg {
 
 template <int N>
-__device__ inline Tube<N> make_tube(const TubeLayout* L, double* smem, int S, int r) {
-  return Tube<N>{S, r, S - 1, tube_ncon(N, S), L, smem, static_cast<int>(threadIdx.x)};
+__device__ inline Tube<N> make_tube(const TubeLayout* L, double* smem, int S, int r,
+                                    const double* tab) {
+  return Tube<N>{S, r, S - 1, tube_ncon(N, S), L, smem, static_cast<int>(threadIdx.x), tab};
 }
 
 // Constraint residuals g_k(x) (compute_sphere/tube/tube_end_constraints,
@@ -24,7 +25,7 @@ __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
     const double* __restrict__ x, double* __restrict__ resid) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const TubeLayout L = make_tube_layout(N, S);
-  Tube<N> t = make_tube<N>(&L, smem, S, r);
+  Tube<N> t = make_tube<N>(&L, smem, S, r, tab);
   int* bad = reinterpret_cast<int*>(smem + L.ndouble);
   const int64_t b = blockIdx.x;
   constexpr int M = N / 2;
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   const int64_t b = blockIdx.x;
   if (skip && skip[b / rep]) return;  // workgroup-uniform
   const TubeLayout L = make_tube_layout(N, S);
-  Tube<N> t = make_tube<N>(&L, smem, S, r);
+  Tube<N> t = make_tube<N>(&L, smem, S, r, tab);
   int* bad = reinterpret_cast<int*>(smem + L.ndouble);
   constexpr int M = N / 2;
   t.setup(tab, b, b / rep, positions, fixed_vals, times_cp, times, radii, bad);
@@ -68,6 +69,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   // definite, so x was never written.  Either way the outputs are NaN.
   const int fl = *bad;
   const bool no_x = (fl & 3) != 0;
+  // The powers share LDS with the factors: recompute them for the outputs.
+  if (!(fl & 1)) t.compute_powers();
+  __syncthreads();
   // Outputs: x (reference order), coefficients (qcqp_impl:777-785 ->
   // linear_impl:254-275) and computeCost (linear_impl:113-130).
   const int n = t.nv * 3 * M;
@@ -87,8 +91,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
     for (int j = 0; j < N; ++j) {
       const int l = j % M;
       const double e = t.xval(xv, s + j / M, d, l);
-      c += smem[L.tabA + k * N + j] * t.pwr(s, l - k) * e;
-      h += smem[L.tabH + k * N + j] * t.pwr(s, 1 - 2 * r + lk + l) * e;
+      c += tab[N * N + k * N + j] * t.pwr(s, l - k) * e;
+      h += tab[k * N + j] * t.pwr(s, 1 - 2 * r + lk + l) * e;
     }
     coeffs[b * per + i] = no_x ? NAN : c;
     acc += h * t.xval(xv, s + k / M, d, lk);

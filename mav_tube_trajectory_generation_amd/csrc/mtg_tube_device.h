@@ -18,7 +18,8 @@
 // each dimension).  A primal-dual Mehrotra interior-point method (the
 // oracle's algorithm, oracle/mtg_oracle.cpp TubeProblem::solveIPM) runs per
 // trajectory: per iteration one block LDL^T factorisation (explicit unit
-// L^-1 per block so the two solves are mat-vecs) and two solves.
+// L^-1 per block so the two solves are mat-vecs) and two solves.  State is
+// sized to 40 KB of LDS at S = 10, N = 10, so 4 trajectories share a CU.
 #pragma once
 #include "mtg_device.h"
 
@@ -26,48 +27,49 @@ namespace mtg {
 
 constexpr int kTubeD = 3;
 
+// LDS per trajectory (doubles).  Sized for 4 workgroups per CU at the
+// reference's S = 10, N = 10 (40 KB): the constant tables stay in global
+// memory (L1/L2-resident), Bezier beta rows are derived from B_ul^-1, P is
+// stored as its symmetric half, the constraint values and complementarity
+// targets are recomputed where used, the step's control points share the
+// dual-residual scratch, L_a^-1 is kept as a packed lower triangle whose
+// diagonal holds 1 / pivot, and W_a = L_a^-1 C_a only for the block the
+// factorisation is on (the solves apply C_a^T L_a^-T / L_a^-1 C_a instead).
 struct TubeLayout {
-  int tabH, tabA, cinv;   // N*N, N*N, M*M
   int bul;                // S*M*M  B_ul^-1 per segment (zero-snapped)
-  int bet;                // S*N*M  beta rows per control point
-  int pw;                 // S*(2N-1) powers of the current times
+  int pw;                 // S*(2N-1) powers of the current times (overlays Li:
+                          // setup and output only)
   int T;                  // S
   int geo;                // S*kGeo tube geometry per segment
   int fixv;               // 2*3*M start/end derivatives [end][d][m]
   int pos;                // (S+1)*3
-  int Pd, Po, q;          // nv*M*M, (nv-1)*M*M, nv*3M
+  int Pd, Po, q;          // nv*M(M+1)/2 (packed symmetric), (nv-1)*M*M, nv*3M
   int x, dx, rd, rhs;     // nv*3M each
-  int cp, dcp, acc;       // S*N*3 each
-  int s, lam, g, ds, dl, prod;  // ncon each
-  int Li;                 // nv*BS*BS  unit lower L_a^-1, row-major
-  int W;                  // max(nv-1,1)*BS*BS  W_a = L_a^-1 C_a, row-major
-  int dinv;               // nv*BS     1 / pivots of S_a = L_a D_a L_a^T
-  int Gc;                 // S*N*9  per control point: sum lam Hess + lam/s w w^T
-  int tmp;                // BS*BS+1 (U columns in factor, solve scratch; last = dummy)
-  int red;                // 64
+  int cp, acc;            // S*N*3 each; acc also holds the step's control points
+  int s, lam, ds, dl;     // ncon each
+  int Li;                 // nv*BS(BS+1)/2 L_a^-1 packed by rows, diagonal = 1/pivot
+  int W;                  // BS*BS  W_a of the current block, row-major
+  int Gc;                 // S*N*6  per control point: sum lam Hess + lam/s w w^T (sym)
+  int tmp;                // 2*BS+2 solve scratch
   int ndouble;
   size_t bytes() const { return sizeof(double) * ndouble; }
 };
 
-constexpr int kGeo = 20;  // n[3] LL[9] L[3] mu n.ps n.pe r2^2 pad
+constexpr int kGeo = 19;  // n[3] LL[9] L[3] mu n.ps n.pe r2^2
 
 __host__ __device__ inline int tube_ncon(int N, int S) { return (S - 1) + 3 * S * (N - 2); }
 
 __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   const int M = N / 2, BS = 3 * M, nv = S - 1, nc = tube_ncon(N, S);
+  const int tri = BS * (BS + 1) / 2;
   TubeLayout l;
   int o = 0;
-  l.tabH = o; o += N * N;
-  l.tabA = o; o += N * N;
-  l.cinv = o; o += M * M;
   l.bul = o;  o += S * M * M;
-  l.bet = o;  o += S * N * M;
-  l.pw = o;   o += S * (2 * N - 1);
   l.T = o;    o += S;
   l.geo = o;  o += S * kGeo;
   l.fixv = o; o += 2 * 3 * M;
   l.pos = o;  o += (S + 1) * 3;
-  l.Pd = o;   o += nv * M * M;
+  l.Pd = o;   o += nv * M * (M + 1) / 2;
   l.Po = o;   o += (nv > 1 ? nv - 1 : 1) * M * M;
   l.q = o;    o += nv * BS;
   l.x = o;    o += nv * BS;
@@ -75,20 +77,17 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   l.rd = o;   o += nv * BS;
   l.rhs = o;  o += nv * BS;
   l.cp = o;   o += S * N * 3;
-  l.dcp = o;  o += S * N * 3;
   l.acc = o;  o += S * N * 3;
   l.s = o;    o += nc;
   l.lam = o;  o += nc;
-  l.g = o;    o += nc;
   l.ds = o;   o += nc;
   l.dl = o;   o += nc;
-  l.prod = o; o += nc;
-  l.Li = o;   o += nv * BS * BS;
-  l.W = o;    o += (nv > 1 ? nv - 1 : 1) * BS * BS;
-  l.dinv = o; o += nv * BS;
-  l.Gc = o;   o += S * N * 9;
-  l.tmp = o;  o += BS * BS + 1;
-  l.red = o;  o += kWave;
+  l.Li = o;
+  l.pw = o;
+  o += (nv * tri > S * (2 * N - 1) ? nv * tri : S * (2 * N - 1));
+  l.W = o;    o += BS * BS;
+  l.Gc = o;   o += S * N * 6;
+  l.tmp = o;  o += 2 * BS + 2;
   l.ndouble = o;
   return l;
 }
@@ -98,10 +97,21 @@ struct Tube {
   static constexpr int M = N / 2;
   static constexpr int BS = 3 * M;
   static constexpr int PWN = 2 * N - 1;
+  static constexpr int kTri = BS * (BS + 1) / 2;
   int S, r, nv, nc;
   const TubeLayout* L;
   double* sm;
   int lane;
+  const double* __restrict__ gtab;  // plan table: H(1) N*N, A(1)^-1 N*N, C^-1 M*M (global)
+
+  __device__ static int tri(int i, int k) { return i * (i + 1) / 2 + k; }  // k <= i
+  __device__ double pd(int a, int j, int k) const {  // symmetric P block a
+    return sm[L->Pd + a * (M * (M + 1) / 2) + (j >= k ? tri(j, k) : tri(k, j))];
+  }
+  __device__ static int gsym(int a, int e) {  // packed symmetric 3 x 3
+    const int lo = a < e ? a : e, hi = a < e ? e : a;
+    return lo == 0 ? hi : (lo == 1 ? 2 + hi : 5);
+  }
 
   __device__ double* at(int off) const { return sm + off; }
   __device__ double pwr(int s, int e) const { return sm[L->pw + s * PWN + e + (N - 1)]; }
@@ -116,7 +126,7 @@ struct Tube {
     const double v = b[(M - 1 - (j - M)) * M + m];
     return (m & 1) ? -v : v;
   }
-  __device__ double beta(int i, int j, int m) const { return sm[L->bet + (i * N + j) * M + m]; }
+  __device__ double beta(int i, int j, int m) const { return beta_raw(i, j, m); }
   // Derivative m of vertex u in dimension d (fixed at the ends).
   __device__ double xval(const double* xv, int u, int d, int m) const {
     if (u == 0) return sm[L->fixv + (0 * 3 + d) * M + m];
@@ -170,7 +180,6 @@ struct Tube {
                         const double* __restrict__ times,
                         const double* __restrict__ radii, int* bad) {
     const int NN = N * N;
-    for (int i = lane; i < 2 * NN + M * M; i += kWave) sm[L->tabH + i] = tab[i];
     for (int i = lane; i < S; i += kWave) sm[L->T + i] = times[b * S + i];
     for (int i = lane; i < (S + 1) * 3; i += kWave) sm[L->pos + i] = positions[bin * (S + 1) * 3 + i];
     for (int i = lane; i < 3 * N; i += kWave) {
@@ -187,27 +196,12 @@ struct Tube {
       if (!(tc > 0.0)) atomicOr(bad, 1);
       double p = 1.0;
       for (int q = 0; q < l; ++q) p *= tc;
-      double v = sm[L->cinv + k * M + l] * p;
+      double v = gtab[2 * NN + k * M + l] * p;
       if (v > -0.00001 && v < 0.00001) v = 0.0;
       sm[L->bul + idx] = v;
     }
-    __syncthreads();
-    for (int idx = lane; idx < S * N * M; idx += kWave) {
-      const int i = idx / (N * M), j = (idx / M) % N, m = idx % M;
-      sm[L->bet + idx] = beta_raw(i, j, m);
-    }
     // Powers of the current times (H, A^-1, cost).
-    for (int idx = lane; idx < S * PWN; idx += kWave) {
-      const int s = idx / PWN;
-      const int e = idx % PWN - (N - 1);
-      const double t = sm[L->T + s];
-      if (!(t > 0.0) || !(t < 1e300)) atomicOr(bad, 1);
-      const double base = e < 0 ? 1.0 / t : t;
-      const int n = e < 0 ? -e : e;
-      double p = 1.0;
-      for (int q = 0; q < n; ++q) p *= base;
-      sm[L->pw + idx] = p;
-    }
+    if (!compute_powers()) atomicOr(bad, 1);
     // Tube geometry per segment (qcqp_impl:369-474).
     for (int i = lane; i < S; i += kWave) {
       const double* p0 = sm + L->pos + i * 3;
@@ -252,9 +246,14 @@ struct Tube {
       G[18] = r2 * r2;
     }
     __syncthreads();
-    // P = 2 R_pp (identical M x M blocks per dimension) and q = 2 R_pf d_f.
-    for (int idx = lane; idx < nv * M * M; idx += kWave) {
-      const int a = idx / (M * M), j = (idx / M) % M, k = idx % M;
+    // P = 2 R_pp (identical M x M blocks per dimension, symmetric half) and
+    // q = 2 R_pf d_f.
+    constexpr int MT = M * (M + 1) / 2;
+    for (int idx = lane; idx < nv * MT; idx += kWave) {
+      const int a = idx / MT, t2 = idx % MT;
+      int j = 0;
+      while (tri(j + 1, 0) <= t2) ++j;
+      const int k = t2 - tri(j, 0);
       const int u = a + 1;  // vertex
       sm[L->Pd + idx] = 2.0 * (Hb(u - 1, 1, 1, j, k) + Hb(u, 0, 0, j, k));
     }
@@ -276,7 +275,26 @@ struct Tube {
   }
 
   __device__ double Hb(int s, int ab, int bb, int j, int k) const {
-    return sm[L->tabH + (ab * M + j) * N + bb * M + k] * pwr(s, 1 - 2 * r + j + k);
+    return gtab[(ab * M + j) * N + bb * M + k] * pwr(s, 1 - 2 * r + j + k);
+  }
+
+  // Powers T_s^e, e in [-(N-1), N-1], of the current times into pw (which
+  // overlays the factor storage: call before the IPM and again for the
+  // outputs).  Returns false if a time is not a valid segment time.
+  __device__ bool compute_powers() {
+    bool ok = true;
+    for (int idx = lane; idx < S * PWN; idx += kWave) {
+      const int s = idx / PWN;
+      const int e = idx % PWN - (N - 1);
+      const double t = sm[L->T + s];
+      if (!(t > 0.0) || !(t < 1e300)) ok = false;
+      const double base = e < 0 ? 1.0 / t : t;
+      const int n = e < 0 ? -e : e;
+      double p = 1.0;
+      for (int q = 0; q < n; ++q) p *= base;
+      sm[L->pw + idx] = p;
+    }
+    return ok;
   }
 
   // --------------------------------------------------------- control points
@@ -363,7 +381,7 @@ struct Tube {
     const int a = idx / BS, d = (idx / M) % 3, m = idx % M;
     double v = sm[L->q + idx];
     for (int k = 0; k < M; ++k) {
-      v += sm[L->Pd + a * M * M + m * M + k] * xv[(a * 3 + d) * M + k];
+      v += pd(a, m, k) * xv[(a * 3 + d) * M + k];
       if (a > 0) v += sm[L->Po + (a - 1) * M * M + k * M + m] * xv[((a - 1) * 3 + d) * M + k];
       if (a < nv - 1) v += sm[L->Po + a * M * M + m * M + k] * xv[((a + 1) * 3 + d) * M + k];
     }
@@ -402,11 +420,12 @@ struct Tube {
         con_of(k, &ii, &jj, &type);
         const double lam = sm[L->lam + k], s = sm[L->s + k];
         const double ws = lam / s;
-        for (int a = 0; a < 3; ++a)
+          for (int a = 0; a < 3; ++a)
           for (int e = 0; e < 3; ++e)
             G[a * 3 + e] += lam * con_hess(type, i, a, e) + ws * w[a] * w[e];
       }
-      for (int e = 0; e < 9; ++e) Gcp[cpi * 9 + e] = G[e];
+      for (int a = 0; a < 3; ++a)
+        for (int e = a; e < 3; ++e) Gcp[cpi * 6 + gsym(a, e)] = G[a * 3 + e];
     }
     __syncthreads();
   }
@@ -453,14 +472,13 @@ struct Tube {
       const int d2 = cc / M, m2 = cc % M;
       const double r0 = is_zero(role), r1 = is_zero(role - 1), r2 = is_zero(role - 2);
       {
-        const double* Pd = sm + L->Pd + a * M * M;
         const double* Po = sm + L->Po + (a < nv - 1 ? a : 0) * M * M;
         double ind[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) ind[d] = is_zero(d - d2);
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const double v = Pd[m * M + m2] * r0 + Po[m * M + m2] * r2;
+          const double v = pd(a, m, m2) * r0 + Po[m * M + m2] * r2;
 #pragma unroll
           for (int d = 0; d < 3; ++d) col[d * M + m] = v * ind[d];
         }
@@ -480,10 +498,10 @@ struct Tube {
           const int j = q < M ? q + M : q - M;
           const int cpi = i * N + j;
 #pragma unroll
-          for (int m = 0; m < M; ++m) b[m] = sm[L->bet + cpi * M + m];
+          for (int m = 0; m < M; ++m) b[m] = beta_raw(i, j, m);
 #pragma unroll
-          for (int d = 0; d < 3; ++d) g[d] = Gcp[cpi * 9 + d * 3 + d2];
-          return sm[L->bet + cpi * M + m2];
+          for (int d = 0; d < 3; ++d) g[d] = Gcp[cpi * 6 + gsym(d, d2)];
+          return beta_raw(i, j, m2);
         };
         bm = load_cp(0, bt, g3);
 #pragma unroll
@@ -507,23 +525,24 @@ struct Tube {
       }
       MTG_TACC(221, tf);
       if (a > 0) {
-        // S_a[:, c] -= sum_t W[t][:] dinv[t] W[t][c]  (W = W_{a-1}); row
-        // t+1 is loaded while row t is applied.
-        const double* Wp = sm + L->W + (a - 1) * BS * BS;
-        const double* dp = sm + L->dinv + (a - 1) * BS;
+        // S_a[:, c] -= sum_t W[t][:] dinv[t] W[t][c]  (W = W_{a-1}, dinv on
+        // the diagonal of the packed L_{a-1}^-1); row t+1 is loaded while row
+        // t is applied.
+        const double* Wp = sm + L->W;
+        const double* Lp = sm + L->Li + (a - 1) * kTri;
         const double on = r0;
         double wr[BS], wn[BS], wc, dt, wcn = 0.0, dtn = 0.0;
 #pragma unroll
         for (int i = 0; i < BS; ++i) wr[i] = Wp[i];
         wc = Wp[cc];
-        dt = dp[0];
+        dt = Lp[0];
 #pragma unroll
         for (int t = 0; t < BS; ++t) {
           if (t + 1 < BS) {
 #pragma unroll
             for (int i = 0; i < BS; ++i) wn[i] = Wp[(t + 1) * BS + i];
             wcn = Wp[(t + 1) * BS + cc];
-            dtn = dp[t + 1];
+            dtn = Lp[tri(t + 1, t + 1)];
           }
           __builtin_amdgcn_sched_barrier(0);
           const double w = wc * dt * on;
@@ -539,11 +558,12 @@ struct Tube {
       // Forward elimination (below the pivot) on all columns at once; the
       // pivot column is broadcast with v_readlane.
       MTG_TACC(222, tf);
-      double pmin = 1.0;
+      double pmin = 1.0, dpiv = 0.0;
 #pragma unroll
       for (int j = 0; j < BS; ++j) {
         const double piv = bcast(col[j], j);
         pmin = fmin(pmin, piv);
+        dpiv = fma(is_zero(j - c), piv, dpiv);  // lane c < BS: its own pivot
         if (j == BS - 1) break;
         const double f = col[j] * rcp64(piv > 0.0 ? piv : 1.0);
 #pragma unroll
@@ -551,20 +571,22 @@ struct Tube {
       }
       bad |= !(pmin > 0.0);
       MTG_TACC(223, tf);
-      // Lanes 0.. store U columns (scratch: the pivots), BS.. L_a^-1 columns,
-      // 2BS.. W_a columns; idle lanes write one dummy slot.
-      {
-        const int base = role == 0 ? L->tmp : role == 1 ? L->Li + a * BS * BS
-                       : role == 2 ? L->W + a * BS * BS : L->tmp + BS * BS;
-        const int stride = role == 3 ? 0 : BS;
-        double* dst = sm + base + (role == 3 ? 0 : cc);
-#pragma unroll
-        for (int i = 0; i < BS; ++i) dst[i * stride] = col[i];
-      }
+      // Lanes 0.. store 1 / pivot on the diagonal of the packed L_a^-1,
+      // BS.. its strictly lower columns, 2BS.. W_a (replacing W_{a-1}, which
+      // every lane has finished reading at the barrier).
       __syncthreads();
-      if (c < BS) {
-        const double p = sm[L->tmp + c * BS + c];
-        sm[L->dinv + a * BS + c] = rcp64(p > 0.0 ? p : 1.0);
+      {
+        double* Li = sm + L->Li + a * kTri;
+        if (role == 0) {
+          Li[tri(cc, cc)] = rcp64(dpiv > 0.0 ? dpiv : 1.0);
+        } else if (role == 1) {
+#pragma unroll
+          for (int i = 1; i < BS; ++i)
+            if (i > cc) Li[tri(i, cc)] = col[i];
+        } else if (role == 2) {
+#pragma unroll
+          for (int i = 0; i < BS; ++i) sm[L->W + i * BS + cc] = col[i];
+        }
       }
       __syncthreads();
       MTG_TACC(224, tf);
@@ -573,70 +595,81 @@ struct Tube {
   }
 
   // Solve K out = rhs with the block factors (rhs overwritten by y).
-  // Lanes 0..BS-1 own one row each; matrix rows are loaded before the
-  // values of the recurrence (sched barriers keep them there).  L_a^-1 is
-  // stored with exact zeros above the diagonal, so full-length sums equal
-  // the triangular ones.
+  // Lanes 0..BS-1 own one row each.  W_a = L_a^-1 C_a is not stored; the
+  // coupling is applied as C_a = I_3 (x) Po_a next to the packed L^-1:
+  //   forward   y_a = L_a^-1 (b_a - C_{a-1}^T L_{a-1}^-T D_{a-1}^-1 y_{a-1})
+  //   backward  x_a = L_a^-T D_a^-1 (y_a - L_a^-1 C_a x_{a+1}).
+  // Triangular sums run over the full row with the out-of-triangle terms
+  // weighted by exact 0 (the unit diagonal by exact 1).
   __device__ void solve(int rhs_off, int out_off) {
     double* tmp = sm + L->tmp;
     double* y = sm + rhs_off;
     double* xo = sm + out_off;
     const bool act = lane < BS;
     const int i = act ? lane : 0;
+    const int di = i / M, mi = i % M;
     for (int a = 0; a < nv; ++a) {
-      double wc[BS], dpv[BS], lr[BS], v1[BS];
-      const double* Wp = sm + L->W + (a > 0 ? a - 1 : 0) * BS * BS;
-      const double* dp = sm + L->dinv + (a > 0 ? a - 1 : 0) * BS;
-      const double* Li = sm + L->Li + a * BS * BS;
-#pragma unroll
-      for (int k = 0; k < BS; ++k) wc[k] = Wp[k * BS + i];
-#pragma unroll
-      for (int k = 0; k < BS; ++k) dpv[k] = dp[k];
-#pragma unroll
-      for (int k = 0; k < BS; ++k) lr[k] = Li[i * BS + k];
+      const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
-#pragma unroll
-      for (int k = 0; k < BS; ++k) v1[k] = y[(a > 0 ? a - 1 : 0) * BS + k];
-      __builtin_amdgcn_sched_barrier(0);
       if (a > 0) {
+        // v = L_{a-1}^-T D_{a-1}^-1 y_{a-1} (row i), then t -= (C^T v)_i.
+        const double* Lp = Li - kTri;
+        const double* z = y + (a - 1) * BS;
+        double v = 0.0;
 #pragma unroll
-        for (int k = 0; k < BS; ++k) t -= wc[k] * dpv[k] * v1[k];
+        for (int k = 0; k < BS; ++k) {
+          const int kk = k > i ? k : i;
+          const double gt = static_cast<double>(k > i), eq = is_zero(k - i);
+          v = fma(fma(Lp[tri(kk, i)], gt, eq), z[k] * Lp[tri(k, k)], v);
+        }
+        if (act) tmp[i] = v;
+        __syncthreads();
+        const double* Po = sm + L->Po + (a - 1) * M * M;
+#pragma unroll
+        for (int m = 0; m < M; ++m) t = fma(-Po[m * M + mi], tmp[di * M + m], t);
       }
-      if (act) tmp[i] = t;
+      if (act) tmp[BS + i] = t;
       __syncthreads();
+      double zi = 0.0;
 #pragma unroll
-      for (int k = 0; k < BS; ++k) v1[k] = tmp[k];
-      double v = 0.0;
-#pragma unroll
-      for (int k = 0; k < BS; ++k) v += lr[k] * v1[k];
-      if (act) y[a * BS + i] = v;
+      for (int k = 0; k < BS; ++k) {
+        const int kk = k < i ? k : i;
+        const double lt = static_cast<double>(k < i), eq = is_zero(k - i);
+        zi = fma(fma(Li[tri(i, kk)], lt, eq), tmp[BS + k], zi);
+      }
+      if (act) y[a * BS + i] = zi;
       __syncthreads();
     }
     for (int a = nv - 1; a >= 0; --a) {
-      double wr[BS], lc[BS], v1[BS];
-      const double* Wa = sm + L->W + (a < nv - 1 ? a : 0) * BS * BS;
-      const double* Li = sm + L->Li + a * BS * BS;
-#pragma unroll
-      for (int k = 0; k < BS; ++k) wr[k] = Wa[i * BS + k];
-#pragma unroll
-      for (int k = 0; k < BS; ++k) lc[k] = Li[k * BS + i];
-      double t = y[a * BS + i];
-      const double di = sm[L->dinv + a * BS + i];
-#pragma unroll
-      for (int k = 0; k < BS; ++k) v1[k] = xo[(a < nv - 1 ? a + 1 : 0) * BS + k];
-      __builtin_amdgcn_sched_barrier(0);
+      const double* Li = sm + L->Li + a * kTri;
+      // u = C_a x_{a+1} (row i), exchanged for L_a^-1 u.
+      double u = 0.0;
       if (a < nv - 1) {
+        const double* Po = sm + L->Po + a * M * M;
+        const double* xn = xo + (a + 1) * BS + di * M;
 #pragma unroll
-        for (int k = 0; k < BS; ++k) t -= wr[k] * v1[k];
+        for (int m = 0; m < M; ++m) u = fma(Po[mi * M + m], xn[m], u);
       }
-      if (act) tmp[i] = t * di;
+      if (act) tmp[i] = u;
       __syncthreads();
+      double t = y[a * BS + i];
 #pragma unroll
-      for (int k = 0; k < BS; ++k) v1[k] = tmp[k];
-      double v = 0.0;
+      for (int k = 0; k < BS; ++k) {
+        const int kk = k < i ? k : i;
+        const double lt = static_cast<double>(k < i), eq = is_zero(k - i);
+        t = fma(-fma(Li[tri(i, kk)], lt, eq), tmp[k], t);
+      }
+      t *= Li[tri(i, i)];
+      if (act) tmp[BS + i] = t;
+      __syncthreads();
+      double xi = 0.0;
 #pragma unroll
-      for (int k = 0; k < BS; ++k) v += lc[k] * v1[k];
-      if (act) xo[a * BS + i] = v;
+      for (int k = 0; k < BS; ++k) {
+        const int kk = k > i ? k : i;
+        const double gt = static_cast<double>(k > i), eq = is_zero(k - i);
+        xi = fma(fma(Li[tri(kk, i)], gt, eq), tmp[BS + k], xi);
+      }
+      if (act) xo[a * BS + i] = xi;
       __syncthreads();
     }
   }
@@ -657,10 +690,19 @@ struct Tube {
     return x;
   }
 
-  // Newton direction for a complementarity target rc (stored in `prod`
-  // beforehand as rc_k): rhs = -rd - sum a_k (lam rp - rc)/s, solve, then
-  // dl, ds.  Expects cp, g, rd valid and the factorisation done.
-  __device__ void direction() {
+  // Complementarity target: affine rc = s lam; corrector
+  // rc = s lam + ds_aff dl_aff - sigma mu (ds, dl still hold the affine step).
+  template <bool kCorr>
+  __device__ double rc_of(int k, double smu) const {
+    const double v = sm[L->s + k] * sm[L->lam + k];
+    return kCorr ? v + sm[L->ds + k] * sm[L->dl + k] - smu : v;
+  }
+
+  // Newton direction for the complementarity target rc_of<kCorr>:
+  // rhs = -rd - sum a_k (lam rp - rc)/s, solve, then dl, ds.  Expects cp, rd
+  // valid and the factorisation done.  The step's control points go to acc.
+  template <bool kCorr>
+  __device__ void direction(double smu) {
     // Per control point: Psi[d] = sum_k w_k[d] (lam_k rp_k - rc_k) / s_k.
     for (int cpi = lane; cpi < S * N; cpi += kWave) {
       const int i = cpi / N, j = cpi % N;
@@ -670,10 +712,10 @@ struct Tube {
         const int k = con_at(i, j, t);
         if (k < 0) continue;
         double w[3];
-        con_eval(k, L->cp, w);
+        const double g = con_eval(k, L->cp, w);
         const double lam = sm[L->lam + k], s = sm[L->s + k];
-        const double rp = sm[L->g + k] + s;
-        const double coef = (lam * rp - sm[L->prod + k]) / s;
+        const double rp = g + s;
+        const double coef = (lam * rp - rc_of<kCorr>(k, smu)) / s;
         for (int d = 0; d < 3; ++d) P3[d] += w[d] * coef;
       }
       for (int d = 0; d < 3; ++d) sm[L->acc + cpi * 3 + d] = P3[d];
@@ -688,18 +730,18 @@ struct Tube {
     MTG_TACC(511, tl);
     solve(L->rhs, L->dx);
     MTG_TACC(210, tl);
-    control_point_steps(sm + L->dx, L->dcp);
+    control_point_steps(sm + L->dx, L->acc);
     __syncthreads();
     for (int k = lane; k < nc; k += kWave) {
       double w[3];
-      con_eval(k, L->cp, w);
+      const double g = con_eval(k, L->cp, w);
       int i, j, type;
       con_of(k, &i, &j, &type);
-      const double* dc = sm + L->dcp + (i * N + j) * 3;
+      const double* dc = sm + L->acc + (i * N + j) * 3;
       const double adx = w[0] * dc[0] + w[1] * dc[1] + w[2] * dc[2];
       const double lam = sm[L->lam + k], s = sm[L->s + k];
-      const double rp = sm[L->g + k] + s;
-      const double rc = sm[L->prod + k];
+      const double rp = g + s;
+      const double rc = rc_of<kCorr>(k, smu);
       const double dl = (lam / s) * (adx + rp) - rc / s;
       sm[L->dl + k] = dl;
       sm[L->ds + k] = (-rc - s * dl) / lam;
@@ -744,7 +786,6 @@ struct Tube {
     for (int k = lane; k < nc; k += kWave) {
       double w[3];
       const double g = con_eval(k, L->cp, w);
-      sm[L->g + k] = g;
       sm[L->s + k] = fmax(-g, 1.0);
       sm[L->lam + k] = 1.0;
     }
@@ -764,7 +805,6 @@ struct Tube {
       for (int k = lane; k < nc; k += kWave) {
         double w[3];
         const double g = con_eval(k, L->cp, w);
-        sm[L->g + k] = g;
         const double s = sm[L->s + k];
         rpn = fmax(rpn, fabs(g + s));
         mu += s * sm[L->lam + k];
@@ -818,9 +858,7 @@ struct Tube {
         break;
       }
       // Affine (predictor) direction: rc = s * lam.
-      for (int k = lane; k < nc; k += kWave) sm[L->prod + k] = sm[L->s + k] * sm[L->lam + k];
-      __syncthreads();
-      direction();
+      direction<false>(0.0);
       MTG_TACC(203, tl);
       const double a_aff = max_step();
       double mua = 0.0;
@@ -831,11 +869,8 @@ struct Tube {
       const double sigma = ratio * ratio * ratio;
       __syncthreads();
       // Corrector: rc = s lam + ds_aff dl_aff - sigma mu.
-      for (int k = lane; k < nc; k += kWave)
-        sm[L->prod + k] = sm[L->s + k] * sm[L->lam + k] + sm[L->ds + k] * sm[L->dl + k] - sigma * mu;
-      __syncthreads();
       MTG_TACC(204, tl);
-      direction();
+      direction<true>(sigma * mu);
       MTG_TACC(205, tl);
       const double alpha = fmin(1.0, 0.99 * max_step());
       double dxn = 0.0;
