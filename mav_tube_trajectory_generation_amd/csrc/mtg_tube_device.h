@@ -44,13 +44,13 @@ struct TubeLayout {
   int fixv;               // 2*3*M start/end derivatives [end][d][m]
   int pos;                // (S+1)*3
   int Pd, Po, q;          // nv*M(M+1)/2 (packed symmetric), (nv-1)*M*M, nv*3M
-  int x, dx, rd, rhs;     // nv*3M each
+  int x, dx, rd, rhs;     // nv*3M each (rhs at least 64)
   int cp, acc;            // S*N*3 each; acc also holds the step's control points
   int s, lam, ds, dl;     // ncon each
   int Li;                 // nv*BS(BS+1)/2 L_a^-1 packed by rows, diagonal = 1/pivot
   int W;                  // BS*BS  W_a of the current block, row-major
   int Gc;                 // S*N*6  per control point: sum lam Hess + lam/s w w^T (sym)
-  int tmp;                // 2*BS+2 solve scratch
+  int tmp;                // 3*BS+2 solve scratch (last slot: dummy store target)
   int ndouble;
   size_t bytes() const { return sizeof(double) * ndouble; }
 };
@@ -75,7 +75,7 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   l.x = o;    o += nv * BS;
   l.dx = o;   o += nv * BS;
   l.rd = o;   o += nv * BS;
-  l.rhs = o;  o += nv * BS;
+  l.rhs = o;  o += nv * BS > kWave ? nv * BS : kWave;  // also factor()'s dummy store slots
   l.cp = o;   o += S * N * 3;
   l.acc = o;  o += S * N * 3;
   l.s = o;    o += nc;
@@ -87,7 +87,7 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   o += (nv * tri > S * (2 * N - 1) ? nv * tri : S * (2 * N - 1));
   l.W = o;    o += BS * BS;
   l.Gc = o;   o += S * N * 6;
-  l.tmp = o;  o += 2 * BS + 2;
+  l.tmp = o;  o += 3 * BS + 2;
   l.ndouble = o;
   return l;
 }
@@ -430,6 +430,8 @@ struct Tube {
     __syncthreads();
   }
 
+  // 1 if x == 0 else 0 (integer arithmetic, see is_zero).
+  __device__ static int izero(int x) { return ((x | -x) >> 31) + 1; }
   // 1.0 if x == 0 else 0.0, by integer arithmetic: a compare would yield a
   // lane mask (SGPR pair) that the compiler hoists and keeps live.
   __device__ static double is_zero(int x) {
@@ -445,31 +447,80 @@ struct Tube {
                                 (static_cast<unsigned int>(lo)));
   }
 
+  // ----------------------------------------------------- lane organisation
+  // For BS <= 16 the wave is 4 rows of 16 lanes: lane (g, c) = 16 g + c.
+  // Dot products and the S_a update are split over the rows (every row takes
+  // every 4th term) and summed with the gfx950 cross-row swaps; in the
+  // elimination row g holds role g (0 = S_a, 1 = identity, 2 = C_a, 3 idle).
+  // For BS > 16 (N = 12) a single group: roles at lanes 0, BS, 2BS.
+  static constexpr int kNG = BS <= 16 ? 4 : 1;
+  __device__ int grp() const { return kNG == 4 ? lane >> 4 : 0; }
+  __device__ int col_of() const { return kNG == 4 ? (lane & 15) : lane % BS; }
+  __device__ int role_of() const {
+    const int c = kNG == 4 ? (lane & 15) : lane % BS;
+    const int r = kNG == 4 ? (lane >> 4) : lane / BS;
+    return (c >= BS || r > 2) ? 3 : r;
+  }
+
+  __device__ static double join(unsigned lo, unsigned hi) {
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | lo);
+  }
+  // x + x(lane ^ 32) and x + x(lane ^ 16): v_permlane{32,16}_swap with the
+  // value as both operands leaves {x(lane), x(partner)} in the two results.
+  __device__ static double xsum32(double x) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = static_cast<unsigned>(b), hi = static_cast<unsigned>(b >> 32);
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return join(l[0], h[0]) + join(l[1], h[1]);
+  }
+  __device__ static double xsum16(double x) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = static_cast<unsigned>(b), hi = static_cast<unsigned>(b >> 32);
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return join(l[0], h[0]) + join(l[1], h[1]);
+  }
+  // Sum over the kNG rows (the result is in every row).  Call with all 64
+  // lanes active.
+  __device__ static double rows_sum(double x) {
+    if constexpr (kNG == 4) return xsum16(xsum32(x));
+    return x;
+  }
+
   // --------------------------------------------------------- factorisation
   // Block LDL^T of the block-tridiagonal KKT matrix.  For vertex block a:
   //   S_a = K_a - W_{a-1}^T D_{a-1}^-1 W_{a-1} = L_a D_a L_a^T,
   //   W_a = L_a^-1 C_a,   C_a = I_3 (x) Po_a (coupling to block a+1).
-  // The elimination runs on [S_a | I | C_a] held column-per-lane in
-  // registers (lanes 0..BS-1, BS..2BS-1, 2BS..3BS-1); the pivot column is
-  // broadcast with v_readlane, so a block needs no LDS traffic and no
-  // barrier inside.  Afterwards lanes BS.. hold L_a^-1 (unit lower) and
-  // lanes 2BS.. hold W_a; the pivots are D_a.  S_a is SPD (no pivoting); a
-  // non-positive pivot sets *fail.
+  // The constraint and Schur terms of S_a are accumulated with the rows
+  // sharing the sums (control points q = g + 4k, W rows t = g + 4k), then
+  // the elimination runs on [S_a | I | C_a] held column-per-lane in
+  // registers; the pivot column is broadcast with v_readlane, so it needs no
+  // LDS traffic and no barrier inside.  Afterwards the identity lanes hold
+  // L_a^-1 (unit lower) and the C_a lanes W_a; the pivots are D_a.  S_a is
+  // SPD (no pivoting); a non-positive pivot sets *fail.
   __device__ void factor(int* fail, bool with_constraints) {
     const double* Gcp = sm + L->Gc;
     int bad = 0;
     unsigned long long tf = 0;
     MTG_TACC(511, tf);
+    const int g = grp();
+    const int cc0 = col_of() < BS ? col_of() : BS - 1;  // clamped on pad lanes
+    const int role0 = role_of();
+    // Per-lane target of the unused stores (rhs is dead during factor():
+    // written by direction() / the start system afterwards).
+    const int dummy = L->rhs + lane;
     for (int a = 0; a < nv; ++a) {
       const int u = a + 1;  // vertex
-      double col[BS];
-      const int c = lane;
-      // Lane roles: 0 = column c of S_a, 1 = identity column, 2 = column of
-      // C_a, 3 = idle.  Loads are unconditional (clamped indices) and roles
-      // enter as exact 0/1 factors (VGPR values: no lane masks kept live).
-      const int role = c < BS ? 0 : c < 2 * BS ? 1 : (c < 3 * BS && a < nv - 1) ? 2 : 3;
-      const int cc = c < BS ? c : c < 2 * BS ? c - BS : c < 3 * BS ? c - 2 * BS : 0;
+      double col[BS], acc[BS];
+      // Opaque per iteration: keeps the compiler from hoisting the 0/1
+      // factors below out of the loop as live lane masks (SGPR pressure).
+      int cc = cc0;
+      asm volatile("" : "+v"(cc));
       const int d2 = cc / M, m2 = cc % M;
+      const int role = (role0 == 2 && a == nv - 1) ? 3 : role0;
+      // Roles enter as exact 0/1 factors (VGPR values: no lane masks kept
+      // live); loads are unconditional with clamped indices.
       const double r0 = is_zero(role), r1 = is_zero(role - 1), r2 = is_zero(role - 2);
       {
         const double* Po = sm + L->Po + (a < nv - 1 ? a : 0) * M * M;
@@ -484,70 +535,62 @@ struct Tube {
         }
 #pragma unroll
         for (int i = 0; i < BS; ++i) col[i] += r1 * is_zero(i - cc);
+#pragma unroll
+        for (int i = 0; i < BS; ++i) acc[i] = 0.0;
       }
       MTG_TACC(220, tf);
       if (with_constraints) {
-        // sum over the control points of vertex u (segment u-1, j = M..N-1;
-        // segment u, j = 0..M-1) of G[d][d2] beta[m] beta[m2]; lanes of
-        // role != 0 accumulate zeros.  Loads of control point q+1 are issued
-        // before the arithmetic of q (sched barriers keep them there).
-        const double on = r0;
-        double bt[M], g3[3], bt2[M], g32[3], bm, bm_n = 0.0;
-        auto load_cp = [&](int q, double* b, double* g) {
-          const int i = q < M ? u - 1 : u;
-          const int j = q < M ? q + M : q - M;
-          const int cpi = i * N + j;
+        // This row's control points of vertex u (q < M: segment u-1,
+        // j = q + M, rows of B_lr^-1; q >= M: segment u, j = q - M):
+        // acc += G[d][d2] beta[m] beta[m2].
 #pragma unroll
-          for (int m = 0; m < M; ++m) b[m] = beta_raw(i, j, m);
+        for (int k = 0; k < (N + kNG - 1) / kNG; ++k) {
+          const int q0 = g + kNG * k;
+          const double wq = static_cast<double>(q0 < N);
+          const int q = q0 < N ? q0 : N - 1;
+          const bool lo = q < M;
+          const int seg = lo ? u - 1 : u;
+          const double sg = lo ? -1.0 : 1.0;  // B_lr^-1 = rowreverse(B_ul^-1) diag((-1)^m)
+          const double* bro = sm + L->bul + seg * M * M + (lo ? M - 1 - q : q - M) * M;
+          const int cpi = seg * N + (lo ? q + M : q - M);
+          double bt[M];
 #pragma unroll
-          for (int d = 0; d < 3; ++d) g[d] = Gcp[cpi * 6 + gsym(d, d2)];
-          return beta_raw(i, j, m2);
-        };
-        bm = load_cp(0, bt, g3);
-#pragma unroll
-        for (int q = 0; q < N; ++q) {
-          if (q + 1 < N) bm_n = load_cp(q + 1, bt2, g32);
-          __builtin_amdgcn_sched_barrier(0);
-          const double bm2 = bm * on;
+          for (int m = 0; m < M; ++m) bt[m] = (m & 1) ? sg * bro[m] : bro[m];
+          const double bm = ((m2 & 1) ? sg * bro[m2] : bro[m2]) * wq;
 #pragma unroll
           for (int d = 0; d < 3; ++d) {
-            const double gd = g3[d] * bm2;
+            const double gd = Gcp[cpi * 6 + gsym(d, d2)] * bm;
 #pragma unroll
-            for (int m = 0; m < M; ++m) col[d * M + m] = fma(gd, bt[m], col[d * M + m]);
+            for (int m = 0; m < M; ++m) acc[d * M + m] = fma(gd, bt[m], acc[d * M + m]);
           }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int m = 0; m < M; ++m) bt[m] = bt2[m];
-#pragma unroll
-          for (int d = 0; d < 3; ++d) g3[d] = g32[d];
-          bm = bm_n;
         }
       }
       MTG_TACC(221, tf);
       if (a > 0) {
-        // S_a[:, c] -= sum_t W[t][:] dinv[t] W[t][c]  (W = W_{a-1}, dinv on
-        // the diagonal of the packed L_{a-1}^-1); row t+1 is loaded while row
-        // t is applied.
+        // acc -= sum_t W[t][:] dinv[t] W[t][c]  over this row's t (W = W_{a-1},
+        // dinv on the diagonal of the packed L_{a-1}^-1).
+        // Row t + kNG is loaded while row t is applied (sched barriers keep
+        // the loads ahead: otherwise they are issued one pair at a time).
         const double* Wp = sm + L->W;
         const double* Lp = sm + L->Li + (a - 1) * kTri;
-        const double on = r0;
+        constexpr int KT = (BS + kNG - 1) / kNG;
         double wr[BS], wn[BS], wc, dt, wcn = 0.0, dtn = 0.0;
+        auto row = [&](int k, double* w, double* c, double* d) {
+          const int t0 = g + kNG * k;
+          const int t = t0 < BS ? t0 : BS - 1;
 #pragma unroll
-        for (int i = 0; i < BS; ++i) wr[i] = Wp[i];
-        wc = Wp[cc];
-        dt = Lp[0];
+          for (int i = 0; i < BS; ++i) w[i] = Wp[t * BS + i];
+          *c = Wp[t * BS + cc];
+          *d = Lp[tri(t, t)] * static_cast<double>(t0 < BS);
+        };
+        row(0, wr, &wc, &dt);
 #pragma unroll
-        for (int t = 0; t < BS; ++t) {
-          if (t + 1 < BS) {
-#pragma unroll
-            for (int i = 0; i < BS; ++i) wn[i] = Wp[(t + 1) * BS + i];
-            wcn = Wp[(t + 1) * BS + cc];
-            dtn = Lp[tri(t + 1, t + 1)];
-          }
+        for (int k = 0; k < KT; ++k) {
+          if (k + 1 < KT) row(k + 1, wn, &wcn, &dtn);
           __builtin_amdgcn_sched_barrier(0);
-          const double w = wc * dt * on;
+          const double w = wc * dt;
 #pragma unroll
-          for (int i = 0; i < BS; ++i) col[i] = fma(-wr[i], w, col[i]);
+          for (int i = 0; i < BS; ++i) acc[i] = fma(-wr[i], w, acc[i]);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < BS; ++i) wr[i] = wn[i];
@@ -555,37 +598,44 @@ struct Tube {
           dt = dtn;
         }
       }
+#pragma unroll
+      for (int i = 0; i < BS; ++i) col[i] = fma(rows_sum(acc[i]), r0, col[i]);
       // Forward elimination (below the pivot) on all columns at once; the
       // pivot column is broadcast with v_readlane.
       MTG_TACC(222, tf);
-      double pmin = 1.0, dpiv = 0.0;
+      double dpiv = 1.0;
 #pragma unroll
       for (int j = 0; j < BS; ++j) {
         const double piv = bcast(col[j], j);
-        pmin = fmin(pmin, piv);
-        dpiv = fma(is_zero(j - c), piv, dpiv);  // lane c < BS: its own pivot
+        dpiv = lane == j ? piv : dpiv;  // lane j: its own pivot
         if (j == BS - 1) break;
         const double f = col[j] * rcp64(piv > 0.0 ? piv : 1.0);
+        // All broadcasts of the step first, then the updates.
+        double pc[BS];
 #pragma unroll
-        for (int i = j + 1; i < BS; ++i) col[i] = fma(-bcast(col[i], j), f, col[i]);
+        for (int i = j + 1; i < BS; ++i) pc[i] = bcast(col[i], j);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = j + 1; i < BS; ++i) col[i] = fma(-pc[i], f, col[i]);
       }
-      bad |= !(pmin > 0.0);
+      bad |= __ballot(lane < BS && !(dpiv > 0.0)) != 0;
       MTG_TACC(223, tf);
-      // Lanes 0.. store 1 / pivot on the diagonal of the packed L_a^-1,
-      // BS.. its strictly lower columns, 2BS.. W_a (replacing W_{a-1}, which
-      // every lane has finished reading at the barrier).
+      // S_a lanes store 1 / pivot on the diagonal of the packed L_a^-1, the
+      // identity lanes its strictly lower columns, the C_a lanes W_a
+      // (replacing W_{a-1}, which every lane has read by the barrier).
+      // Offsets are selected per lane with integer masks (no branches),
+      // unused stores go to a per-lane dummy slot.
       __syncthreads();
       {
-        double* Li = sm + L->Li + a * kTri;
-        if (role == 0) {
-          Li[tri(cc, cc)] = rcp64(dpiv > 0.0 ? dpiv : 1.0);
-        } else if (role == 1) {
+        const int li = L->Li + a * kTri;
+        const int s0 = -izero(role), s1 = -izero(role - 1), s2 = -izero(role - 2);
+        sm[((li + tri(cc, cc)) & s0) | (dummy & ~s0)] = rcp64(dpiv > 0.0 ? dpiv : 1.0);
 #pragma unroll
-          for (int i = 1; i < BS; ++i)
-            if (i > cc) Li[tri(i, cc)] = col[i];
-        } else if (role == 2) {
-#pragma unroll
-          for (int i = 0; i < BS; ++i) sm[L->W + i * BS + cc] = col[i];
+        for (int i = 0; i < BS; ++i) {
+          const int a1 = s1 & ((cc - i) >> 31);  // identity lane, i > cc
+          const int o = ((li + tri(i, cc)) & a1) | ((L->W + i * BS + cc) & s2) |
+                        (dummy & ~(a1 | s2));
+          sm[o] = col[i];
         }
       }
       __syncthreads();
@@ -595,81 +645,105 @@ struct Tube {
   }
 
   // Solve K out = rhs with the block factors (rhs overwritten by y).
-  // Lanes 0..BS-1 own one row each.  W_a = L_a^-1 C_a is not stored; the
+  // Row i of a block belongs to lanes (g, i) of every row g, which share its
+  // dot products; row 0 writes.  W_a = L_a^-1 C_a is not stored; the
   // coupling is applied as C_a = I_3 (x) Po_a next to the packed L^-1:
   //   forward   y_a = L_a^-1 (b_a - C_{a-1}^T L_{a-1}^-T D_{a-1}^-1 y_{a-1})
   //   backward  x_a = L_a^-T D_a^-1 (y_a - L_a^-1 C_a x_{a+1}).
   // Triangular sums run over the full row with the out-of-triangle terms
-  // weighted by exact 0 (the unit diagonal by exact 1).
+  // weighted by exact 0 (the unit diagonal by exact 1).  tmp[0, BS) and
+  // tmp[BS, 2BS) are exchange buffers, tmp[2BS, 3BS) holds D^-1 y of the
+  // previous block.
   __device__ void solve(int rhs_off, int out_off) {
     double* tmp = sm + L->tmp;
     double* y = sm + rhs_off;
     double* xo = sm + out_off;
-    const bool act = lane < BS;
-    const int i = act ? lane : 0;
+    const int g = grp();
+    const int i = col_of() < BS ? col_of() : BS - 1;
+    const bool wr = kNG == 4 ? (g == 0 && col_of() < BS) : lane < BS;
     const int di = i / M, mi = i % M;
+    constexpr int KS = (BS + kNG - 1) / kNG;
     for (int a = 0; a < nv; ++a) {
       const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
       if (a > 0) {
-        // v = L_{a-1}^-T D_{a-1}^-1 y_{a-1} (row i), then t -= (C^T v)_i.
+        // v = L_{a-1}^-T (D_{a-1}^-1 y_{a-1}) (row i), then t -= (C^T v)_i.
         const double* Lp = Li - kTri;
-        const double* z = y + (a - 1) * BS;
         double v = 0.0;
 #pragma unroll
-        for (int k = 0; k < BS; ++k) {
-          const int kk = k > i ? k : i;
-          const double gt = static_cast<double>(k > i), eq = is_zero(k - i);
-          v = fma(fma(Lp[tri(kk, i)], gt, eq), z[k] * Lp[tri(k, k)], v);
+        for (int kk = 0; kk < KS; ++kk) {
+          const int k0 = g + kNG * kk;
+          const int k = k0 < BS ? k0 : BS - 1;
+          const int kx = k > i ? k : i;
+          const double gt = static_cast<double>(k > i && k0 < BS);
+          const double eq = is_zero(k0 - i);
+          v = fma(fma(Lp[tri(kx, i)], gt, eq), tmp[2 * BS + k], v);
         }
-        if (act) tmp[i] = v;
+        v = rows_sum(v);
+        if (wr) tmp[i] = v;
         __syncthreads();
         const double* Po = sm + L->Po + (a - 1) * M * M;
 #pragma unroll
         for (int m = 0; m < M; ++m) t = fma(-Po[m * M + mi], tmp[di * M + m], t);
       }
-      if (act) tmp[BS + i] = t;
+      if (wr) tmp[BS + i] = t;
       __syncthreads();
       double zi = 0.0;
 #pragma unroll
-      for (int k = 0; k < BS; ++k) {
-        const int kk = k < i ? k : i;
-        const double lt = static_cast<double>(k < i), eq = is_zero(k - i);
-        zi = fma(fma(Li[tri(i, kk)], lt, eq), tmp[BS + k], zi);
+      for (int kk = 0; kk < KS; ++kk) {
+        const int k0 = g + kNG * kk;
+        const int k = k0 < BS ? k0 : BS - 1;
+        const int kx = k < i ? k : i;
+        const double lt = static_cast<double>(k < i && k0 < BS);
+        const double eq = is_zero(k0 - i);
+        zi = fma(fma(Li[tri(i, kx)], lt, eq), tmp[BS + k], zi);
       }
-      if (act) y[a * BS + i] = zi;
+      zi = rows_sum(zi);
+      if (wr) {
+        y[a * BS + i] = zi;
+        tmp[2 * BS + i] = zi * Li[tri(i, i)];
+      }
       __syncthreads();
     }
     for (int a = nv - 1; a >= 0; --a) {
       const double* Li = sm + L->Li + a * kTri;
-      // u = C_a x_{a+1} (row i), exchanged for L_a^-1 u.
-      double u = 0.0;
+      double t = y[a * BS + i];
       if (a < nv - 1) {
+        // u = C_a x_{a+1} (row i), exchanged; t -= (L_a^-1 u)_i.
         const double* Po = sm + L->Po + a * M * M;
         const double* xn = xo + (a + 1) * BS + di * M;
+        double u = 0.0;
 #pragma unroll
         for (int m = 0; m < M; ++m) u = fma(Po[mi * M + m], xn[m], u);
-      }
-      if (act) tmp[i] = u;
-      __syncthreads();
-      double t = y[a * BS + i];
+        if (wr) tmp[i] = u;
+        __syncthreads();
+        double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < BS; ++k) {
-        const int kk = k < i ? k : i;
-        const double lt = static_cast<double>(k < i), eq = is_zero(k - i);
-        t = fma(-fma(Li[tri(i, kk)], lt, eq), tmp[k], t);
+        for (int kk = 0; kk < KS; ++kk) {
+          const int k0 = g + kNG * kk;
+          const int k = k0 < BS ? k0 : BS - 1;
+          const int kx = k < i ? k : i;
+          const double lt = static_cast<double>(k < i && k0 < BS);
+          const double eq = is_zero(k0 - i);
+          s = fma(fma(Li[tri(i, kx)], lt, eq), tmp[k], s);
+        }
+        t -= rows_sum(s);
       }
       t *= Li[tri(i, i)];
-      if (act) tmp[BS + i] = t;
+      if (wr) tmp[BS + i] = t;
       __syncthreads();
       double xi = 0.0;
 #pragma unroll
-      for (int k = 0; k < BS; ++k) {
-        const int kk = k > i ? k : i;
-        const double gt = static_cast<double>(k > i), eq = is_zero(k - i);
-        xi = fma(fma(Li[tri(kk, i)], gt, eq), tmp[BS + k], xi);
+      for (int kk = 0; kk < KS; ++kk) {
+        const int k0 = g + kNG * kk;
+        const int k = k0 < BS ? k0 : BS - 1;
+        const int kx = k > i ? k : i;
+        const double gt = static_cast<double>(k > i && k0 < BS);
+        const double eq = is_zero(k0 - i);
+        xi = fma(fma(Li[tri(kx, i)], gt, eq), tmp[BS + k], xi);
       }
-      if (act) xo[a * BS + i] = xi;
+      xi = rows_sum(xi);
+      if (wr) xo[a * BS + i] = xi;
       __syncthreads();
     }
   }

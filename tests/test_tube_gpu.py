@@ -133,3 +133,37 @@ def test_stale_control_point_times(ctx, dev, oracle):
     assert out["status"][0] == ref["status"] == 0
     assert rel_err_coeffs(out["coeffs"][0], ref["coeffs"]) <= 1e-6
     assert rel_err(out["cost"][0], ref["cost"]) <= 1e-6
+
+
+@pytest.mark.parametrize("n,r,S", [(4, 1, 3), (6, 2, 5), (8, 3, 4), (10, 4, 2), (12, 5, 6)])
+def test_polynomial_orders_vs_oracle(ctx, dev, oracle, n, r, S):
+    """Every supported N: the kernel's lane organisation differs for BS =
+    3 N / 2 <= 16 (row-split sums) and N = 12 (single group)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    m = n // 2
+    B = 6
+    items = []
+    for b in range(B):
+        v = oracle.random_vertices(m - 1, S, 3, -10.0, 10.0, 300 + 7 * n + b)
+        items.append((v, oracle.estimate_segment_times(v, 3.0, 5.0)))
+    pos = np.stack([v.vals[:, 0, :] for v, _ in items])
+    fv = np.zeros((B, 3, n))
+    for b, (v, _) in enumerate(items):
+        fv[b, :, :m] = v.vals[0, :m, :].T
+        fv[b, :, m:] = v.vals[S, :m, :].T
+    times = np.stack([t for _, t in items])
+    radii = np.full((B, S, 2), 0.15)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    out = mtg.tube_solve(ctx, n, r, T(pos), T(fv), T(times), T(times), T(radii), tol=1e-10,
+                         max_iter=100)
+    o = {k: v.cpu().numpy() for k, v in out.items()}
+    agree = 0
+    for b, (v, t) in enumerate(items):
+        ref = oracle.tube_solve(n, r, v, t, np.full((S, 2), 0.15), tol=1e-10, max_iter=100)
+        assert o["status"][b] == ref["status"], b
+        if ref["status"] != 0:
+            continue
+        agree += 1
+        assert rel_err_coeffs(o["coeffs"][b], ref["coeffs"]) <= 1e-6, b
+        assert rel_err(o["cost"][b], ref["cost"]) <= 1e-6, b
+    assert agree >= B // 2

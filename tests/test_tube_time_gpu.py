@@ -111,11 +111,15 @@ def test_tube_time_cost_repeated_calls(ctx, dev, oracle):
 
 def test_tube_time_optimize_vs_oracle(ctx, dev, oracle):
     """Same steps as the oracle's driver: accepted points, evaluation counts
-    and the final J, with one divergent path allowed (accept/reject compares
-    J values that agree only to the QCQP tolerance)."""
+    and the final J on at least 3/4 of the problems.  Paths can diverge:
+    accept/reject compares J values that agree only to the QCQP tolerance,
+    and a QCQP breakdown (about 1-2% of random tube solves, in either
+    implementation, depending on rounding: tools/tube_status_agreement.py) ends a
+    path, so at 10 evaluations roughly one problem in seven takes another
+    path."""
     import mav_tube_trajectory_generation_amd as mtg
     S, E = 4, 10
-    items = _batch(oracle, S, range(400, 406))
+    items = _batch(oracle, S, range(400, 416))
     t0 = np.stack([t for _, t in items])
     pos, fv, radii = _geometry(dev, items)
     out = mtg.tube_time_optimize(ctx, N, R, pos, fv, radii, _T(dev, t0), max_evals=E)
@@ -141,7 +145,7 @@ def test_tube_time_optimize_vs_oracle(ctx, dev, oracle):
                                                max_evals=E)
         if er == ev[b] and np.max(np.abs(T[b] - tr)) <= 1e-6 * np.max(tr):
             agree += 1
-    assert agree >= len(items) - 1 and breakdowns <= 1
+    assert agree >= 0.75 * len(items) and breakdowns <= 2
 
 
 def test_tube_time_rejects_bad_arguments(ctx, dev, oracle):
