@@ -50,7 +50,6 @@ struct TubeLayout {
   int Li;                 // nv*BS(BS+1)/2 L_a^-1 packed by rows, diagonal = 1/pivot
   int W;                  // BS*BS  W_a of the current block, row-major
   int Gc;                 // S*N*6  per control point: sum lam Hess + lam/s w w^T (sym)
-  int tmp;                // 3*BS+2 solve scratch (last slot: dummy store target)
   int ndouble;
   size_t bytes() const { return sizeof(double) * ndouble; }
 };
@@ -87,7 +86,6 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   o += (nv * tri > S * (2 * N - 1) ? nv * tri : S * (2 * N - 1));
   l.W = o;    o += BS * BS;
   l.Gc = o;   o += S * N * 6;
-  l.tmp = o;  o += 3 * BS + 2;
   l.ndouble = o;
   return l;
 }
@@ -646,16 +644,16 @@ struct Tube {
 
   // Solve K out = rhs with the block factors (rhs overwritten by y).
   // Row i of a block belongs to lanes (g, i) of every row g, which share its
-  // dot products; row 0 writes.  W_a = L_a^-1 C_a is not stored; the
-  // coupling is applied as C_a = I_3 (x) Po_a next to the packed L^-1:
+  // dot products; the vectors of the recurrence stay in registers (lane k
+  // holds entry k) and move between lanes with __shfl, so the only barriers
+  // are between the two sweeps and at the end.  W_a = L_a^-1 C_a is not
+  // stored; the coupling is applied as C_a = I_3 (x) Po_a next to the
+  // packed L^-1:
   //   forward   y_a = L_a^-1 (b_a - C_{a-1}^T L_{a-1}^-T D_{a-1}^-1 y_{a-1})
   //   backward  x_a = L_a^-T D_a^-1 (y_a - L_a^-1 C_a x_{a+1}).
   // Triangular sums run over the full row with the out-of-triangle terms
-  // weighted by exact 0 (the unit diagonal by exact 1).  tmp[0, BS) and
-  // tmp[BS, 2BS) are exchange buffers, tmp[2BS, 3BS) holds D^-1 y of the
-  // previous block.
+  // weighted by exact 0 (the unit diagonal by exact 1).
   __device__ void solve(int rhs_off, int out_off) {
-    double* tmp = sm + L->tmp;
     double* y = sm + rhs_off;
     double* xo = sm + out_off;
     const int g = grp();
@@ -663,89 +661,69 @@ struct Tube {
     const bool wr = kNG == 4 ? (g == 0 && col_of() < BS) : lane < BS;
     const int di = i / M, mi = i % M;
     constexpr int KS = (BS + kNG - 1) / kNG;
+    // L^-1 row i (k < i) / column i (k > i) coefficient of this lane's k-th
+    // term, and the term's index.
+    auto kidx = [&](int kk) {
+      const int k0 = g + kNG * kk;
+      return k0 < BS ? k0 : BS - 1;
+    };
+    auto lrow = [&](const double* Lb, int kk) {  // (L^-1)[i][k], unit diagonal
+      const int k0 = g + kNG * kk, k = kidx(kk);
+      const int kx = k < i ? k : i;
+      return fma(Lb[tri(i, kx)], static_cast<double>(k < i && k0 < BS), is_zero(k0 - i));
+    };
+    auto lcol = [&](const double* Lb, int kk) {  // (L^-1)[k][i], unit diagonal
+      const int k0 = g + kNG * kk, k = kidx(kk);
+      const int kx = k > i ? k : i;
+      return fma(Lb[tri(kx, i)], static_cast<double>(k > i && k0 < BS), is_zero(k0 - i));
+    };
+    double u = 0.0;  // D_{a-1}^-1 y_{a-1}, entry i
     for (int a = 0; a < nv; ++a) {
       const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
       if (a > 0) {
-        // v = L_{a-1}^-T (D_{a-1}^-1 y_{a-1}) (row i), then t -= (C^T v)_i.
+        // v = L_{a-1}^-T u (row i), then t -= (C^T v)_i.
         const double* Lp = Li - kTri;
         double v = 0.0;
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          const int k0 = g + kNG * kk;
-          const int k = k0 < BS ? k0 : BS - 1;
-          const int kx = k > i ? k : i;
-          const double gt = static_cast<double>(k > i && k0 < BS);
-          const double eq = is_zero(k0 - i);
-          v = fma(fma(Lp[tri(kx, i)], gt, eq), tmp[2 * BS + k], v);
-        }
+        for (int kk = 0; kk < KS; ++kk) v = fma(lcol(Lp, kk), __shfl(u, kidx(kk)), v);
         v = rows_sum(v);
-        if (wr) tmp[i] = v;
-        __syncthreads();
         const double* Po = sm + L->Po + (a - 1) * M * M;
 #pragma unroll
-        for (int m = 0; m < M; ++m) t = fma(-Po[m * M + mi], tmp[di * M + m], t);
+        for (int m = 0; m < M; ++m) t = fma(-Po[m * M + mi], __shfl(v, di * M + m), t);
       }
-      if (wr) tmp[BS + i] = t;
-      __syncthreads();
-      double zi = 0.0;
+      double z = 0.0;
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int k0 = g + kNG * kk;
-        const int k = k0 < BS ? k0 : BS - 1;
-        const int kx = k < i ? k : i;
-        const double lt = static_cast<double>(k < i && k0 < BS);
-        const double eq = is_zero(k0 - i);
-        zi = fma(fma(Li[tri(i, kx)], lt, eq), tmp[BS + k], zi);
-      }
-      zi = rows_sum(zi);
-      if (wr) {
-        y[a * BS + i] = zi;
-        tmp[2 * BS + i] = zi * Li[tri(i, i)];
-      }
-      __syncthreads();
+      for (int kk = 0; kk < KS; ++kk) z = fma(lrow(Li, kk), __shfl(t, kidx(kk)), z);
+      z = rows_sum(z);
+      u = z * Li[tri(i, i)];
+      if (wr) y[a * BS + i] = z;
     }
+    __syncthreads();
+    double xn = 0.0;  // x_{a+1}, entry i
     for (int a = nv - 1; a >= 0; --a) {
       const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
       if (a < nv - 1) {
-        // u = C_a x_{a+1} (row i), exchanged; t -= (L_a^-1 u)_i.
+        // c = C_a x_{a+1} (row i); t -= (L_a^-1 c)_i.
         const double* Po = sm + L->Po + a * M * M;
-        const double* xn = xo + (a + 1) * BS + di * M;
-        double u = 0.0;
+        double c = 0.0;
 #pragma unroll
-        for (int m = 0; m < M; ++m) u = fma(Po[mi * M + m], xn[m], u);
-        if (wr) tmp[i] = u;
-        __syncthreads();
+        for (int m = 0; m < M; ++m) c = fma(Po[mi * M + m], __shfl(xn, di * M + m), c);
         double s = 0.0;
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          const int k0 = g + kNG * kk;
-          const int k = k0 < BS ? k0 : BS - 1;
-          const int kx = k < i ? k : i;
-          const double lt = static_cast<double>(k < i && k0 < BS);
-          const double eq = is_zero(k0 - i);
-          s = fma(fma(Li[tri(i, kx)], lt, eq), tmp[k], s);
-        }
+        for (int kk = 0; kk < KS; ++kk) s = fma(lrow(Li, kk), __shfl(c, kidx(kk)), s);
         t -= rows_sum(s);
       }
       t *= Li[tri(i, i)];
-      if (wr) tmp[BS + i] = t;
-      __syncthreads();
-      double xi = 0.0;
+      double x = 0.0;
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int k0 = g + kNG * kk;
-        const int k = k0 < BS ? k0 : BS - 1;
-        const int kx = k > i ? k : i;
-        const double gt = static_cast<double>(k > i && k0 < BS);
-        const double eq = is_zero(k0 - i);
-        xi = fma(fma(Li[tri(kx, i)], gt, eq), tmp[BS + k], xi);
-      }
-      xi = rows_sum(xi);
-      if (wr) xo[a * BS + i] = xi;
-      __syncthreads();
+      for (int kk = 0; kk < KS; ++kk) x = fma(lcol(Li, kk), __shfl(t, kidx(kk)), x);
+      x = rows_sum(x);
+      xn = x;
+      if (wr) xo[a * BS + i] = x;
     }
+    __syncthreads();
   }
 
   __device__ static double wave_max(double x) {
