@@ -195,9 +195,9 @@ def load_pmc_traffic(workload, config_key):
     try:
         with open(path) as f:
             data = json.load(f)
-        entry = data.get(workload, {})
-        if entry.get("config") == config_key:
-            return entry.get("bytes_per_launch")
+        for entry in data.values():  # keyed by profile tag; matched by config
+            if entry.get("config") == config_key:
+                return entry.get("bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None

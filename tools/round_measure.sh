@@ -1,16 +1,34 @@
-# Whole measurement pass of a round (run on the GPU box via gpurun from the
-# repo root): default bench (with the CPU baseline), the other workloads,
-# rocprofv3 kernel-trace + PMC passes per workload, the batch sweep.
-# Then, in the container: tools/pmc_summary.py per tag.
+#!/bin/bash
+# Whole measurement pass of a round, in two gpurun calls from the repo root:
+#   bash tools/round_measure.sh benches    -- every bench line
+#   bash tools/round_measure.sh profiles   -- rocprofv3 kernel stats, HBM PMC
+#                                             passes, SQ counters, batch sweep
+# Then, in the container: tools/pmc_summary.py / tools/sq_summary.py per tag
+#  and copy the bench lines to profiles/<round>_bench_*.json.
 set -e -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python bench.py > gpurun_out/bench_linear.json 2> gpurun_out/bench_linear.err
-timeout -k 10 300 python bench.py --workload time --steps 20 --warmup 3 > gpurun_out/bench_time.json 2> gpurun_out/bench_time.err
-timeout -k 10 300 python bench.py --workload time --soft --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_time_soft.json 2> gpurun_out/bench_time_soft.err
-timeout -k 10 300 python bench.py --workload tube --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_tube.json 2> gpurun_out/bench_tube.err
-timeout -k 10 300 python bench.py --workload time-qcqp --steps 5 --warmup 1 > gpurun_out/bench_time_qcqp.json 2> gpurun_out/bench_time_qcqp.err
-bash tools/profile.sh linear
-bash tools/profile.sh time --workload time --steps 5 --warmup 1
-bash tools/profile.sh tube --workload tube --steps 5 --warmup 1
-timeout -k 10 300 python tools/sweep.py > gpurun_out/sweep_linear.jsonl 2>&1
+B() { timeout -k 10 300 python bench.py "$@"; }
+case "${1:-benches}" in
+  benches)
+    B > gpurun_out/bench_linear.json 2> gpurun_out/bench_linear.err
+    B --batch 8192 --no-cpu-baseline > gpurun_out/bench_linear_8192.json 2> gpurun_out/bench_linear_8192.err
+    B --batch 65536 --no-cpu-baseline --steps 50 --warmup 5 > gpurun_out/bench_linear_65536.json 2> gpurun_out/bench_linear_65536.err
+    B --workload tube --steps 20 --warmup 3 > gpurun_out/bench_tube.json 2> gpurun_out/bench_tube.err
+    B --workload time --steps 20 --warmup 3 > gpurun_out/bench_time.json 2> gpurun_out/bench_time.err
+    B --workload time --soft --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_time_soft.json 2> gpurun_out/bench_time_soft.err
+    B --workload time-qcqp --steps 5 --warmup 1 > gpurun_out/bench_time_qcqp.json 2> gpurun_out/bench_time_qcqp.err
+    B --workload extrema > gpurun_out/bench_extrema.json 2> gpurun_out/bench_extrema.err
+    B --workload sample > gpurun_out/bench_sample.json 2> gpurun_out/bench_sample.err
+    ;;
+  profiles)
+    bash tools/profile.sh linear
+    bash tools/profile.sh linear_65536 --batch 65536 --steps 20 --warmup 2
+    bash tools/profile.sh tube --workload tube --steps 5 --warmup 1
+    bash tools/profile.sh time --workload time --steps 5 --warmup 1
+    bash tools/pmc_sq.sh tube --workload tube --steps 5 --warmup 1
+    bash tools/pmc_sq.sh linear_65536 --batch 65536 --steps 20 --warmup 2
+    bash tools/pmc_sq.sh linear
+    timeout -k 10 300 python tools/sweep.py > gpurun_out/sweep_linear.jsonl 2>&1
+    ;;
+esac
 echo ALLDONE
