@@ -419,19 +419,30 @@ def main():
         torch.cuda.synchronize(dev)
         dist.barrier()
     if use_graph:
-        try:
+        try:  # capture only: nothing executes (no collective runs) here
             for name, n in (("warmup", args.warmup), ("timed", args.steps)):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     for _ in range(n):
                         step()
                 graphs[name] = g
-            graphs["warmup"].replay()
         except Exception as exc:  # capture unsupported here: eager launches
             use_graph = False
             graph_note = f" (graph capture failed: {type(exc).__name__}; eager)"
             torch.cuda.synchronize(dev)
             print(f"bench: graph capture failed, eager: {exc}", file=sys.stderr)
+        if world > 1:
+            # Every rank must take the same path, or a replayed all-gather on
+            # one rank would wait for an eager one that never comes.
+            ok = torch.tensor([1.0 if use_graph else 0.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() < 0.5 and use_graph:
+                use_graph = False
+                graph_note = " (graph capture failed on another rank; eager)"
+        if use_graph:
+            graphs["warmup"].replay()
+        else:
+            graphs = {}
     if not use_graph:
         for _ in range(args.warmup):
             step()
