@@ -202,4 +202,120 @@ hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
 #undef CALL
 }
 
+// ---------------------------------------------------------------------------
+// evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:2735-2766) for
+// every constraint in one launch.  Workgroup = one trajectory; lane group c
+// (a whole number of waves, so the derivative switch is wave-uniform) runs
+// constraint c's search over the (segment, part) items; each group reduces
+// in the reference's candidate order, then lane 0 forms
+// cost = sum_c min(maximum_cost, exp((max_c - lim_c) / lim_c * weight)).
+// The searches of all constraints run concurrently instead of one dependent
+// launch each.
+constexpr int kSoftBlockMax = 512;  // 2 waves per SIMD: up to 256 VGPRs, no scratch
+
+template <int N>
+__global__ __launch_bounds__(kSoftBlockMax) void soft_cost_kernel(int D, int S, int parts, int log2parts,
+                                                         int group, const double* __restrict__ coeffs,
+                                                         const double* __restrict__ times,
+                                                         SoftSpec spec, double* __restrict__ maxima,
+                                                         double* __restrict__ cost) {
+  extern __shared__ double sm_soft[];
+  const int per = S * D * N;
+  double* c_s = sm_soft;          // per + S
+  double* val_s = sm_soft + per + S;  // blockDim.x
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  for (int i = tid; i < per; i += blockDim.x) c_s[i] = coeffs[b * per + i];
+  for (int i = tid; i < S; i += blockDim.x) c_s[per + i] = times[b * S + i];
+  __syncthreads();
+  const int cidx = tid / group, r = tid - cidx * group;
+  const bool active = cidx < spec.n && r < S * parts;
+  double best_v = -1.0, best_t = 0.0, mv = 0.0, mt = 0.0;
+  if (active) {
+    const int s = r >> log2parts, part = r & (parts - 1);
+    const double* c = c_s + s * D * N;
+    const double T = c_s[per + s];
+    int K = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxSoftConstraints; ++q)  // compile-time indices
+      if (q == cidx) K = spec.derivative[q];
+    switch (K) {  // wave-uniform: groups are whole waves
+      case 0: ext_segment_search<N, 0>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt); break;
+      case 1: ext_segment_search<N, 1>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt); break;
+      case 2: ext_segment_search<N, 2>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt); break;
+      case 3:
+        if constexpr (N >= 5)
+          ext_segment_search<N, 3>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt);
+        break;
+      case 4:
+        if constexpr (N >= 6)
+          ext_segment_search<N, 4>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt);
+        break;
+      default: break;
+    }
+  }
+  val_s[tid] = best_v;
+  __syncthreads();
+  // Group leaders: maximum in candidate order (strict '>', Extremum() = 0).
+  if (cidx < spec.n && r == 0) {
+    double v = 0.0;
+    for (int i = 0; i < S * parts; ++i) {
+      const double x = val_s[tid + i];
+      if (x > v) v = x;
+    }
+    val_s[tid] = sqrt(v);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double total = 0.0;
+#pragma unroll
+    for (int q = 0; q < kMaxSoftConstraints; ++q) {
+      if (q >= spec.n) break;
+      const double m = val_s[q * group];
+      if (maxima) maxima[b * spec.n + q] = m;
+      const double relative_violation = (m - spec.limit[q]) / spec.limit[q];
+      total += fmin(spec.maximum_cost, exp(relative_violation * spec.weight));
+    }
+    cost[b] = total;
+  }
+}
+
+hipError_t launch_soft_cost(int N, int D, int S, int64_t B, const double* coeffs,
+                            const double* times, const SoftSpec& spec, double* maxima,
+                            double* cost, hipStream_t st) {
+  if (S < 1 || spec.n < 1 || spec.n > kMaxSoftConstraints) return hipErrorInvalidValue;
+  int parts = kExtParts, log2parts = 3;
+  auto group_of = [&](int p) { return (S * p + 63) / 64 * 64; };
+  while (parts > 1 && spec.n * group_of(parts) > kSoftBlockMax) {
+    parts >>= 1;
+    --log2parts;
+  }
+  const int group = group_of(parts);
+  const int threads = spec.n * group;
+  if (threads > kSoftBlockMax) return hipErrorNotSupported;  // caller: one launch per constraint
+  const size_t lds = sizeof(double) * (static_cast<size_t>(S) * D * N + S + threads);
+  const dim3 grid(static_cast<unsigned>(B));
+#define CALL(n)                                                                                 \
+  {                                                                                             \
+    if (lds > 65536) {                                                                          \
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(soft_cost_kernel<n>), \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                               static_cast<int>(lds));                          \
+      if (e != hipSuccess) return e;                                                            \
+    }                                                                                           \
+    hipLaunchKernelGGL(soft_cost_kernel<n>, grid, dim3(threads), lds, st, D, S, parts, log2parts, \
+                       group, coeffs, times, spec, maxima, cost);                               \
+    return hipGetLastError();                                                                   \
+  }
+  switch (N) {
+    case 4: CALL(4)
+    case 6: CALL(6)
+    case 8: CALL(8)
+    case 10: CALL(10)
+    case 12: CALL(12)
+    default: return hipErrorInvalidValue;
+  }
+#undef CALL
+}
+
 }  // namespace mtg

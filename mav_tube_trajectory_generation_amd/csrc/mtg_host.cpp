@@ -435,18 +435,35 @@ int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeff
       n_constraints < 1 || n_constraints > mtg::kMaxSoftConstraints || !derivatives ||
       !limits)
     return MTG_ERR_INVALID_ARG;
-  mtg::SoftLimits lim{};
-  lim.n = n_constraints;
+  mtg::SoftSpec spec{};
+  spec.n = n_constraints;
+  spec.weight = weight;
+  spec.maximum_cost = maximum_cost;
   for (int c = 0; c < n_constraints; ++c) {
     // addMaximumMagnitudeConstraint: CHECK_GE(derivative, 0), CHECK_GE(value, 0)
     if (derivatives[c] < 0 || derivatives[c] > mtg::kMaxExtremaDerivative ||
         N - derivatives[c] - 1 <= 0 || !(limits[c] >= 0.0))
       return MTG_ERR_INVALID_ARG;
-    lim.value[c] = limits[c];
+    spec.derivative[c] = derivatives[c];
+    spec.limit[c] = limits[c];
   }
   if (B == 0) return MTG_OK;
   if (!coeffs || !times || !maxima || !cost) return MTG_ERR_INVALID_ARG;
+  if (B > 0x7fffffff) return MTG_ERR_INVALID_ARG;
   const hipStream_t st = static_cast<hipStream_t>(stream);
+  // Small batches are latency-bound: all constraints in one launch (measured
+  // 69.6 -> 43.8 us at B = 1024, 2 constraints).  Large batches are
+  // throughput-bound and pack 3 trajectories per workgroup in the
+  // per-constraint kernel (74 vs 48 M evaluations/s at B = 65 536).
+  if (B < mtg::kSoftOneLaunchMaxBatch) {
+    const hipError_t e = mtg::launch_soft_cost(N, D, S, B, coeffs, times, spec, maxima, cost, st);
+    if (e != hipErrorNotSupported) return from_hip(e);
+  }
+  // One launch per constraint, the last one forming the cost (also for
+  // trajectories whose lane groups exceed one workgroup).
+  mtg::SoftLimits lim{};
+  lim.n = n_constraints;
+  for (int c = 0; c < n_constraints; ++c) lim.value[c] = limits[c];
   const mtg::SoftCostArgs none{};
   const mtg::SoftCostArgs last{cost, lim, weight, maximum_cost};
   for (int c = 0; c < n_constraints; ++c) {

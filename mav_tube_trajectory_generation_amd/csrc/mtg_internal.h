@@ -168,6 +168,19 @@ struct MinOut {
   double* value;
   int32_t* segment;
 };
+// All constraints of a soft-constraint evaluation in one launch
+// (mtg_soft_constraint_cost): one workgroup per trajectory, one
+// wave-aligned lane group per constraint, the cost formed in the workgroup.
+constexpr int64_t kSoftOneLaunchMaxBatch = 4096;
+struct SoftSpec {
+  int n;
+  int derivative[kMaxSoftConstraints];
+  double limit[kMaxSoftConstraints];
+  double weight, maximum_cost;
+};
+hipError_t launch_soft_cost(int N, int D, int S, int64_t B, const double* coeffs,
+                            const double* times, const SoftSpec& spec, double* maxima,
+                            double* cost, hipStream_t st);
 hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
                                 const double* coeffs, const double* times, double* max_time,
                                 double* max_value, int32_t* max_segment, int value_stride,

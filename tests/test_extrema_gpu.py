@@ -130,6 +130,33 @@ def test_soft_constraint_cost_vs_oracle(ctx, dev, oracle):
     assert torch.all(out["cost"] == 1.0e12)
 
 
+@pytest.mark.parametrize("S,ders,lims,B", [
+    (2, [0, 1, 2, 3, 4], [20.0, 3.0, 1.5, 5.0, 9.0], 24),   # one launch, 5 lane groups
+    (20, [1, 2, 3], [3.0, 1.5, 4.0], 16),                   # one launch, fewer parts
+    (10, [2, 1], [1.5, 3.0], 4100),                          # per-constraint launches
+])
+def test_soft_constraint_cost_launch_shapes(ctx, dev, oracle, S, ders, lims, B):
+    """Both launch organisations of mtg_soft_constraint_cost (all constraints
+    in one workgroup per trajectory below 4096 trajectories, one launch per
+    constraint above) against the oracle, with up to five constraints."""
+    import mav_tube_trajectory_generation_amd as mtg
+    N, D = 10, 3
+    n_ref = 12
+    coeffs, times = _problems(oracle, N, D, S, list(range(900, 900 + n_ref)))
+    reps = (B + n_ref - 1) // n_ref
+    cb = np.ascontiguousarray(np.tile(coeffs, (reps, 1, 1, 1))[:B])
+    tb = np.ascontiguousarray(np.tile(times, (reps, 1))[:B])
+    out = mtg.soft_constraint_cost(torch.from_numpy(cb).to(dev), torch.from_numpy(tb).to(dev),
+                                   ders, lims, weight=100.0)
+    torch.cuda.synchronize()
+    cost = out["cost"].cpu().numpy()
+    maxima = out["maxima"].cpu().numpy()
+    for b in list(range(n_ref)) + [B - 1]:
+        rc, rm = oracle.soft_constraint_cost(N, cb[b], tb[b], ders, lims, 100.0)
+        assert np.allclose(maxima[b], rm, rtol=1e-10, atol=0), b
+        assert abs(cost[b] - rc) <= 1e-8 * rc, (b, cost[b], rc)
+
+
 def test_extrema_zero_and_edge_inputs(ctx, dev, oracle):
     """Identically-zero derivative (no roots; Extremum stays {0, 0, 0}) and a
     maximum forced onto the end of the last segment."""
