@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=5)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph)")
+    p.add_argument("--select", action="store_true",
+                   help="linear: include the device selection step (RCCL all-gather + argmin, "
+                        "always on at --gpus > 1) also on one GPU")
     p.add_argument("--kernel", default="auto",
                    choices=["auto", "generic", "standard", "lane"],
                    help="linear-solve kernel (mtg_plan_set_kernel); auto picks by batch size")
@@ -245,10 +248,31 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    select = world > 1 or args.select
+    # RCCL prints its version banner on stdout at communicator set-up; keep
+    # stdout for the one JSON line (the banner goes to stderr).
+    import contextlib
+
+    @contextlib.contextmanager
+    def stdout_to_stderr():
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            yield
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+
+    if select:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        with stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
@@ -277,7 +301,7 @@ def main():
 
         def step():
             plan.solve(fixed_d, times_d, free=False, out=out)
-            if world > 1:  # RCCL all-gather of (cost, index) + global argmin, on device
+            if select:  # local argmin kernel, RCCL all-gather, global argmin kernel
                 return select_best_device(out["cost"], global_batch)
             return None
 
@@ -413,11 +437,12 @@ def main():
     use_graph = not args.no_graph
     graph_note = ""
     graphs = {}
-    if world > 1:
-        for _ in range(max(args.warmup, 2)):
-            step()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
+    if select:  # communicator set up and first collectives outside any capture
+        with stdout_to_stderr():
+            for _ in range(max(args.warmup, 2)):
+                step()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
     if use_graph:
         try:  # capture only: nothing executes (no collective runs) here
             for name, n in (("warmup", args.warmup), ("timed", args.steps)):
@@ -504,8 +529,9 @@ def main():
                 "traffic": traffic, "alg_bytes_per_launch": alg_bytes}
     roof["kernel_ms"] = kernel_ms
     roof["kernel_timing"] = timing
-    if world > 1:
-        roof["kernel_timing"] += "; per-step device time includes the all-gather and argmin"
+    if select and wl == "linear":
+        roof["kernel_timing"] += ("; per-step device time includes the selection (local argmin "
+                                  "kernel, RCCL all-gather, global argmin kernel)")
 
     if rank == 0:
         cpu = None
@@ -516,7 +542,8 @@ def main():
         cfg = {"workload": config_name(wl, B, world, S), "global_batch": global_batch,
                "kernel": plan.kernel_for_batch(B) if wl == "linear" else None,
                "batch_per_gpu": B, "segments": S, "N": N, "D": D, "r": r,
-               "parallelism": f"shard{world}"}
+               "parallelism": f"shard{world}",
+               "selection": bool(select and wl == "linear")}
         if useful_per_step is not None:
             cfg["converged_per_step"] = useful_per_step
         line = {
@@ -537,7 +564,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if world > 1:
+    if select:
         dist.destroy_process_group()
 
 

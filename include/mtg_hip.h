@@ -491,6 +491,22 @@ int mtg_collision_cost(const mtg_plan* plan, int64_t B, const double* coeffs,
                        double* grad_coeffs, double* grad_free, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Selection for the multi-GPU path (BASELINE config 4: the
+ * shards solve independently and the ranks all-gather costs for
+ * selection).  mtg_select_local reduces rank `rank`'s shard of `count`
+ * costs (device), global indices start .. start+count-1, to the triple
+ * out[3] = (cost, global index, rank) (device): NaN never wins, the lowest
+ * index wins ties, an empty shard gives (+inf, -1, rank), all NaN / +inf
+ * gives the shard's first index.  After the caller all-gathers the triples
+ * (RCCL, 24 B per rank, rank order), mtg_select_global picks the winner of
+ * `world` triples into out[3]: smallest cost, first rank on ties, empty
+ * shards and NaN last, the first triple if none is finite.  One launch
+ * each, stream-ordered, graph-capturable. */
+int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank, double* out,
+                     void* stream);
+int mtg_select_global(const double* triples, int world, double* out, void* stream);
+
+/* ------------------------------------------------------------------------
  * Host-side input generation (vertex.cpp:27-82, 228-269) for batches:
  * trajectory b uses createRandomVertices(max_derivative = M-1, S, +/-pos_bound,
  * seed = seed0 + b) and estimateSegmentTimes(v_max, a_max) (Nfabian, 6.5).

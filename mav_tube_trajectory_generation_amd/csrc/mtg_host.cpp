@@ -475,6 +475,20 @@ int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeff
   return MTG_OK;
 }
 
+int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank, double* out,
+                     void* stream) {
+  if (count < 0 || start < 0 || rank < 0 || !out || (count > 0 && !costs))
+    return MTG_ERR_INVALID_ARG;
+  return from_hip(mtg::launch_select_local(costs, count, start, rank, out,
+                                           static_cast<hipStream_t>(stream)));
+}
+
+int mtg_select_global(const double* triples, int world, double* out, void* stream) {
+  if (world < 1 || !triples || !out) return MTG_ERR_INVALID_ARG;
+  return from_hip(mtg::launch_select_global(triples, world, out,
+                                            static_cast<hipStream_t>(stream)));
+}
+
 int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* times,
                          double* Q, double* A, double* Ainv, double* H, void* stream) {
   if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || n < 0 || (n && !times))

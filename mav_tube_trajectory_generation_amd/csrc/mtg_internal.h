@@ -187,4 +187,9 @@ hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
                                 int value_offset, const SoftCostArgs& soft, hipStream_t st,
                                 const MinOut* mino = nullptr);
 
+// Multi-GPU selection (mtg_select.hip).
+hipError_t launch_select_local(const double* costs, int64_t count, int64_t start, int rank,
+                               double* out, hipStream_t st);
+hipError_t launch_select_global(const double* triples, int world, double* out, hipStream_t st);
+
 }  // namespace mtg

@@ -9,7 +9,10 @@ broadcast of the winning trajectory's coefficients from its owner.
 Two selection paths:
   select_best_device  each rank reduces its shard to one (cost, global index,
                       rank) triple on the device, the triples are all-gathered
-                      (24 B per rank) and reduced again on the device.  No host
+                      (24 B per rank) and reduced again on the device: on GPU
+                      tensors one HIP launch each (mtg_select_local /
+                      mtg_select_global) around the RCCL all-gather; on CPU
+                      tensors (gloo) the same rule with torch ops.  No host
                       synchronisation, so it can sit inside a timed loop or a
                       captured graph.
   select_best         the same, returned as Python numbers (one sync).
@@ -19,6 +22,13 @@ Two selection paths:
 """
 import torch
 import torch.distributed as dist
+
+
+def _hip():
+    """The HIP selection kernels (device tensors only; no CPU fallback)."""
+    from ._abi import check, lib
+    from .batch import _ptr, _stream
+    return lib(), check, _ptr, _stream
 
 
 def shard_range(global_batch, world, rank):
@@ -54,8 +64,16 @@ def local_best(local_costs, global_batch, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     start, count = shard_range(global_batch, world, rank)
-    # Only kernels with scalar arguments (no host->device copies), so the
-    # whole selection can be captured in a graph.
+    if local_costs.is_cuda:  # one HIP launch (mtg_select_local)
+        lib, check, ptr, stream = _hip()
+        c = local_costs
+        if c.dtype != torch.float64 or not c.is_contiguous():
+            c = c.to(torch.float64).contiguous()
+        out = torch.empty(3, dtype=torch.float64, device=c.device)
+        check(lib.mtg_select_local(ptr(c), count, start, rank, ptr(out), stream(c.device)),
+              "mtg_select_local")
+        return out
+    # CPU tensors (gloo): the same rule with torch ops.
     out = torch.full((3,), float(rank), dtype=torch.float64, device=local_costs.device)
     if count == 0:
         out[0] = float("inf")
@@ -79,6 +97,12 @@ def select_best_device(local_costs, global_batch, group=None):
     mine = local_best(local_costs, global_batch, group)
     flat = torch.empty(world * 3, dtype=torch.float64, device=mine.device)
     dist.all_gather_into_tensor(flat, mine, group=group)
+    if flat.is_cuda:  # one HIP launch (mtg_select_global)
+        lib, check, ptr, stream = _hip()
+        out = torch.empty(3, dtype=torch.float64, device=flat.device)
+        check(lib.mtg_select_global(ptr(flat), world, ptr(out), stream(flat.device)),
+              "mtg_select_global")
+        return out
     allv = flat.view(world, 3)
     # Empty shards (index -1) only win when every shard is empty.
     key = torch.where(allv[:, 1] < 0, torch.full_like(allv[:, 0], float("nan")), allv[:, 0])

@@ -1,0 +1,117 @@
+"""GPU selection kernels of the multi-GPU path (mtg_select_local /
+mtg_select_global) against the selection rule written in
+numpy, and the whole select_best_device step on a one-rank RCCL group."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _ref_local(c, start, rank):
+    if len(c) == 0:
+        return (math.inf, -1.0, float(rank))
+    k = np.where(np.isnan(c), np.inf, c)
+    i = int(np.argmin(k))  # first minimum
+    return (float(k[i]), float(i + start), float(rank))
+
+
+def _ref_global(t):
+    keys = np.where((t[:, 1] < 0) | np.isnan(t[:, 0]), np.inf, t[:, 0])
+    return tuple(t[int(np.argmin(keys))])
+
+
+def _call_local(dev, c, start, rank):
+    from mav_tube_trajectory_generation_amd._abi import check, lib
+    from mav_tube_trajectory_generation_amd.batch import _ptr, _stream
+    ct = torch.from_numpy(np.ascontiguousarray(c, dtype=np.float64)).to(dev)
+    out = torch.empty(3, dtype=torch.float64, device=dev)
+    check(lib().mtg_select_local(_ptr(ct) if len(c) else None, len(c), start, rank, _ptr(out),
+                                 _stream(dev)), "mtg_select_local")
+    return tuple(out.cpu().numpy())
+
+
+def _same(a, b):
+    return all((x == y) or (math.isinf(x) and math.isinf(y)) for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("case", ["random", "nan", "ties", "all_nan", "all_inf", "empty",
+                                  "single", "large"])
+def test_select_local_matches_rule(ctx, dev, case):
+    rng = np.random.default_rng(abs(hash(case)) % 1000)
+    n = {"empty": 0, "single": 1, "large": 65536}.get(case, 3000)
+    c = rng.uniform(1.0, 2.0, n)
+    if case == "nan":
+        c[rng.integers(0, n, 50)] = np.nan
+        c[17] = np.nan
+    if case == "ties":
+        c[:] = np.round(c, 1)
+        c[[5, 900, 2999]] = 0.5
+    if case == "all_nan":
+        c[:] = np.nan
+    if case == "all_inf":
+        c[:] = np.inf
+    if case == "large":
+        c[40000] = 0.1
+        c[60000] = 0.1
+    got = _call_local(dev, c, 12345, 3)
+    assert _same(got, _ref_local(c, 12345, 3)), (got, _ref_local(c, 12345, 3))
+
+
+def test_select_global_matches_rule(ctx, dev):
+    from mav_tube_trajectory_generation_amd._abi import check, lib
+    from mav_tube_trajectory_generation_amd.batch import _ptr, _stream
+    rng = np.random.default_rng(5)
+    cases = []
+    for world in (1, 2, 3, 8):
+        t = np.stack([rng.uniform(1, 2, world), np.arange(world) * 100.0, np.arange(world) * 1.0], 1)
+        cases.append(t)
+        t2 = t.copy(); t2[:, 0] = 1.5; cases.append(t2)                  # ties: first rank
+        t3 = t.copy(); t3[0, 1] = -1; t3[0, 0] = np.inf; cases.append(t3)  # empty shard
+        t4 = t.copy(); t4[:, 0] = np.nan; cases.append(t4)                # nothing finite
+        t5 = t.copy(); t5[-1, 0] = 0.0; t5[0, 0] = np.nan; cases.append(t5)
+    for t in cases:
+        tt = torch.from_numpy(np.ascontiguousarray(t.reshape(-1))).to(dev)
+        out = torch.empty(3, dtype=torch.float64, device=dev)
+        check(lib().mtg_select_global(_ptr(tt), t.shape[0], _ptr(out), _stream(dev)),
+              "mtg_select_global")
+        got = tuple(out.cpu().numpy())
+        ref = _ref_global(t)
+        assert all((x == y) or (np.isnan(x) and np.isnan(y)) or (math.isinf(x) and math.isinf(y))
+                   for x, y in zip(got, ref)), (t, got, ref)
+
+
+def test_select_best_device_one_rank_rccl(ctx, dev):
+    """The whole device selection step (local kernel, RCCL all-gather, global
+    kernel) on a one-rank process group, inside a captured HIP graph."""
+    import torch.distributed as dist
+
+    from mav_tube_trajectory_generation_amd.shard import select_best, select_best_device
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29650 + os.getpid() % 200))
+    created = not dist.is_initialized()
+    if created:
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        c = torch.rand(4096, dtype=torch.float64, device=dev) + 1.0
+        c[1234] = 0.25
+        c[17] = float("nan")
+        assert select_best(c, 4096) == (1234, 0.25, 0)
+        res = torch.empty(3, dtype=torch.float64, device=dev)
+        select_best_device(c, 4096)  # warm-up outside the capture
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            res.copy_(select_best_device(c, 4096))
+        c[1234] = 3.0
+        c[99] = 0.125
+        g.replay()
+        torch.cuda.synchronize(dev)
+        assert tuple(res.cpu().numpy()) == (0.125, 99.0, 0.0)
+    finally:
+        if created:
+            dist.destroy_process_group()
