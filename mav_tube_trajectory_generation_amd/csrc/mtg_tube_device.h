@@ -296,27 +296,44 @@ struct Tube {
   }
 
   // --------------------------------------------------------- control points
+  // One lane per control point (i, j): its beta row is formed once and used
+  // for the three dimensions (same products and summation order as one
+  // lane per (i, j, d)).
   __device__ void control_points(const double* xv, int out) {
-    for (int idx = lane; idx < S * N * 3; idx += kWave) {
-      const int i = idx / (N * 3), j = (idx / 3) % N, d = idx % 3;
+    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+      const int i = cpi / N, j = cpi % N;
       const int u = cp_vertex(i, j);
-      double c = 0.0;
+      double bt[M];
 #pragma unroll
-      for (int m = 0; m < M; ++m) c += beta(i, j, m) * xval(xv, u, d, m);
-      sm[out + idx] = c;
+      for (int m = 0; m < M; ++m) bt[m] = beta(i, j, m);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        double c = 0.0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) c += bt[m] * xval(xv, u, d, m);
+        sm[out + cpi * 3 + d] = c;
+      }
     }
   }
   // Same, for a step direction (fixed vertices contribute zero).
   __device__ void control_point_steps(const double* dxv, int out) {
-    for (int idx = lane; idx < S * N * 3; idx += kWave) {
-      const int i = idx / (N * 3), j = (idx / 3) % N, d = idx % 3;
+    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+      const int i = cpi / N, j = cpi % N;
       const int u = cp_vertex(i, j);
-      double c = 0.0;
-      if (u > 0 && u < S) {
+      const bool fr = u > 0 && u < S;
+      const double* xu = dxv + ((fr ? u : 1) - 1) * 3 * M;
+      double bt[M];
 #pragma unroll
-        for (int m = 0; m < M; ++m) c += beta(i, j, m) * dxv[((u - 1) * 3 + d) * M + m];
+      for (int m = 0; m < M; ++m) bt[m] = beta(i, j, m);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        double c = 0.0;
+        if (fr) {
+#pragma unroll
+          for (int m = 0; m < M; ++m) c += bt[m] * xu[d * M + m];
+        }
+        sm[out + cpi * 3 + d] = c;
       }
-      sm[out + idx] = c;
     }
   }
 
