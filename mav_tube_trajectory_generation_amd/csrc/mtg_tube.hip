@@ -12,7 +12,9 @@ namespace mtg {
 template <int N>
 __device__ inline Tube<N> make_tube(const TubeLayout* L, double* smem, int S, int r,
                                     const double* tab) {
-  return Tube<N>{S, r, S - 1, tube_ncon(N, S), L, smem, static_cast<int>(threadIdx.x), tab};
+  const int tid = static_cast<int>(threadIdx.x);
+  return Tube<N>{S,   r,         S - 1, tube_ncon(N, S), L, smem, tid & (kWave - 1), tab,
+                 tid, static_cast<int>(blockDim.x), tid / kWave};
 }
 
 // Constraint residuals g_k(x) (compute_sphere/tube/tube_end_constraints,
@@ -31,7 +33,7 @@ __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
   constexpr int M = N / 2;
   t.setup(tab, b, b / rep, positions, fixed_vals, times_cp, times, radii, bad);
   const int n = t.nv * 3 * M;
-  for (int idx = t.lane; idx < n; idx += kWave) {
+  for (int idx = t.tid; idx < n; idx += t.nthr) {
     // reference order d*(S-1)*M + (u-1)*M + m  ->  internal ((u-1)*3+d)*M + m
     const int d = idx / ((S - 1) * M), a = (idx / M) % (S - 1), m = idx % M;
     smem[L.x + (a * 3 + d) * M + m] = x[b * n + idx];
@@ -39,14 +41,24 @@ __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
   __syncthreads();
   t.control_points(smem + L.x, L.cp);
   __syncthreads();
-  for (int k = t.lane; k < t.nc; k += kWave) {
+  for (int k = t.tid; k < t.nc; k += t.nthr) {
     double w[3];
     resid[b * t.nc + k] = t.con_eval(k, L.cp, w);
   }
 }
 
+// Two waves per trajectory for N <= 10: both run the data-parallel phases,
+// wave 0 the block factorisation and solves; with 40 KB of LDS per
+// trajectory a CU holds 4 trajectories = 8 waves, two per SIMD (registers
+// capped at 256 per wave).  N = 12 keeps one wave (its 18 x 18 blocks need
+// more registers than two waves per SIMD leave).
 template <int N>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void tube_solve_kernel(
+constexpr int tube_threads() { return N <= 10 ? 2 * kWave : kWave; }
+
+template <int N>
+__global__ __launch_bounds__(tube_threads<N>())
+__attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
+void tube_solve_kernel(
     int S, int r, int rep, const double* __restrict__ tab, const double* __restrict__ positions,
     const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
     const double* __restrict__ times, const double* __restrict__ radii, double tol,
@@ -76,14 +88,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   // linear_impl:254-275) and computeCost (linear_impl:113-130).
   const int n = t.nv * 3 * M;
   if (x_out)
-    for (int idx = t.lane; idx < n; idx += kWave) {
+    for (int idx = t.tid; idx < n; idx += t.nthr) {
       const int d = idx / ((S - 1) * M), a = (idx / M) % (S - 1), m = idx % M;
       x_out[b * n + idx] = no_x ? NAN : smem[L.x + (a * 3 + d) * M + m];
     }
   const double* xv = smem + L.x;
   double acc = 0.0;
   const int per = S * 3 * N;
-  for (int i = t.lane; i < per; i += kWave) {
+  for (int i = t.tid; i < per; i += t.nthr) {
     const int s = i / (3 * N), d = (i / N) % 3, k = i % N;
     const int lk = k % M;
     double c = 0.0, h = 0.0;
@@ -97,8 +109,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
     coeffs[b * per + i] = no_x ? NAN : c;
     acc += h * t.xval(xv, s + k / M, d, lk);
   }
-  const double J = 0.5 * Tube<N>::wave_sum(acc);
-  if (t.lane == 0) {
+  const double J = 0.5 * t.block_sum(acc);
+  if (t.tid == 0) {
     if (cost) cost[b] = no_x ? NAN : J;
     if (iters) iters[b] = it;
     if (status)
@@ -147,7 +159,7 @@ hipError_t solve_n(const TubeArgs& a, double tol, int max_iter, double* x, doubl
   const size_t bytes = tube_lds_bytes(N, a.S);
   hipError_t e = prepare_lds(tube_solve_kernel<N>, bytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tube_solve_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(kWave),
+  hipLaunchKernelGGL(tube_solve_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(tube_threads<N>()),
                      bytes, st, a.S, a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp,
                      a.times, a.radii, tol, max_iter, a.skip, x, coeffs, cost, iters, status);
   return hipGetLastError();

@@ -50,6 +50,7 @@ struct TubeLayout {
   int Li;                 // nv*BS(BS+1)/2 L_a^-1 packed by rows, diagonal = 1/pivot
   int W;                  // BS*BS  W_a of the current block, row-major
   int Gc;                 // S*N*6  per control point: sum lam Hess + lam/s w w^T (sym)
+  int red;                // 4: cross-wave reductions
   int ndouble;
   size_t bytes() const { return sizeof(double) * ndouble; }
 };
@@ -86,6 +87,7 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   o += (nv * tri > S * (2 * N - 1) ? nv * tri : S * (2 * N - 1));
   l.W = o;    o += BS * BS;
   l.Gc = o;   o += S * N * 6;
+  l.red = o;  o += 4;
   l.ndouble = o;
   return l;
 }
@@ -99,8 +101,12 @@ struct Tube {
   int S, r, nv, nc;
   const TubeLayout* L;
   double* sm;
-  int lane;
-  const double* __restrict__ gtab;  // plan table: H(1) N*N, A(1)^-1 N*N, C^-1 M*M (global)
+  int lane;                          // lane in its wave
+  const double* __restrict__ gtab;
+  int tid, nthr, wv;                 // thread, threads (64 or 128), wave
+  // With two waves per trajectory the data-parallel phases use both; the
+  // block LDL^T and the block solves run on wave 0 (wave 1 meets the same
+  // barriers with nothing to do).  // plan table: H(1) N*N, A(1)^-1 N*N, C^-1 M*M (global)
 
   __device__ static int tri(int i, int k) { return i * (i + 1) / 2 + k; }  // k <= i
   __device__ double pd(int a, int j, int k) const {  // symmetric P block a
@@ -178,17 +184,17 @@ struct Tube {
                         const double* __restrict__ times,
                         const double* __restrict__ radii, int* bad) {
     const int NN = N * N;
-    for (int i = lane; i < S; i += kWave) sm[L->T + i] = times[b * S + i];
-    for (int i = lane; i < (S + 1) * 3; i += kWave) sm[L->pos + i] = positions[bin * (S + 1) * 3 + i];
-    for (int i = lane; i < 3 * N; i += kWave) {
+    for (int i = tid; i < S; i += nthr) sm[L->T + i] = times[b * S + i];
+    for (int i = tid; i < (S + 1) * 3; i += nthr) sm[L->pos + i] = positions[bin * (S + 1) * 3 + i];
+    for (int i = tid; i < 3 * N; i += nthr) {
       // fixed_vals[d][end*M + m] -> fixv[end][d][m]
       const int d = i / N, e = (i % N) / M, m = i % M;
       sm[L->fixv + (e * 3 + d) * M + m] = fixed_vals[bin * 3 * N + i];
     }
-    if (lane == 0) *bad = 0;
+    if (tid == 0) *bad = 0;
     __syncthreads();
     // B_ul^-1(T_cp) = C^-1 diag(T^l), snapped |x| < 1e-5 (qcqp_impl:299-307).
-    for (int idx = lane; idx < S * M * M; idx += kWave) {
+    for (int idx = tid; idx < S * M * M; idx += nthr) {
       const int i = idx / (M * M), k = (idx / M) % M, l = idx % M;
       const double tc = times_cp[bin * S + i];
       if (!(tc > 0.0)) atomicOr(bad, 1);
@@ -201,7 +207,7 @@ struct Tube {
     // Powers of the current times (H, A^-1, cost).
     if (!compute_powers()) atomicOr(bad, 1);
     // Tube geometry per segment (qcqp_impl:369-474).
-    for (int i = lane; i < S; i += kWave) {
+    for (int i = tid; i < S; i += nthr) {
       const double* p0 = sm + L->pos + i * 3;
       const double* p1 = p0 + 3;
       double n[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
@@ -247,7 +253,7 @@ struct Tube {
     // P = 2 R_pp (identical M x M blocks per dimension, symmetric half) and
     // q = 2 R_pf d_f.
     constexpr int MT = M * (M + 1) / 2;
-    for (int idx = lane; idx < nv * MT; idx += kWave) {
+    for (int idx = tid; idx < nv * MT; idx += nthr) {
       const int a = idx / MT, t2 = idx % MT;
       int j = 0;
       while (tri(j + 1, 0) <= t2) ++j;
@@ -255,11 +261,11 @@ struct Tube {
       const int u = a + 1;  // vertex
       sm[L->Pd + idx] = 2.0 * (Hb(u - 1, 1, 1, j, k) + Hb(u, 0, 0, j, k));
     }
-    for (int idx = lane; idx < (nv - 1) * M * M; idx += kWave) {
+    for (int idx = tid; idx < (nv - 1) * M * M; idx += nthr) {
       const int a = idx / (M * M), j = (idx / M) % M, k = idx % M;
       sm[L->Po + idx] = 2.0 * Hb(a + 1, 0, 1, j, k);  // vertex a+1 -> a+2
     }
-    for (int idx = lane; idx < nv * BS; idx += kWave) {
+    for (int idx = tid; idx < nv * BS; idx += nthr) {
       const int a = idx / BS, d = (idx / M) % 3, j = idx % M;
       const int u = a + 1;
       double v = 0.0;
@@ -281,7 +287,7 @@ struct Tube {
   // outputs).  Returns false if a time is not a valid segment time.
   __device__ bool compute_powers() {
     bool ok = true;
-    for (int idx = lane; idx < S * PWN; idx += kWave) {
+    for (int idx = tid; idx < S * PWN; idx += nthr) {
       const int s = idx / PWN;
       const int e = idx % PWN - (N - 1);
       const double t = sm[L->T + s];
@@ -300,7 +306,7 @@ struct Tube {
   // for the three dimensions (same products and summation order as one
   // lane per (i, j, d)).
   __device__ void control_points(const double* xv, int out) {
-    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+    for (int cpi = tid; cpi < S * N; cpi += nthr) {
       const int i = cpi / N, j = cpi % N;
       const int u = cp_vertex(i, j);
       double bt[M];
@@ -317,7 +323,7 @@ struct Tube {
   }
   // Same, for a step direction (fixed vertices contribute zero).
   __device__ void control_point_steps(const double* dxv, int out) {
-    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+    for (int cpi = tid; cpi < S * N; cpi += nthr) {
       const int i = cpi / N, j = cpi % N;
       const int u = cp_vertex(i, j);
       const bool fr = u > 0 && u < S;
@@ -420,7 +426,7 @@ struct Tube {
   // columns are built in registers by factor().
   __device__ void assemble_g() {
     double* Gcp = sm + L->Gc;
-    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+    for (int cpi = tid; cpi < S * N; cpi += nthr) {
       const int i = cpi / N, j = cpi % N;
       double G[9];
 #pragma unroll
@@ -537,6 +543,8 @@ struct Tube {
       // Roles enter as exact 0/1 factors (VGPR values: no lane masks kept
       // live); loads are unconditional with clamped indices.
       const double r0 = is_zero(role), r1 = is_zero(role - 1), r2 = is_zero(role - 2);
+      double dpiv = 1.0;
+      if (wv == 0) {  // ---- wave 0: assemble and eliminate block a
       {
         const double* Po = sm + L->Po + (a < nv - 1 ? a : 0) * M * M;
         double ind[3];
@@ -618,7 +626,6 @@ struct Tube {
       // Forward elimination (below the pivot) on all columns at once; the
       // pivot column is broadcast with v_readlane.
       MTG_TACC(222, tf);
-      double dpiv = 1.0;
 #pragma unroll
       for (int j = 0; j < BS; ++j) {
         const double piv = bcast(col[j], j);
@@ -635,13 +642,14 @@ struct Tube {
       }
       bad |= __ballot(lane < BS && !(dpiv > 0.0)) != 0;
       MTG_TACC(223, tf);
+      }  // ---- wave 0
       // S_a lanes store 1 / pivot on the diagonal of the packed L_a^-1, the
       // identity lanes its strictly lower columns, the C_a lanes W_a
       // (replacing W_{a-1}, which every lane has read by the barrier).
       // Offsets are selected per lane with integer masks (no branches),
       // unused stores go to a per-lane dummy slot.
       __syncthreads();
-      {
+      if (wv == 0) {
         const int li = L->Li + a * kTri;
         const int s0 = -izero(role), s1 = -izero(role - 1), s2 = -izero(role - 2);
         sm[((li + tri(cc, cc)) & s0) | (dummy & ~s0)] = rcp64(dpiv > 0.0 ? dpiv : 1.0);
@@ -656,7 +664,7 @@ struct Tube {
       __syncthreads();
       MTG_TACC(224, tf);
     }
-    if (bad && lane == 0) *fail = 1;
+    if (bad && tid == 0) *fail = 1;
   }
 
   // Solve K out = rhs with the block factors (rhs overwritten by y).
@@ -695,7 +703,7 @@ struct Tube {
       return fma(Lb[tri(kx, i)], static_cast<double>(k > i && k0 < BS), is_zero(k0 - i));
     };
     double u = 0.0;  // D_{a-1}^-1 y_{a-1}, entry i
-    for (int a = 0; a < nv; ++a) {
+    for (int a = 0; a < (wv == 0 ? nv : 0); ++a) {  // wave 0 only
       const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
       if (a > 0) {
@@ -718,7 +726,7 @@ struct Tube {
     }
     __syncthreads();
     double xn = 0.0;  // x_{a+1}, entry i
-    for (int a = nv - 1; a >= 0; --a) {
+    for (int a = (wv == 0 ? nv - 1 : -1); a >= 0; --a) {  // wave 0 only
       const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
       if (a < nv - 1) {
@@ -758,6 +766,20 @@ struct Tube {
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
     return x;
   }
+  // Workgroup reductions (one or two waves); every thread calls them.
+  template <int kOp>  // 0 max, 1 min, 2 sum
+  __device__ double block_red(double x) {
+    x = kOp == 0 ? wave_max(x) : kOp == 1 ? wave_min(x) : wave_sum(x);
+    if (nthr == kWave) return x;
+    if (lane == 0) sm[L->red + wv] = x;
+    __syncthreads();
+    const double a = sm[L->red], c = sm[L->red + 1];
+    __syncthreads();
+    return kOp == 0 ? fmax(a, c) : kOp == 1 ? fmin(a, c) : a + c;
+  }
+  __device__ double block_max(double x) { return block_red<0>(x); }
+  __device__ double block_min(double x) { return block_red<1>(x); }
+  __device__ double block_sum(double x) { return block_red<2>(x); }
 
   // Complementarity target: affine rc = s lam; corrector
   // rc = s lam + ds_aff dl_aff - sigma mu (ds, dl still hold the affine step).
@@ -773,7 +795,7 @@ struct Tube {
   template <bool kCorr>
   __device__ void direction(double smu) {
     // Per control point: Psi[d] = sum_k w_k[d] (lam_k rp_k - rc_k) / s_k.
-    for (int cpi = lane; cpi < S * N; cpi += kWave) {
+    for (int cpi = tid; cpi < S * N; cpi += nthr) {
       const int i = cpi / N, j = cpi % N;
       double P3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
@@ -790,7 +812,7 @@ struct Tube {
       for (int d = 0; d < 3; ++d) sm[L->acc + cpi * 3 + d] = P3[d];
     }
     __syncthreads();
-    for (int idx = lane; idx < nv * BS; idx += kWave) {
+    for (int idx = tid; idx < nv * BS; idx += nthr) {
       const int a = idx / BS, d = (idx / M) % 3, m = idx % M;
       sm[L->rhs + idx] = -sm[L->rd + idx] - gather_cp(L->acc, a, d, m);
     }
@@ -801,7 +823,7 @@ struct Tube {
     MTG_TACC(210, tl);
     control_point_steps(sm + L->dx, L->acc);
     __syncthreads();
-    for (int k = lane; k < nc; k += kWave) {
+    for (int k = tid; k < nc; k += nthr) {
       double w[3];
       const double g = con_eval(k, L->cp, w);
       int i, j, type;
@@ -818,14 +840,14 @@ struct Tube {
     __syncthreads();
   }
 
-  __device__ double max_step() const {
+  __device__ double max_step() {
     double alpha = 1.0;
-    for (int k = lane; k < nc; k += kWave) {
+    for (int k = tid; k < nc; k += nthr) {
       const double ds = sm[L->ds + k], dl = sm[L->dl + k];
       if (ds < 0) alpha = fmin(alpha, -sm[L->s + k] / ds);
       if (dl < 0) alpha = fmin(alpha, -sm[L->lam + k] / dl);
     }
-    return wave_min(alpha);
+    return block_min(alpha);
   }
 
   // Full IPM (oracle TubeProblem::solveIPM).  Returns iterations; *status
@@ -837,30 +859,30 @@ struct Tube {
   // 1e5 * tol instead, report it not converged (status 1).
   __device__ int ipm(double tol, int max_iter, int* status, int* bad) {
     int* fail = bad + 1;
-    if (lane == 0) *fail = 0;
+    if (tid == 0) *fail = 0;
     __syncthreads();
     // Unconstrained start: P x = -q.
     factor(fail, false);
     __syncthreads();
     if (*fail) {
-      if (lane == 0) *bad |= 2;
+      if (tid == 0) *bad |= 2;
       *status = 2;
       return 0;
     }
-    for (int idx = lane; idx < nv * BS; idx += kWave) sm[L->rhs + idx] = -sm[L->q + idx];
+    for (int idx = tid; idx < nv * BS; idx += nthr) sm[L->rhs + idx] = -sm[L->q + idx];
     __syncthreads();
     solve(L->rhs, L->x);
     control_points(sm + L->x, L->cp);
     __syncthreads();
-    for (int k = lane; k < nc; k += kWave) {
+    for (int k = tid; k < nc; k += nthr) {
       double w[3];
       const double g = con_eval(k, L->cp, w);
       sm[L->s + k] = fmax(-g, 1.0);
       sm[L->lam + k] = 1.0;
     }
     double qn = 0.0;
-    for (int idx = lane; idx < nv * BS; idx += kWave) qn = fmax(qn, fabs(sm[L->q + idx]));
-    qn = wave_max(qn);
+    for (int idx = tid; idx < nv * BS; idx += nthr) qn = fmax(qn, fabs(sm[L->q + idx]));
+    qn = block_max(qn);
     __syncthreads();
     int it = 0;
     *status = 1;
@@ -871,17 +893,17 @@ struct Tube {
       control_points(sm + L->x, L->cp);
       __syncthreads();
       double rpn = 0.0, mu = 0.0;
-      for (int k = lane; k < nc; k += kWave) {
+      for (int k = tid; k < nc; k += nthr) {
         double w[3];
         const double g = con_eval(k, L->cp, w);
         const double s = sm[L->s + k];
         rpn = fmax(rpn, fabs(g + s));
         mu += s * sm[L->lam + k];
       }
-      rpn = wave_max(rpn);
-      mu = wave_sum(mu) / nc;
+      rpn = block_max(rpn);
+      mu = block_sum(mu) / nc;
       // Omega[cp][d] = sum_k lam_k w_k[d]  (dual residual weights).
-      for (int cpi = lane; cpi < S * N; cpi += kWave) {
+      for (int cpi = tid; cpi < S * N; cpi += nthr) {
         const int i = cpi / N, j = cpi % N;
         double O3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
@@ -897,13 +919,13 @@ struct Tube {
       }
       __syncthreads();
       double rdn = 0.0;
-      for (int idx = lane; idx < nv * BS; idx += kWave) {
+      for (int idx = tid; idx < nv * BS; idx += nthr) {
         const int a = idx / BS, d = (idx / M) % 3, m = idx % M;
         const double v = Pxq(sm + L->x, idx) + gather_cp(L->acc, a, d, m);
         sm[L->rd + idx] = v;
         rdn = fmax(rdn, fabs(v));
       }
-      rdn = wave_max(rdn);
+      rdn = block_max(rdn);
       __syncthreads();
       if (rdn <= tol * (1.0 + qn) && rpn <= tol && mu <= tol) {
         *status = 0;
@@ -917,7 +939,7 @@ struct Tube {
       MTG_TACC(200, tl);
       assemble_g();
       MTG_TACC(201, tl);
-      if (lane == 0) *fail = 0;
+      if (tid == 0) *fail = 0;
       __syncthreads();
       factor(fail, true);
       __syncthreads();
@@ -931,9 +953,9 @@ struct Tube {
       MTG_TACC(203, tl);
       const double a_aff = max_step();
       double mua = 0.0;
-      for (int k = lane; k < nc; k += kWave)
+      for (int k = tid; k < nc; k += nthr)
         mua += (sm[L->s + k] + a_aff * sm[L->ds + k]) * (sm[L->lam + k] + a_aff * sm[L->dl + k]);
-      mua = wave_sum(mua) / nc;
+      mua = block_sum(mua) / nc;
       const double ratio = mua / mu;
       const double sigma = ratio * ratio * ratio;
       __syncthreads();
@@ -943,14 +965,14 @@ struct Tube {
       MTG_TACC(205, tl);
       const double alpha = fmin(1.0, 0.99 * max_step());
       double dxn = 0.0;
-      for (int idx = lane; idx < nv * BS; idx += kWave) dxn = fmax(dxn, fabs(sm[L->dx + idx]));
-      dxn = wave_max(dxn);
+      for (int idx = tid; idx < nv * BS; idx += nthr) dxn = fmax(dxn, fabs(sm[L->dx + idx]));
+      dxn = block_max(dxn);
       if (!(alpha > 0.0) || !(dxn < 1e300) || !(sigma < 1e300)) {
         *status = brk;
         break;
       }
-      for (int idx = lane; idx < nv * BS; idx += kWave) sm[L->x + idx] += alpha * sm[L->dx + idx];
-      for (int k = lane; k < nc; k += kWave) {
+      for (int idx = tid; idx < nv * BS; idx += nthr) sm[L->x + idx] += alpha * sm[L->dx + idx];
+      for (int k = tid; k < nc; k += nthr) {
         sm[L->s + k] += alpha * sm[L->ds + k];
         sm[L->lam + k] += alpha * sm[L->dl + k];
       }
