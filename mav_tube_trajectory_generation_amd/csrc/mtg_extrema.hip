@@ -75,8 +75,11 @@ __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
   if (active) {
     const double T = traj_s[traj_per_block * S * D * N + bl * S + s];
     const double* c = traj_s + (bl * S + s) * D * N;
+    // Pruning bound: |p^(K)|^2 at the part's right end (a wave may hold
+    // several trajectories, so the bound stays per lane).
+    const double lb = kMin ? 0.0 : ext_mag2<N, K>(c, D, ldexp(T * (part + 1), -log2parts));
     ext_segment_search<N, K, kMin>(c, D, T, part, parts, log2parts, best_v, best_t, min_v,
-                                   min_t);
+                                   min_t, lb);
   }
   val_s[tid] = best_v;
   time_s[tid] = best_t;
@@ -229,30 +232,41 @@ __global__ __launch_bounds__(kSoftBlockMax) void soft_cost_kernel(int D, int S, 
   for (int i = tid; i < S; i += blockDim.x) c_s[per + i] = times[b * S + i];
   __syncthreads();
   const int cidx = tid / group, r = tid - cidx * group;
-  const bool active = cidx < spec.n && r < S * parts;
+  const bool group_on = cidx < spec.n;  // wave-uniform: groups are whole waves
+  const bool active = group_on && r < S * parts;
   double best_v = -1.0, best_t = 0.0, mv = 0.0, mt = 0.0;
-  if (active) {
-    const int s = r >> log2parts, part = r & (parts - 1);
+  if (group_on) {
+    const int s = active ? r >> log2parts : 0, part = r & (parts - 1);
     const double* c = c_s + s * D * N;
     const double T = c_s[per + s];
     int K = 0;
 #pragma unroll
     for (int q = 0; q < kMaxSoftConstraints; ++q)  // compile-time indices
       if (q == cidx) K = spec.derivative[q];
-    switch (K) {  // wave-uniform: groups are whole waves
-      case 0: ext_segment_search<N, 0>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt); break;
-      case 1: ext_segment_search<N, 1>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt); break;
-      case 2: ext_segment_search<N, 2>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt); break;
+    // Every lane of a wave searches the same trajectory and derivative, so
+    // the wave's largest |p^(K)|^2 at the parts' right ends bounds the
+    // maximum from below for the pruning (idle lanes give 0; all lanes of
+    // the wave take part in the exchange).
+#define MTG_SOFT_SEARCH(k)                                                                     \
+  {                                                                                            \
+    double lb = active ? ext_mag2<N, k>(c, D, ldexp(T * (part + 1), -log2parts)) : 0.0;       \
+    for (int off = 32; off > 0; off >>= 1) lb = fmax(lb, __shfl_xor(lb, off, 64));             \
+    if (active)                                                                                \
+      ext_segment_search<N, k>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt, lb);   \
+  }
+    switch (K) {
+      case 0: MTG_SOFT_SEARCH(0) break;
+      case 1: MTG_SOFT_SEARCH(1) break;
+      case 2: MTG_SOFT_SEARCH(2) break;
       case 3:
-        if constexpr (N >= 5)
-          ext_segment_search<N, 3>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt);
+        if constexpr (N >= 5) MTG_SOFT_SEARCH(3)
         break;
       case 4:
-        if constexpr (N >= 6)
-          ext_segment_search<N, 4>(c, D, T, part, parts, log2parts, best_v, best_t, mv, mt);
+        if constexpr (N >= 6) MTG_SOFT_SEARCH(4)
         break;
       default: break;
     }
+#undef MTG_SOFT_SEARCH
   }
   val_s[tid] = best_v;
   __syncthreads();

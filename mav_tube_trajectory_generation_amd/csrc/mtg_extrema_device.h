@@ -52,11 +52,13 @@ __device__ inline double ext_mag2(const double* c, int D, double t) {
 // (|p^(K)|^2) and best_t with strict '>' in candidate order; with kMin also
 // min_v / min_t with strict '<' (the minimum of Trajectory::
 // computeMinMaxMagnitude, trajectory.cpp:184-220; caller starts min_v at
-// +inf).
+// +inf).  lb: a value |p^(K)|^2 attains somewhere on the trajectory (0 if
+// none is known); without kMin, nodes whose upper bound lies below it are
+// pruned, which never drops the trajectory's maximum.
 template <int N, int K, bool kMin = false>
 __device__ inline void ext_segment_search(const double* c, int D, double T, int part, int parts,
                                           int log2parts, double& best_v, double& best_t,
-                                          double& min_v, double& min_t) {
+                                          double& min_v, double& min_t, double lb = 0.0) {
   auto take = [&](double v, double t) {
     if (v > best_v) {
       best_v = v;
@@ -108,8 +110,28 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
       tp *= T;
     }
   }
-  // Bernstein coefficients on [0, 1]: beta_i = sum_{j<=i} C(i,j)/C(M,j) q_j,
-  // normalised to max |beta| = 1.
+  // The lane's part [u0, u0 + w0] of [0, 1] in the local variable v in
+  // [0, 1]: q(u0 + w0 v) by a Taylor shift (synthetic division) and an exact
+  // power-of-two scaling.  The part's Bernstein coefficients then come from
+  // one conversion instead of two de Casteljau splits of the segment's.
+  const double w0 = ldexp(1.0, -log2parts);
+  const double u0 = part * w0;
+  if (part > 0) {
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = M - 1; j >= i; --j) q[j] = fma(u0, q[j + 1], q[j]);
+  }
+  if (log2parts > 0) {
+    double wp = w0;
+#pragma unroll
+    for (int j = 1; j <= M; ++j) {
+      q[j] *= wp;
+      wp *= w0;
+    }
+  }
+  // Bernstein coefficients on the part: beta_i = sum_{j<=i} C(i,j)/C(M,j)
+  // q_j, normalised to max |beta| = 1.
   double beta[M + 1];
   double mx = 0.0;
 #pragma unroll
@@ -127,8 +149,13 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
       beta[i] *= inv;
       q[i] *= inv;
     }
-    // Depth-first walk of the dyadic tree under node (log2parts, part).
-    int level = log2parts, idx = part;
+    // Depth-first walk of the dyadic tree under the part (local level 0;
+    // global level = level + log2parts).  Bracket tolerances are the global
+    // 1e-12 in local units.
+    const double tol = ldexp(1.0e-12, log2parts);
+    const double hw = T * w0 * mx;  // d t / d v times the normalisation
+    const int max_level = kExtMaxLevel - log2parts;
+    int level = 0, idx = 0;
     for (;;) {
       const double w = ldexp(1.0, -level);
       const double a = idx * w;
@@ -151,6 +178,21 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
 #pragma unroll
           for (int i = 0; i <= M - r; ++i) bb[i] = fma(u, bb[i + 1] - bb[i], bb[i]);
       }
+      // Prune (maximum only): g = |p^(K)|^2 has g' = 2 f, so on the node
+      // g <= g(t_a) + 2 (t_e - t_a) max(0, max_i beta_i) mx (convex hull of
+      // the Bernstein coefficients).  A node whose bound is below a value g
+      // attains on the trajectory cannot hold the maximum; the 1e-12 margin
+      // keeps rounding from pruning the node that does.
+      bool pruned = false;
+      if constexpr (!kMin) {
+        double bmax = 0.0;
+#pragma unroll
+        for (int i = 0; i <= M; ++i) bmax = fmax(bmax, bb[i]);
+        lb = fmax(lb, best_v);
+        const double ta = fma(w0, a, u0) * T;
+        const double ub = fma(2.0 * (e - a) * hw, bmax, ext_mag2<N, K>(c, D, ta));
+        pruned = ub < lb * (1.0 - 1.0e-12);
+      }
       // Sign variations (zeros skipped), first / last nonzero signs.
       int var = 0;
       double first = 0.0, last = 0.0;
@@ -162,9 +204,12 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
         first = (first == 0.0) ? x : first;
         last = nz ? x : last;
       }
+      if (pruned) var = 0;
       double root = -1.0;
-      if (bb[0] == 0.0 && a > 0.0)  // root exactly at the node's left end
-        take(ext_mag2<N, K>(c, D, a * T), a * T);
+      if (!pruned && bb[0] == 0.0 && (a > 0.0 || part > 0)) {  // root exactly at the node's left end
+        const double ua = fma(w0, a, u0);
+        take(ext_mag2<N, K>(c, D, ua * T), ua * T);
+      }
       bool descend = false;
       if (var == 1) {
         // Laguerre's method safeguarded by the bracket (bisection when a
@@ -186,33 +231,37 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
           }
           if (fabs(fx) <= 32.0 * 2.220446049250313e-16 * ab) break;
           if ((fx > 0.0) == pos_lo) lo = x; else hi = x;
-          const double G = d1 / fx;
-          const double H = G * G - 2.0 * d2 / fx;
+          const double rf = 1.0 / fx;
+          const double G = d1 * rf;
+          const double H = G * G - 2.0 * d2 * rf;
           const double rad = fmax((M - 1) * (M * H - G * G), 0.0);
           const double sq = sqrt(rad);
           const double den = G >= 0.0 ? G + sq : G - sq;
           double xn = den != 0.0 ? x - M / den : 0.5 * (lo + hi);
           if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
-          const bool done = fabs(xn - x) <= 1.0e-12 || hi - lo <= 1.0e-12;
+          const bool done = fabs(xn - x) <= tol || hi - lo <= tol;
           x = xn;
           if (done) break;
         }
         root = x;
       } else if (var > 1) {
-        if (level >= kExtMaxLevel) root = 0.5 * (a + e);  // unresolved cluster
+        if (level >= max_level) root = 0.5 * (a + e);  // unresolved cluster
         else descend = true;
       }
-      if (root >= 0.0) take(ext_mag2<N, K>(c, D, root * T), root * T);
+      if (root >= 0.0) {
+        const double ur = fma(w0, root, u0);
+        take(ext_mag2<N, K>(c, D, ur * T), ur * T);
+      }
       if (descend) {
         ++level;
         idx *= 2;
         continue;
       }
-      while (level > log2parts && (idx & 1)) {
+      while (level > 0 && (idx & 1)) {
         idx >>= 1;
         --level;
       }
-      if (level == log2parts) break;
+      if (level == 0) break;
       ++idx;
     }
   }
@@ -229,12 +278,20 @@ __device__ inline double ext_trajectory_max_wave(const double* coeffs, const dou
     parts >>= 1;
     --log2parts;
   }
+  // Lower bound for the pruning: |p^(K)|^2 at every part's right end.
+  double lb = 0.0;
+  for (int item = lane; item < S * parts; item += 64) {
+    const int s = item >> log2parts, part = item & (parts - 1);
+    lb = fmax(lb, ext_mag2<N, K>(coeffs + s * D * N, D, ldexp(times[s] * (part + 1), -log2parts)));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lb = fmax(lb, __shfl_xor(lb, off, 64));
   double best = 0.0;
   for (int item = lane; item < S * parts; item += 64) {
     const int s = item >> log2parts, part = item & (parts - 1);
     double v = -1.0, t = 0.0, mv = 0.0, mt = 0.0;
     ext_segment_search<N, K>(coeffs + s * D * N, D, times[s], part, parts, log2parts, v, t, mv,
-                             mt);
+                             mt, lb);
     best = fmax(best, v);
   }
 #pragma unroll

@@ -40,6 +40,9 @@ __device__ double std_objective(StdSv<N, R, D>& sv, const double* __restrict__ t
     *bad = true;
     return NAN;
   }
+  // kSoft: the H(1) rows are reloaded per evaluation (L2 hits), so they are
+  // not live across the extremum searches.
+  if constexpr (kSoft) sv.load_first_rows(tab);
   sv.assemble(tab);
   __syncthreads();
   *not_spd = sv.solve() || *not_spd;
@@ -99,7 +102,7 @@ size_t time_std_lds_bytes(int N, int S, int D, bool soft) {
 }
 
 template <int N, int R, int D, bool kSoft>
-__global__ __launch_bounds__(kWave) void time_cost_std_kernel(
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void time_cost_std_kernel(
     int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     const double* __restrict__ times, mtg_time_params p, double* __restrict__ cost,
     double* __restrict__ grad, int32_t* __restrict__ status) {
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(kWave) void time_cost_std_kernel(
 // evaluations are not counted).  A state machine with one objective call
 // site, as time_optimize_kernel.
 template <int N, int R, int D, bool kSoft>
-__global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void time_optimize_std_kernel(
     int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     double* __restrict__ times_io, mtg_time_params p, int max_evals,
     double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
