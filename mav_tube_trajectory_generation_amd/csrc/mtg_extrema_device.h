@@ -56,7 +56,7 @@ __device__ inline double ext_mag2(const double* c, int D, double t) {
 // none is known); without kMin, nodes whose upper bound lies below it are
 // pruned, which never drops the trajectory's maximum.
 template <int N, int K, bool kMin = false>
-__device__ inline void ext_segment_search(const double* c, int D, double T, int part, int parts,
+__device__ __attribute__((always_inline)) inline void ext_segment_search(const double* c, int D, double T, int part, int parts,
                                           int log2parts, double& best_v, double& best_t,
                                           double& min_v, double& min_t, double lb = 0.0) {
   auto take = [&](double v, double t) {
@@ -204,7 +204,13 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
         first = (first == 0.0) ? x : first;
         last = nz ? x : last;
       }
-      if (pruned) var = 0;
+      // One sign change from - to + inside the node is a strict local minimum
+      // of g, below g at the node's ends, so never the maximum: maximum-only
+      // searches skip its refinement (a root exactly at the left end is
+      // still taken below).
+      bool local_min = false;
+      if constexpr (!kMin) local_min = var == 1 && first < 0.0;
+      if (pruned || local_min) var = 0;
       double root = -1.0;
       if (!pruned && bb[0] == 0.0 && (a > 0.0 || part > 0)) {  // root exactly at the node's left end
         const double ua = fma(w0, a, u0);
@@ -271,7 +277,7 @@ __device__ inline void ext_segment_search(const double* c, int D, double T, int 
 // coeffs S x D x N and times S in LDS; work items (segment, part) strided
 // over the lanes.  Returns the maximum on every lane.
 template <int N, int K>
-__device__ inline double ext_trajectory_max_wave(const double* coeffs, const double* times,
+__device__ __attribute__((always_inline)) inline double ext_trajectory_max_wave(const double* coeffs, const double* times,
                                                  int S, int D, int lane) {
   int parts = 8, log2parts = 3;
   while (parts > 1 && S * parts > 64) {
@@ -301,7 +307,7 @@ __device__ inline double ext_trajectory_max_wave(const double* coeffs, const dou
 
 // Runtime-derivative dispatch (POSITION..SNAP, nonlinear_impl:2697-2724).
 template <int N>
-__device__ inline double ext_trajectory_max_wave_k(int K, const double* coeffs,
+__device__ __attribute__((always_inline)) inline double ext_trajectory_max_wave_k(int K, const double* coeffs,
                                                    const double* times, int S, int D, int lane) {
   switch (K) {
     case 0: return ext_trajectory_max_wave<N, 0>(coeffs, times, S, D, lane);

@@ -29,7 +29,7 @@ using StdSv = stdp::Solver<N, R, D>;
 // - tolerance)) (evaluateMaximumMagnitudeConstraint, :2687-2733) instead of
 // a cost term.
 template <int N, int R, int D, bool kSoft>
-__device__ double std_objective(StdSv<N, R, D>& sv, const double* __restrict__ tab,
+__device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& sv, const double* __restrict__ tab,
                                 const double* T, const mtg_time_params& p, double* cbuf,
                                 bool* bad, bool* not_spd, double* viol) {
   *viol = 0.0;
@@ -102,7 +102,7 @@ size_t time_std_lds_bytes(int N, int S, int D, bool soft) {
 }
 
 template <int N, int R, int D, bool kSoft>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void time_cost_std_kernel(
+__global__ __launch_bounds__(kWave) void time_cost_std_kernel(
     int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     const double* __restrict__ times, mtg_time_params p, double* __restrict__ cost,
     double* __restrict__ grad, int32_t* __restrict__ status) {
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) v
 // evaluations are not counted).  A state machine with one objective call
 // site, as time_optimize_kernel.
 template <int N, int R, int D, bool kSoft>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void time_optimize_std_kernel(
+__global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
     int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     double* __restrict__ times_io, mtg_time_params p, int max_evals,
     double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
