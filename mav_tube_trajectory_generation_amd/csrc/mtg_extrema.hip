@@ -58,7 +58,8 @@ __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
   const int s = rem >> log2parts;
   const int part = rem & (parts - 1);
   const int64_t b = static_cast<int64_t>(blockIdx.x) * traj_per_block + bl;
-  const bool active = bl < traj_per_block && b < B;
+  const bool skipped = b < B && soft.skip && soft.skip[b / soft.skip_rep];
+  const bool active = bl < traj_per_block && b < B && !skipped;
   {
     const int64_t b0 = static_cast<int64_t>(blockIdx.x) * traj_per_block;
     const int nt = static_cast<int>(min(static_cast<int64_t>(traj_per_block), B - b0));
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(kExtBlock) void max_magnitude_kernel(
   // Reduction in candidate order: segment ascending, part ascending; strict
   // '>' keeps the first maximum (Extremum::operator<, extremum.h:35-36;
   // linear_impl:474).  Extremum() starts at {0, 0, 0}.
-  if (active && rem == 0) {
+  if (active && rem == 0) {  // skipped trajectories keep their outputs
     double v = 0.0, t = 0.0;
     int seg = 0;
     for (int i = 0; i < lanes_per_traj; ++i) {
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(kSoftBlockMax) void soft_cost_kernel(int D, int S, 
   double* val_s = sm_soft + per + S;  // blockDim.x
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
+  if (spec.skip && spec.skip[b / spec.skip_rep]) return;  // workgroup-uniform
   for (int i = tid; i < per; i += blockDim.x) c_s[i] = coeffs[b * per + i];
   for (int i = tid; i < S; i += blockDim.x) c_s[per + i] = times[b * S + i];
   __syncthreads();

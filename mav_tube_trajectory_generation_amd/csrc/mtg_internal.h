@@ -154,6 +154,11 @@ struct SoftCostArgs {
   double* cost;  // null: plain maximum search
   SoftLimits lim;
   double weight, maximum_cost;
+  // Optional per-trajectory skip flags, indexed by trajectory / skip_rep: a
+  // set flag makes the trajectory's lanes skip the search and leave its
+  // outputs untouched (finished trajectories of the device optimisers).
+  const int32_t* skip = nullptr;
+  int skip_rep = 1;
 };
 // Collision cost over a dense occupancy grid (mtg_collision.hip).
 size_t collision_lds_bytes(int N, int S);
@@ -177,6 +182,8 @@ struct SoftSpec {
   int derivative[kMaxSoftConstraints];
   double limit[kMaxSoftConstraints];
   double weight, maximum_cost;
+  const int32_t* skip = nullptr;  // as SoftCostArgs::skip
+  int skip_rep = 1;
 };
 hipError_t launch_soft_cost(int N, int D, int S, int64_t B, const double* coeffs,
                             const double* times, const SoftSpec& spec, double* maxima,

@@ -302,6 +302,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   double* Tcur = smem + lay.aux;   // accepted times
   double* T0 = Tcur + S;           // initial times (bounds)
   double* g = T0 + S;              // gradient at Tcur
+  double* gv = g + S;              // gradient of the violation (hard constraints)
   t.load_inputs(pl.tab, pl.slots, pl.fixed_map, times_io + b * S, fixed_vals + b * D * nf, nf);
   for (int i = t.lane; i < S; i += kWave) {
     const double v = times_io[b * S + i];
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
   int phase = kBase, gi = 0, evals = 0, nsolve = 0;
-  double f = 0.0, fv = 0.0, Jlo = 0.0;
+  double f = 0.0, fv = 0.0, Jlo = 0.0, vlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   int fl = 0;
   while (phase != kDone) {
@@ -328,9 +329,13 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
       gi = 0;
     } else if (phase == kGrad) {
       if (gi & 1) {
-        if (t.lane == 0) g[gi >> 1] = (J - Jlo) / (2.0 * p.increment);
+        if (t.lane == 0) {
+          g[gi >> 1] = (J - Jlo) / (2.0 * p.increment);
+          gv[gi >> 1] = (viol - vlo) / (2.0 * p.increment);
+        }
       } else {
         Jlo = J;
+        vlo = viol;
       }
       if (++gi == 2 * S) phase = kTrial;
     } else {  // trial point
@@ -355,13 +360,15 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
     } else if (phase == kTrial) {
       if (!(evals < max_evals && alpha > 1e-9)) break;
       // Scaled direction -g_n T0_n, normalised so the largest relative move
-      // is alpha.
+      // is alpha; from an infeasible incumbent (hard constraints) the
+      // direction descends the violation instead.
+      const double* dir = fv > 0.0 ? gv : g;
       double gmax = 0.0;
-      for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(g[i] * T0[i]));
+      for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(dir[i] * T0[i]));
       if (!(gmax > 0.0)) break;
       int moved = 0;
       for (int i = 0; i < S; ++i) {
-        const double step = alpha * T0[i] * (g[i] * T0[i]) / gmax;
+        const double step = alpha * T0[i] * (dir[i] * T0[i]) / gmax;
         double tn = Tcur[i] - step;
         tn = fmin(fmax(tn, kLower), 2.0 * T0[i]);
         if (tn != Tcur[i]) moved = 1;
@@ -481,7 +488,9 @@ int linear_kernel_for_batch(const PlanDev& pl, int64_t B) {
   if (pl.kernel != MTG_KERNEL_AUTO) return pl.kernel;
   if (!pl.std_pattern) return MTG_KERNEL_GENERIC;
   if (has_linear_lane(pl) && B >= kLaneMinBatch) return MTG_KERNEL_LANE;
-  return MTG_KERNEL_STANDARD;
+  // The same test launch_linear_solve applies (std_pattern already implies
+  // S <= kMaxStdS), so the reported kernel is the one that runs.
+  return use_std_kernel(pl) ? MTG_KERNEL_STANDARD : MTG_KERNEL_GENERIC;
 }
 
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,

@@ -182,12 +182,13 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
   double* Tcur = T + S;   // accepted times
   double* T0 = Tcur + S;  // initial times (bounds)
   double* g = T0 + S;     // gradient at Tcur
+  double* gv = g + S;     // gradient of the violation at Tcur (hard constraints)
   std_load_fixed(sv, fixed_vals + b * D * sv.nf);
   for (int i = lane; i < S; i += kWave) T[i] = Tcur[i] = T0[i] = times_io[b * S + i];
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
   int phase = kBase, gi = 0, evals = 0, nsolve = 0;
-  double f = 0.0, fv = 0.0, Jlo = 0.0;
+  double f = 0.0, fv = 0.0, Jlo = 0.0, vlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   bool bad = false, not_spd = false;
   while (phase != kDone) {
@@ -203,9 +204,13 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
       gi = 0;
     } else if (phase == kGrad) {
       if (gi & 1) {
-        if (lane == 0) g[gi >> 1] = (J - Jlo) / (2.0 * p.increment);
+        if (lane == 0) {
+          g[gi >> 1] = (J - Jlo) / (2.0 * p.increment);
+          gv[gi >> 1] = (viol - vlo) / (2.0 * p.increment);
+        }
       } else {
         Jlo = J;
+        vlo = viol;
       }
       if (++gi == 2 * S) phase = kTrial;
     } else {  // trial point
@@ -229,13 +234,15 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
     } else if (phase == kTrial) {
       if (!(evals < max_evals && alpha > 1e-9)) break;
       // Scaled direction -g_n T0_n, normalised so the largest relative move
-      // is alpha.
+      // is alpha; from an infeasible incumbent (hard constraints) the
+      // direction descends the violation instead.
+      const double* dir = fv > 0.0 ? gv : g;
       double gmax = 0.0;
-      for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(g[i] * T0[i]));
+      for (int i = 0; i < S; ++i) gmax = fmax(gmax, fabs(dir[i] * T0[i]));
       if (!(gmax > 0.0)) break;
       int moved = 0;
       for (int i = 0; i < S; ++i) {
-        const double step = alpha * T0[i] * (g[i] * T0[i]) / gmax;
+        const double step = alpha * T0[i] * (dir[i] * T0[i]) / gmax;
         double tn = Tcur[i] - step;
         tn = fmin(fmax(tn, kLower), 2.0 * T0[i]);
         if (tn != Tcur[i]) moved = 1;

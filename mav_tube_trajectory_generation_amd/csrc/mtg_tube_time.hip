@@ -248,8 +248,13 @@ hipError_t evaluate_points(const TubeArgs& a, int P, const double* T, double tol
     SoftLimits lim{};
     lim.n = p.n_soft;
     for (int c = 0; c < p.n_soft; ++c) lim.value[c] = p.soft_limit[c];
-    const SoftCostArgs none{};
-    const SoftCostArgs last{w.softc, lim, p.soft_weight, p.soft_maximum_cost};
+    // Finished trajectories (skip) are left out of the searches too.
+    SoftCostArgs none{};
+    none.skip = skip;
+    none.skip_rep = P;
+    SoftCostArgs last{w.softc, lim, p.soft_weight, p.soft_maximum_cost};
+    last.skip = skip;
+    last.skip_rep = P;
     for (int c = 0; c < p.n_soft; ++c) {
       e = launch_max_magnitude(a.N, 3, S, BP, p.soft_derivative[c], w.coeffs, w.pts, nullptr,
                                w.maxima, nullptr, p.n_soft, c, c == p.n_soft - 1 ? last : none,

@@ -64,6 +64,9 @@ def local_best(local_costs, global_batch, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     start, count = shard_range(global_batch, world, rank)
+    if local_costs.numel() != count:
+        raise ValueError(f"rank {rank}: {local_costs.numel()} local costs, but the shard of "
+                         f"{global_batch} over {world} ranks holds {count}")
     if local_costs.is_cuda:  # one HIP launch (mtg_select_local)
         lib, check, ptr, stream = _hip()
         c = local_costs

@@ -1775,30 +1775,37 @@ static int timeOptimizeImpl(int N, int D, int r, int S, int K, const uint8_t* ma
     return J;
   };
 
-  auto gradient = [&](const std::vector<double>& t, std::vector<double>* g) {
-    for (int n = 0; n < S; ++n) {  // grad_mode 2 of orc_time_cost
+  // Central differences of J (grad_mode 2 of orc_time_cost) and, for the
+  // hard constraints, of the violation at the same points.
+  auto gradient = [&](const std::vector<double>& t, std::vector<double>* g,
+                      std::vector<double>* gv) {
+    for (int n = 0; n < S; ++n) {
       std::vector<double> ts = t, tb = t;
       ts[n] = ts[n] <= 0.1 ? 0.1 : ts[n] - increment;
       tb[n] = tb[n] <= 0.1 ? 0.1 : tb[n] + increment;
       const double Js = objective(ts);
+      const double vs = viol;
       const double Jb = objective(tb);
       (*g)[n] = (Jb - Js) / (2.0 * increment);
+      (*gv)[n] = (viol - vs) / (2.0 * increment);
     }
   };
   const std::vector<double> T0(times_io, times_io + S);
-  std::vector<double> T = T0, g(S), trial(S);
+  std::vector<double> T = T0, g(S), gv(S), trial(S);
   double f = objective(T);
   double fv = viol;
-  gradient(T, &g);
+  gradient(T, &g, &gv);
   int n_eval = 1;
   double alpha = 0.1;
   while (n_eval < max_evals && alpha > 1e-9) {
+    // From an infeasible incumbent the step descends the violation.
+    const std::vector<double>& dir = fv > 0.0 ? gv : g;
     double gmax = 0.0;
-    for (int n = 0; n < S; ++n) gmax = std::max(gmax, std::fabs(g[n] * T0[n]));
+    for (int n = 0; n < S; ++n) gmax = std::max(gmax, std::fabs(dir[n] * T0[n]));
     if (!(gmax > 0.0)) break;
     bool same = true;
     for (int n = 0; n < S; ++n) {
-      const double x = T[n] - alpha * T0[n] * (g[n] * T0[n]) / gmax;
+      const double x = T[n] - alpha * T0[n] * (dir[n] * T0[n]) / gmax;
       trial[n] = std::min(std::max(x, 0.1), 2.0 * T0[n]);
       same = same && trial[n] == T[n];
     }
@@ -1812,7 +1819,7 @@ static int timeOptimizeImpl(int N, int D, int r, int S, int K, const uint8_t* ma
       f = ft;
       fv = vt;
       alpha = std::min(alpha * 1.5, 1.0);
-      gradient(T, &g);
+      gradient(T, &g, &gv);
     } else {
       alpha *= 0.5;
     }

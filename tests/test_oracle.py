@@ -362,3 +362,27 @@ def test_free_objectives_oracle(oracle):
         d3, J3, e3 = oracle.free_optimize(N, R, v, t, dp, 10)
         assert np.max(np.abs(d3 - ref["dp"])) <= 1e-8 * (1 + np.max(np.abs(ref["dp"])))
         assert J3 <= J2 and 2 <= e3 <= 10
+
+
+def test_hard_constraint_optimizer_descends_violation(oracle):
+    """The device optimiser's hard-constraint mode (use_soft_constraints =
+    false, nonlinear_impl:861-872; oracle port orc_time_optimize_hard) steps
+    along the violation's central-difference gradient while the incumbent is
+    infeasible, so from an infeasible start the violation falls (the plain
+    -grad J direction shortens the times and raises |v|, |a|)."""
+    N, R, D, S, tol = 10, 4, 3, 6, 0.1
+    for seed in (960, 961, 962):
+        v = standard_vertices(N, S, D, seed)
+        t0 = oracle.estimate_segment_times(v, 3.0, 5.0)
+        c0 = oracle.linear_solve(N, R, v, t0)["coeffs"]
+        lims = [(1, 0.8 * oracle.max_magnitude(N, c0, t0, 1)["value"]),
+                (2, 0.8 * oracle.max_magnitude(N, c0, t0, 2)["value"])]
+        T, _, _ = oracle.time_optimize(N, R, v, t0, 20, soft=lims, hard=True,
+                                       hard_tolerance=tol)
+
+        def viol(c, t):
+            return max(oracle.max_magnitude(N, c, t, k)["value"] - lim - tol for k, lim in lims)
+
+        v0 = viol(c0, t0)
+        v1 = viol(oracle.linear_solve(N, R, v, T)["coeffs"], T)
+        assert v0 > 0.0 and v1 < 0.5 * v0, (seed, v0, v1)

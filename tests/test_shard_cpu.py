@@ -57,6 +57,13 @@ def _worker(rank, world, port, global_batch, result_q):
     ties = select_best_device(torch.from_numpy(tie), global_batch).tolist()
     # An empty shard (global batch smaller than the world) never wins.
     tiny = select_best_device(torch.tensor([3.0] if rank == 0 else []), 1).tolist()
+    # A cost tensor that is not this rank's shard is refused before any launch.
+    try:
+        select_best_device(torch.from_numpy(costs[:-1]), global_batch)
+        short_refused = False
+    except ValueError:
+        short_refused = True
+    assert short_refused
     result_q.put((rank, idx, cost, owner, best.numpy(), dev_triple, all_nan, ties, tiny))
     dist.barrier()
     dist.destroy_process_group()

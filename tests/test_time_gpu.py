@@ -240,6 +240,11 @@ def test_time_optimize_hard_constraints_vs_oracle(ctx, dev, oracle, kernel, star
         viol = max(oracle.max_magnitude(N, c1, T, k)["value"] - lim - tol for k, lim in lims)
         if start == "feasible":
             assert viol <= 1e-9, viol
+        else:
+            # From an infeasible start the steps descend the violation.
+            viol0 = max(oracle.max_magnitude(N, c0, times[b], k)["value"] - lim - tol
+                        for k, lim in lims)
+            assert viol0 > 0.0 and viol < viol0, (viol0, viol)
         if int(out["evals"][0]) == ec and np.max(np.abs(T - Tc) / Tc) <= 1e-6:
             assert rel_err(float(out["cost"][0]), fc) <= 1e-6
             agree += 1
