@@ -22,9 +22,14 @@
 //     initial_stepsize_rel default) and evaluation budget max_iterations
 //     (NLopt maxeval, :101).  Optimiser trajectories therefore differ from NLopt's
 //     (parity unpinned); the callback value is pinned;
-//   * the collision cost (w_c > 0) needs the supereight octree (out of scope,
-//     SURVEY.md §8f rank 4; the reference dereferences a null octree there,
-//     §8a T6): it is ignored with a warning;
+//   * the collision cost reads a dense occupancy grid (setOccupancyGrid) in
+//     place of the supereight octree (setOctree).  kOptimizeFreeConstraints
+//     AndCollision and kOptimizeFreeConstraintsAndCollisionAndTime (the
+//     reference demo, src/main.cpp:77) run on the device (mtg_coll_optimize:
+//     a batched projected L-BFGS in place of NLopt's LD_LBFGS, parity
+//     unpinned); the time-only and free-derivative objectives ignore w_c
+//     with a warning, as the reference's objectiveFunctionTime would
+//     dereference a null octree there (§8a T6);
 //   * addMaximumMagnitudeConstraint with use_soft_constraints (the default)
 //     adds the soft cost of evaluateMaximumMagnitudeAsSoftConstraint
 //     (:2735-2766) to the objective, evaluated on the device after every
@@ -36,7 +41,10 @@
 //     device optimiser then accepts only feasible improving trials
 //     (feasibility first from an infeasible start, mtg_time_params
 //     hard_constraints); the other objectives' device optimisers ignore hard
-//     constraints with a warning.
+//     constraints with a warning.  As in the reference, the constraint is
+//     only registered as an NLopt inequality when the selected algorithm
+//     takes one (addMaximumMagnitudeConstraint returns false otherwise, e.g.
+//     for the default LN_SBPLX, and the constraint then has no effect).
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_NONLINEAR_H_
 
@@ -52,6 +60,39 @@
 #include <vector>
 
 #include "mav_tube_trajectory_generation_amd/polynomial_optimization_qcqp.h"
+
+// The NLopt names the reference's parameters and return codes use
+// (nlopt.hpp is absent: only the enumerations, in NLopt's numbering, so that
+// code such as main.cpp:104-105 `static_cast<nlopt::algorithm>(11)` and
+// comparisons with nlopt::MAXEVAL_REACHED compile unchanged).
+namespace nlopt {
+enum algorithm {
+  GN_DIRECT = 0, GN_DIRECT_L, GN_DIRECT_L_RAND, GN_DIRECT_NOSCAL, GN_DIRECT_L_NOSCAL,
+  GN_DIRECT_L_RAND_NOSCAL, GN_ORIG_DIRECT, GN_ORIG_DIRECT_L, GD_STOGO, GD_STOGO_RAND,
+  LD_LBFGS_NOCEDAL, LD_LBFGS, LN_PRAXIS, LD_VAR1, LD_VAR2, LD_TNEWTON, LD_TNEWTON_RESTART,
+  LD_TNEWTON_PRECOND, LD_TNEWTON_PRECOND_RESTART, GN_CRS2_LM, GN_MLSL, GD_MLSL, GN_MLSL_LDS,
+  GD_MLSL_LDS, LD_MMA, LN_COBYLA, LN_NEWUOA, LN_NEWUOA_BOUND, LN_NELDERMEAD, LN_SBPLX,
+  LN_AUGLAG, LD_AUGLAG, LN_AUGLAG_EQ, LD_AUGLAG_EQ, LN_BOBYQA, GN_ISRES, AUGLAG, AUGLAG_EQ,
+  G_MLSL, G_MLSL_LDS, LD_SLSQP, LD_CCSAQ, GN_ESCH, GN_AGS, NUM_ALGORITHMS
+};
+enum result {
+  FAILURE = -1, INVALID_ARGS = -2, OUT_OF_MEMORY = -3, ROUNDOFF_LIMITED = -4, FORCED_STOP = -5,
+  SUCCESS = 1, STOPVAL_REACHED = 2, FTOL_REACHED = 3, XTOL_REACHED = 4, MAXEVAL_REACHED = 5,
+  MAXTIME_REACHED = 6
+};
+// Algorithms that accept inequality constraints (NLopt's add_inequality_
+// constraint throws for the others).
+inline bool takesInequalityConstraints(algorithm a) {
+  switch (a) {
+    case GN_ORIG_DIRECT: case GN_ORIG_DIRECT_L: case LD_MMA: case LN_COBYLA: case LN_AUGLAG:
+    case LD_AUGLAG: case LN_AUGLAG_EQ: case LD_AUGLAG_EQ: case GN_ISRES: case AUGLAG:
+    case AUGLAG_EQ: case LD_SLSQP: case LD_CCSAQ: case GN_AGS:
+      return true;
+    default:
+      return false;
+  }
+}
+}  // namespace nlopt
 
 namespace mav_trajectory_generation {
 
@@ -85,6 +126,7 @@ struct NonlinearOptimizationParameters {
   int max_iterations = 5;  // read: objective-evaluation budget
   double max_time = -1;
   double time_penalty = 500.0;  // read
+  nlopt::algorithm algorithm = nlopt::LN_SBPLX;  // read: whether hard constraints are taken
   int random_seed = 0;
   bool use_soft_constraints = true;
   double soft_constraint_weight = 100.0;
@@ -114,6 +156,10 @@ struct NonlinearOptimizationParameters {
   double coll_check_time_increment = 0.1;
   bool is_coll_raise_first_iter = true;
   double add_coll_raise = 0.0;
+  double use_esdf = 0.0;
+  // Build extension: history pairs of the device L-BFGS that stands in for
+  // NLopt's LD_LBFGS in the collision objectives.
+  int lbfgs_memory = 10;
 };
 
 // polynomial_optimization_nonlinear.h:212-236.
@@ -163,7 +209,11 @@ class PolynomialOptimizationNonLinear {
     return ret;
   }
 
-  // nonlinear_impl:847-875.
+  // nonlinear_impl:847-875.  The constraint is stored either way (it also
+  // sets the free-derivative bounds of setFreeEndpointDerivativeHardConstraints,
+  // :2890-2902); with use_soft_constraints = false it becomes an inequality
+  // only if the algorithm takes one, else false is returned (NLopt throws in
+  // add_inequality_constraint, :862-872) and the constraint is inactive.
   bool addMaximumMagnitudeConstraint(int derivative_order, double maximum_value) {
     MTG_CHECK(derivative_order >= 0, "derivative must be >= 0");
     MTG_CHECK(maximum_value >= 0.0, "maximum_value must be >= 0");
@@ -173,6 +223,8 @@ class PolynomialOptimizationNonLinear {
       return false;
     }
     soft_.push_back(std::make_pair(derivative_order, maximum_value));
+    if (!params_.use_soft_constraints && !nlopt::takesInequalityConstraints(params_.algorithm))
+      return false;
     return true;
   }
 
@@ -234,9 +286,13 @@ class PolynomialOptimizationNonLinear {
       return optimizeFreeConstraints();
     if (params_.objective == NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndTime)
       return optimizeTimeAndFreeConstraints();
+    if (params_.objective == NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndCollision)
+      return optimizeCollision(false);
+    if (params_.objective ==
+        NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndCollisionAndTime)
+      return optimizeCollision(true);
     MTG_CHECK(params_.objective == NonlinearOptimizationParameters::kOptimizeTime,
-              "objective not part of this build: kOptimizeTime, kOptimizeFreeConstraints and "
-              "kOptimizeFreeConstraintsAndTime (SURVEY.md 8a T1-T6, 8f rank 2)");
+              "unknown optimization objective (nonlinear_impl:305-307)");
     warnCollision();
     if (params_.solve_time_with_qcqp) return optimizeTimeQCQP();
     const auto t0 = std::chrono::steady_clock::now();
@@ -384,16 +440,70 @@ class PolynomialOptimizationNonLinear {
     }
   }
 
+  // setOctree (polynomial_optimization_nonlinear.h:357-363) is kept for
+  // source compatibility: supereight is absent, so the octree is not read and
+  // the map must be given to setOccupancyGrid.
+  void setOctree(const void* octree) {
+    if (octree)
+      internal::warn("setOctree: supereight is not available; pass the map to setOccupancyGrid");
+  }
+
   // Occupancy map for the collision cost (build extension standing in for
   // setOctree, polynomial_optimization_nonlinear.h:357-363; supereight is
   // absent): a dense grid of log-odds, voxel (x, y, z) at (z*ny + y)*nx + x,
   // occupied iff >= 0, uploaded once.
   void setOccupancyGrid(const std::vector<float>& occupancy, int nx, int ny, int nz) {
-    MTG_CHECK(static_cast<size_t>(nx) * ny * nz == occupancy.size(), "grid size mismatch");
+    MTG_CHECK(nx >= 0 && ny >= 0 && nz >= 0 &&
+                  static_cast<size_t>(nx) * ny * nz == occupancy.size(),
+              "grid size mismatch");
     occ_dims_[0] = nx;
     occ_dims_[1] = ny;
     occ_dims_[2] = nz;
     occupancy_.upload(occupancy);
+    grid_set_ = true;
+  }
+
+  // The collision objective at x (objectiveFunctionFreeConstraintsAndCollision,
+  // nonlinear_impl:1115-1272, x = d_p dimension-major; with the objective
+  // kOptimizeFreeConstraintsAndCollisionAndTime :1274-1535, x = [T; d_p]) on
+  // the tube-pattern problem, with the reference's collision raise state of
+  // this object (total_cost_iter0_ set by the first evaluation, the last
+  // evaluation's total).  `gradient` (nullable) is resized to x.size().
+  double evaluateCollisionObjective(const std::vector<double>& x,
+                                    std::vector<double>* gradient) {
+    MTG_CHECK(grid_set_, "setOccupancyGrid first");
+    const int mode = collisionMode();
+    const size_t np = poly_opt_.getNumberFreeConstraints();
+    const size_t S = poly_opt_.getNumberSegments();
+    const size_t nv = (mode ? S : 0) + dimension_ * np;
+    MTG_CHECK(x.size() == nv, "x has " << x.size() << " entries, need " << nv);
+    const mtg_coll_params cp = collParams();
+    const int64_t nb = mtg_coll_workspace_bytes(poly_opt_.getPlan(), 1, mode, &cp, 0);
+    MTG_CHECK(nb > 0, "mtg_coll_workspace_bytes: " << mtg_status_string(static_cast<int>(nb)));
+    internal::DeviceBuffer<double> d_df, d_x, d_t, d_ref, d_cost(1), d_g(nv), d_terms(4);
+    internal::DeviceBuffer<int32_t> d_coll(1), d_st(1);
+    internal::DeviceBuffer<unsigned char> ws(static_cast<size_t>(nb));
+    d_df.upload(packFixedQcqp());
+    d_x.upload(x);
+    d_t.upload(segmentTimesOfQcqp());
+    const double ref = params_.is_coll_raise_first_iter ? total_cost_iter0_ : last_total_;
+    d_ref.upload(&ref, 1);
+    internal::checkStatus(
+        mtg_coll_cost(poly_opt_.getPlan(), 1, mode, d_df.get(), d_x.get(), d_t.get(),
+                      occupancy_.get(), occ_dims_[0], occ_dims_[1], occ_dims_[2], &cp,
+                      d_ref.get(), d_cost.get(), gradient ? d_g.get() : nullptr, d_terms.get(),
+                      d_coll.get(), d_st.get(), ws.get(), static_cast<size_t>(nb), nullptr),
+        "mtg_coll_cost");
+    internal::synchronize();
+    double J = 0.0;
+    d_cost.download(&J, 1);
+    if (gradient) *gradient = d_g.download();
+    if (is_iter0_) {  // nonlinear_impl:1253-1257
+      total_cost_iter0_ = J;
+      is_iter0_ = false;
+    }
+    last_total_ = J;
+    return J;
   }
 
   // getCostAndGradientCollision (nonlinear_impl:1609-1780) of the tube-pattern
@@ -401,7 +511,7 @@ class PolynomialOptimizationNonLinear {
   // (mtg_collision_cost); gradient (nullable) w.r.t. its free derivatives.
   double getCostAndGradientCollision(std::vector<VectorXd>* gradients, bool* is_collision) {
     MTG_CHECK(is_collision != nullptr, "is_collision must not be null");
-    MTG_CHECK(occupancy_.size() > 0 || occ_dims_[0] == 0, "setOccupancyGrid first");
+    MTG_CHECK(grid_set_, "setOccupancyGrid first");
     Trajectory traj;
     poly_opt_.getTrajectory(&traj);
     const int S = traj.K(), D = traj.D();
@@ -412,17 +522,7 @@ class PolynomialOptimizationNonLinear {
         const VectorXd c = traj.segments()[s][d].getCoefficients(0);
         for (int k = 0; k < N; ++k) coeffs[(static_cast<size_t>(s) * D + d) * N + k] = c[k];
       }
-    mtg_collision_params cp;
-    cp.map_resolution = params_.map_resolution;
-    for (int k = 0; k < 3; ++k) {
-      cp.min_bound[k] = params_.min_bound[k];
-      cp.max_bound[k] = params_.max_bound[k];
-    }
-    cp.epsilon = params_.epsilon;
-    cp.robot_radius = params_.robot_radius;
-    cp.coll_pot_multiplier = params_.coll_pot_multiplier;
-    cp.coll_check_time_increment = params_.coll_check_time_increment;
-    cp.box_side = 20;
+    const mtg_collision_params cp = collisionParams();
     const size_t np = poly_opt_.getNumberFreeConstraints();
     internal::DeviceBuffer<double> d_c, d_t, d_cost(1), d_g(np ? D * np : 1);
     internal::DeviceBuffer<int32_t> d_coll(1);
@@ -459,6 +559,174 @@ class PolynomialOptimizationNonLinear {
   }
 
  private:
+  mtg_collision_params collisionParams() const {
+    mtg_collision_params cp;
+    cp.map_resolution = params_.map_resolution;
+    for (int k = 0; k < 3; ++k) {
+      cp.min_bound[k] = params_.min_bound[k];
+      cp.max_bound[k] = params_.max_bound[k];
+    }
+    cp.epsilon = params_.epsilon;
+    cp.robot_radius = params_.robot_radius;
+    cp.coll_pot_multiplier = params_.coll_pot_multiplier;
+    cp.coll_check_time_increment = params_.coll_check_time_increment;
+    cp.box_side = 20;  // findOccupiedVoxels side (nonlinear_impl:1798)
+    return cp;
+  }
+
+  int collisionMode() const {
+    return params_.objective ==
+                   NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndCollisionAndTime
+               ? 1
+               : 0;
+  }
+
+  mtg_coll_params collParams() const {
+    mtg_coll_params p;
+    p.coll = collisionParams();
+    p.w_d = params_.weights.w_d;
+    p.w_c = params_.weights.w_c;
+    p.w_t = params_.weights.w_t;
+    p.w_sc = params_.weights.w_sc;
+    p.is_collision_safe = params_.is_collision_safe ? 1 : 0;
+    p.is_coll_raise_first_iter = params_.is_coll_raise_first_iter ? 1 : 0;
+    p.add_coll_raise = params_.add_coll_raise;
+    p.simple_numgrad_time = params_.is_simple_numgrad_time ? 1 : 0;
+    p.simple_numgrad_constraints = params_.is_simple_numgrad_constraints ? 1 : 0;
+    p.increment_time = params_.increment_time;
+    // Soft costs only with use_soft_constraints (:1174-1177); otherwise the
+    // constraints would be NLopt inequalities, which LD_LBFGS does not take.
+    p.n_soft = params_.use_soft_constraints ? static_cast<int>(soft_.size()) : 0;
+    for (int c = 0; c < 8; ++c) {
+      p.soft_derivative[c] = c < p.n_soft ? soft_[c].first : 0;
+      p.soft_limit[c] = c < p.n_soft ? soft_[c].second : 1.0;
+    }
+    p.soft_weight = params_.soft_constraint_weight;
+    p.soft_maximum_cost = 1.0e12;
+    p.f_rel = params_.f_rel;
+    p.f_abs = params_.f_abs;
+    p.x_rel = params_.x_rel;
+    p.x_abs = params_.x_abs;
+    p.lbfgs_memory = params_.lbfgs_memory;
+    return p;
+  }
+
+  // setFreeEndpointDerivativeHardConstraints (nonlinear_impl:2858-2905) over
+  // the free derivatives x (dimension-major), including the reference's
+  // stride of derivative_to_optimize per vertex when
+  // solve_with_position_constraint is set (:2879-2880).
+  void freeEndpointBounds(size_t n, std::vector<double>* lo, std::vector<double>* hi) const {
+    const size_t np = poly_opt_.getNumberFreeConstraints();
+    const size_t S = poly_opt_.getNumberSegments();
+    lo->assign(n, -HUGE_VAL);
+    hi->assign(n, HUGE_VAL);
+    const int r = poly_opt_.getDerivativeToOptimize();
+    for (size_t k = 0; k < dimension_; ++k)
+      for (size_t v = 0; v + 1 < S; ++v) {
+        size_t start;
+        if (params_.solve_with_position_constraint) {
+          start = k * np + v * r;
+        } else {
+          start = k * np + v * (r + 1);
+          (*lo)[start] = params_.min_bound[static_cast<long>(k)];
+          (*hi)[start] = params_.max_bound[static_cast<long>(k)];
+        }
+        for (const auto& c : soft_) {
+          const size_t idx =
+              start + (params_.solve_with_position_constraint ? c.first - 1 : c.first);
+          (*lo)[idx] = -std::abs(c.second);
+          (*hi)[idx] = std::abs(c.second);
+        }
+      }
+  }
+
+  // optimizeFreeConstraintsAndCollision (nonlinear_impl:495-607) and
+  // optimizeFreeConstraintsAndCollisionAndTime (:708-845): initial solution
+  // from the tube QCQP (with solve_with_position_constraint directly; else
+  // computeInitialSolutionWithPositionConstraints, :199-272, which rebuilds
+  // the same all-intermediates-free pattern and recovers the same d_p), the
+  // reference's bounds and initial steps, then the device L-BFGS of
+  // mtg_coll_optimize in place of NLopt (max_iterations evaluations, f_rel /
+  // f_abs / x_rel / x_abs).  The problem keeps the best point found.
+  int optimizeCollision(bool with_time) {
+    MTG_CHECK(grid_set_, "setOccupancyGrid first: the collision objectives need a map");
+    MTG_CHECK(dimension_ == 3, "the collision objectives are 3-D (nonlinear_impl:1796-1797)");
+    const auto t0 = std::chrono::steady_clock::now();
+    poly_opt_.solveQCQP();
+    poly_opt_.getTrajectory(&trajectory_initial_);
+    std::vector<VectorXd> free;
+    poly_opt_.getFreeConstraints(&free);
+    MTG_CHECK(!free.empty() && free.front().size() > 0, "no free constraints (:516-517)");
+    const std::vector<double> d0 = packFree(free);
+    std::vector<double> times = segmentTimesOfQcqp();
+    const size_t S = times.size(), np = poly_opt_.getNumberFreeConstraints();
+    const size_t off = with_time ? S : 0, nv = off + d0.size();
+    std::vector<double> x(nv), lo(nv), hi(nv), step(nv);
+    for (size_t i = 0; i < S && with_time; ++i) {
+      x[i] = times[i];
+      lo[i] = 0.1;  // :785-789
+      hi[i] = HUGE_VAL;
+    }
+    std::vector<double> lod, hid;
+    freeEndpointBounds(d0.size(), &lod, &hid);
+    for (size_t i = 0; i < d0.size(); ++i) {
+      x[off + i] = d0[i];
+      lo[off + i] = lod[i];
+      hi[off + i] = hid[i];
+    }
+    for (size_t i = 0; i < nv; ++i) {  // :559-567 (position steps) and :800-805
+      const double a = std::abs(x[i]);
+      step[i] = (!with_time && a > 5) ? params_.initial_stepsize_position
+                                      : params_.initial_stepsize_rel * a;
+    }
+    const int mode = with_time ? 1 : 0;
+    const mtg_coll_params cp = collParams();
+    const int64_t nb = mtg_coll_workspace_bytes(poly_opt_.getPlan(), 1, mode, &cp, 1);
+    MTG_CHECK(nb > 0, "mtg_coll_workspace_bytes: " << mtg_status_string(static_cast<int>(nb)));
+    internal::DeviceBuffer<double> d_df, d_x, d_t, d_lo, d_hi, d_step, d_cost(1), d_terms(4);
+    internal::DeviceBuffer<int32_t> d_ev(1), d_res(1), d_st(1);
+    internal::DeviceBuffer<unsigned char> ws(static_cast<size_t>(nb));
+    d_df.upload(packFixedQcqp());
+    d_x.upload(x);
+    d_t.upload(times);
+    d_lo.upload(lo);
+    d_hi.upload(hi);
+    d_step.upload(step);
+    const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
+    internal::checkStatus(
+        mtg_coll_optimize(poly_opt_.getPlan(), 1, mode, d_df.get(), d_x.get(), d_t.get(),
+                          d_lo.get(), d_hi.get(), d_step.get(), occupancy_.get(), occ_dims_[0],
+                          occ_dims_[1], occ_dims_[2], &cp, budget, d_cost.get(), d_ev.get(),
+                          d_res.get(), d_st.get(), d_terms.get(), ws.get(),
+                          static_cast<size_t>(nb), nullptr),
+        "mtg_coll_optimize");
+    internal::synchronize();
+    x = d_x.download();
+    int32_t evals = 0, res = 0, st = 0;
+    d_ev.download(&evals, 1);
+    d_res.download(&res, 1);
+    d_st.download(&st, 1);
+    double terms[4] = {0, 0, 0, 0};
+    d_terms.download(terms, 4);
+    if (with_time) {
+      for (size_t i = 0; i < S; ++i) times[i] = x[i];
+      poly_opt_.updateSegmentTimes(times);
+    }
+    for (size_t d = 0; d < dimension_; ++d)
+      for (size_t i = 0; i < np; ++i) free[d][i] = x[off + d * np + i];
+    poly_opt_.setFreeConstraints(free);
+    optimization_info_.n_iterations = evals;
+    optimization_info_.cost_trajectory = terms[0];
+    optimization_info_.cost_collision = terms[1];
+    optimization_info_.cost_time = terms[2];
+    optimization_info_.cost_soft_constraints = terms[3];
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? res : nlopt::FAILURE;
+    optimization_info_.optimization_time =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    free_optimized_ = true;
+    return optimization_info_.stopping_reason;
+  }
+
   // optimizeTime in the fork's form: initial QCQP solve (nonlinear_impl:
   // 341-349), device optimiser over the QCQP objective, final QCQP solve at
   // the optimised times.
@@ -563,26 +831,8 @@ class PolynomialOptimizationNonLinear {
     poly_opt_.getFreeConstraints(&free);
     const std::vector<double> x0 = packFree(free);
     const size_t np = poly_opt_.getNumberFreeConstraints();
-    const size_t S = poly_opt_.getNumberSegments();
-    std::vector<double> lo(x0.size(), -HUGE_VAL), hi(x0.size(), HUGE_VAL);
-    const int r = poly_opt_.getDerivativeToOptimize();
-    for (size_t k = 0; k < dimension_; ++k)
-      for (size_t n = 0; n + 1 < S; ++n) {
-        size_t start;
-        if (params_.solve_with_position_constraint) {
-          start = k * np + n * r;
-        } else {
-          start = k * np + n * (r + 1);
-          lo[start] = params_.min_bound[static_cast<long>(k)];
-          hi[start] = params_.max_bound[static_cast<long>(k)];
-        }
-        for (const auto& c : soft_) {
-          const size_t idx =
-              start + (params_.solve_with_position_constraint ? c.first - 1 : c.first);
-          lo[idx] = -std::abs(c.second);
-          hi[idx] = std::abs(c.second);
-        }
-      }
+    std::vector<double> lo, hi;
+    freeEndpointBounds(x0.size(), &lo, &hi);
     internal::DeviceBuffer<double> d_df, d_dp, d_t, d_lo, d_hi, d_cost(1);
     internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
     d_df.upload(packFixedQcqp());
@@ -696,7 +946,8 @@ class PolynomialOptimizationNonLinear {
   }
   void warnCollision() const {
     if (params_.weights.w_c > 0.0)
-      internal::warn("collision cost (w_c > 0) is out of scope here and ignored");
+      internal::warn("this objective has no collision term here (w_c > 0 ignored; "
+                     "kOptimizeFreeConstraintsAndCollision(AndTime) use it)");
   }
   std::vector<double> packFixed() const {
     std::vector<VectorXd> df;
@@ -718,6 +969,12 @@ class PolynomialOptimizationNonLinear {
   std::vector<std::pair<int, double>> soft_;  // (derivative, maximum_value)
   internal::DeviceBuffer<float> occupancy_;
   int occ_dims_[3] = {0, 0, 0};
+  bool grid_set_ = false;
+  // Collision raise state (polynomial_optimization_nonlinear.h:672-673, and
+  // the optimization_info_ totals of the last evaluation, :1216-1219).
+  double total_cost_iter0_ = 0.0;
+  double last_total_ = 0.0;
+  bool is_iter0_ = true;
   bool free_optimized_ = false;
   bool qcqp_time_optimized_ = false;
 };

@@ -491,6 +491,102 @@ int mtg_collision_cost(const mtg_plan* plan, int64_t B, const double* coeffs,
                        double* grad_coeffs, double* grad_free, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Collision-driven objectives of PolynomialOptimizationNonLinear: the
+ * reference demo's path (src/main.cpp:77, 104-105: kOptimizeFreeConstraints
+ * AndCollision with NLopt LD_LBFGS).
+ *   mode 0  objectiveFunctionFreeConstraintsAndCollision
+ *           (nonlinear_impl:1115-1272), x = d_p (D x n_free, dimension-major,
+ *           the x layout of :1130-1141), segment times from `times`;
+ *   mode 1  objectiveFunctionFreeConstraintsAndCollisionAndTime
+ *           (:1274-1535), x = [T (S); d_p (D x n_free)].
+ * J = w_d J_d + w_c J_c + w_t J_t (mode 1) + w_sc J_sc with
+ *   J_d  = sum_dim d^T R d (getCostAndGradientDerivative, :1537-1606),
+ *          gradient 2 (R_pf d_f + R_pp d_p);
+ *   J_c  = the collision walk of mtg_collision_cost (:1609-1780) with its
+ *          eq. (14) gradient through L = A^-1 M; on a collision J_c = 0 and
+ *          the gradient keeps the terms accumulated before it (the
+ *          reference's zeroing loop at :1773-1777 works on copies);
+ *   J_sc = evaluateMaximumMagnitudeAsSoftConstraint (:2735-2766) when
+ *          n_soft > 0, gradient by central differences over every free
+ *          variable with step coll.map_resolution
+ *          (getCostAndGradientSoftConstraints, :2365-2432; mode 1 with
+ *          simple_numgrad_constraints: forward differences,
+ *          getCostAndGradientSoftConstraintsSimple :2434-2493);
+ *   J_t  = sum T (mode 1; getCostAndGradientTime :2495-2584): gradient
+ *          w_d dJ_d/dT_n + w_c dJ_c/dT_n + w_sc dJ_sc/dT_n + w_t by central
+ *          (forward with simple_numgrad_time, :2586-2657) differences with
+ *          step increment_time and the 0.1 clamp of :2529-2530, d held
+ *          fixed; the perturbed J_c walks the coefficients of T over the
+ *          perturbed segment times (L_ is not refreshed there) and dJ_sc/dT
+ *          is 0 (updateSegmentTimes leaves the segments that
+ *          computeMaximumOfMagnitude reads unchanged).
+ * When the walk at x collides, J_d, J_sc and J_t are not evaluated (0, zero
+ * gradients, :1171-1178) and with is_collision_safe the collision term is
+ * raised so that J = raise_ref + add_coll_raise (:1207-1226); raise_ref is
+ * the caller's total_cost_iter0_ (is_coll_raise_first_iter) or the previous
+ * evaluation's total (NULL: 0, the reference's initial values).  Collisions
+ * of the perturbed-time walks are ignored (J_c = 0 there; the reference
+ * dereferences a null gradient vector in that case, :1773-1777).
+ * terms (B x 4, nullable): w_d J_d, w_c J_c (after the raise), w_t J_t,
+ * w_sc J_sc (OptimizationInfo cost_trajectory / collision / time /
+ * soft_constraints).
+ *
+ * mtg_coll_optimize replaces the NLopt run of optimizeFreeConstraintsAnd
+ * Collision (:495-607) / ...AndCollisionAndTime (:708-845): NLopt is absent,
+ * and LD_LBFGS is replaced by a batched projected L-BFGS run on the device
+ * (memory lbfgs_memory pairs; first direction -g scaled so its largest
+ * entry moves max(initial_step); backtracking by safeguarded quadratic
+ * interpolation on the Armijo condition, c1 = 1e-4, every trial one counted
+ * evaluation; stops at max_evals evaluations (NLopt maxeval), NLopt's
+ * ftol / xtol tests on an accepted step, or a projected gradient of zero).
+ * The collision raise state follows the reference: total_cost_iter0_ is the
+ * first evaluation's J, the "last iteration" is the previous evaluation.
+ *   x_io          B x nx   in: start point, out: best point found
+ *   lower, upper  B x nx   bounds (nullable: unbounded)
+ *   initial_step  B x nx   NLopt initial step (nullable: 0.1 |x0|)
+ *   cost B, evals B, result B (NLopt codes: 1 SUCCESS, 3 FTOL_REACHED,
+ *   4 XTOL_REACHED, 5 MAXEVAL_REACHED, -1 FAILURE), status B (MTG_TRAJ_*),
+ *   terms B x 4 (at the best point) — all nullable.
+ * The optimiser enqueues max_evals rounds of a few launches; finished
+ * trajectories are skipped on the device, nothing synchronises with the host
+ * and nothing is allocated: scratch is the caller's `workspace` of at least
+ * mtg_coll_workspace_bytes(plan, B, mode, params, optimize) bytes.
+ * Requirements: D = 3 (the collision cost, :1796-1797), 1 <= n_free,
+ * lbfgs_memory 1..16, n_soft 0..8; times > 0.
+ */
+typedef struct mtg_coll_params {
+  mtg_collision_params coll;      /* map, potential and sampling parameters */
+  double w_d, w_c, w_t, w_sc;     /* ::weights (0.1, 10, 1, 1) */
+  int is_collision_safe;          /* ::is_collision_safe (1) */
+  int is_coll_raise_first_iter;   /* ::is_coll_raise_first_iter (1) */
+  double add_coll_raise;          /* ::add_coll_raise (0) */
+  int simple_numgrad_time;        /* ::is_simple_numgrad_time (mode 1) */
+  int simple_numgrad_constraints; /* ::is_simple_numgrad_constraints (mode 1) */
+  double increment_time;          /* ::increment_time (0.1) */
+  int n_soft;                     /* soft magnitude constraints 0..8 */
+  int soft_derivative[8];         /* derivative order of constraint c, 0..4 */
+  double soft_limit[8];           /* maximum_value of constraint c, > 0 */
+  double soft_weight;             /* ::soft_constraint_weight (100) */
+  double soft_maximum_cost;       /* 1e12 */
+  double f_rel, f_abs, x_rel, x_abs; /* NLopt stopping tests (<= 0: off) */
+  int lbfgs_memory;               /* history pairs (10) */
+} mtg_coll_params;
+
+int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
+                                 const mtg_coll_params* params, int optimize);
+int mtg_coll_cost(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
+                  const double* x, const double* times, const float* occupancy, int nx,
+                  int ny, int nz, const mtg_coll_params* params, const double* raise_ref,
+                  double* cost, double* grad, double* terms, int32_t* collision,
+                  int32_t* status, void* workspace, size_t workspace_bytes, void* stream);
+int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
+                      double* x_io, const double* times, const double* lower,
+                      const double* upper, const double* initial_step, const float* occupancy,
+                      int nx, int ny, int nz, const mtg_coll_params* params, int max_evals,
+                      double* cost, int32_t* evals, int32_t* result, int32_t* status,
+                      double* terms, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * Selection for the multi-GPU path (BASELINE config 4: the
  * shards solve independently and the ranks all-gather costs for
  * selection).  mtg_select_local reduces rank `rank`'s shard of `count`

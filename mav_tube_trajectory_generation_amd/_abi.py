@@ -35,6 +35,59 @@ def make_collision_params(map_resolution, min_bound, max_bound, epsilon=0.5, rob
                            coll_pot_multiplier, coll_check_time_increment, box_side)
 
 
+class CollObjectiveParams(ctypes.Structure):
+    """mtg_coll_params (include/mtg_hip.h)."""
+    _fields_ = [("coll", CollisionParams), ("w_d", ctypes.c_double), ("w_c", ctypes.c_double),
+                ("w_t", ctypes.c_double), ("w_sc", ctypes.c_double),
+                ("is_collision_safe", ctypes.c_int), ("is_coll_raise_first_iter", ctypes.c_int),
+                ("add_coll_raise", ctypes.c_double), ("simple_numgrad_time", ctypes.c_int),
+                ("simple_numgrad_constraints", ctypes.c_int), ("increment_time", ctypes.c_double),
+                ("n_soft", ctypes.c_int), ("soft_derivative", ctypes.c_int * 8),
+                ("soft_limit", ctypes.c_double * 8), ("soft_weight", ctypes.c_double),
+                ("soft_maximum_cost", ctypes.c_double), ("f_rel", ctypes.c_double),
+                ("f_abs", ctypes.c_double), ("x_rel", ctypes.c_double),
+                ("x_abs", ctypes.c_double), ("lbfgs_memory", ctypes.c_int)]
+
+
+# Defaults of NonlinearOptimizationParameters for the collision objectives
+# (polynomial_optimization_nonlinear.h:46-84, cost_weights :163).
+COLL_DEFAULTS = dict(map_resolution=0.0, min_bound=(0.0, 0.0, 0.0), max_bound=(0.0, 0.0, 0.0),
+                     epsilon=0.5, robot_radius=0.5, coll_pot_multiplier=1.0,
+                     coll_check_time_increment=0.1, box_side=20, w_d=0.1, w_c=10.0, w_t=1.0,
+                     w_sc=1.0, is_collision_safe=True, is_coll_raise_first_iter=True,
+                     add_coll_raise=0.0, simple_numgrad_time=False,
+                     simple_numgrad_constraints=False, increment_time=0.1, soft=(),
+                     soft_weight=100.0, soft_maximum_cost=1.0e12, f_rel=0.05, f_abs=-1.0,
+                     x_rel=-1.0, x_abs=-1.0, lbfgs_memory=10)
+
+
+def make_coll_params(**kw):
+    """mtg_coll_params from COLL_DEFAULTS updated by `kw` (soft: list of
+    (derivative, maximum_value) magnitude constraints)."""
+    unknown = set(kw) - set(COLL_DEFAULTS)
+    if unknown:
+        raise MTGError(f"unknown collision-objective parameters {sorted(unknown)}")
+    d = dict(COLL_DEFAULTS, **kw)
+    soft = list(d["soft"] or [])
+    if len(soft) > 8:
+        raise MTGError("at most 8 soft constraints")
+    p = CollObjectiveParams()
+    p.coll = make_collision_params(d["map_resolution"], d["min_bound"], d["max_bound"],
+                                   d["epsilon"], d["robot_radius"], d["coll_pot_multiplier"],
+                                   d["coll_check_time_increment"], d["box_side"])
+    for k in ("w_d", "w_c", "w_t", "w_sc", "add_coll_raise", "increment_time", "soft_weight",
+              "soft_maximum_cost", "f_rel", "f_abs", "x_rel", "x_abs"):
+        setattr(p, k, float(d[k]))
+    for k in ("is_collision_safe", "is_coll_raise_first_iter", "simple_numgrad_time",
+              "simple_numgrad_constraints", "lbfgs_memory"):
+        setattr(p, k, int(d[k]))
+    p.n_soft = len(soft)
+    for i, (der, v) in enumerate(soft):
+        p.soft_derivative[i] = int(der)
+        p.soft_limit[i] = float(v)
+    return p
+
+
 class TimeParams(ctypes.Structure):
     """mtg_time_params (include/mtg_hip.h)."""
     _fields_ = [("time_penalty", ctypes.c_double), ("increment", ctypes.c_double),
@@ -94,6 +147,17 @@ SIGNATURES = {
                                           ctypes.c_int, ctypes.c_int,
                                           ctypes.POINTER(CollisionParams), _vp, _vp, _vp, _vp,
                                           _vp]),
+    "mtg_coll_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64, ctypes.c_int,
+                                                  ctypes.POINTER(CollObjectiveParams),
+                                                  ctypes.c_int]),
+    "mtg_coll_cost": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp, _vp,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(CollObjectiveParams), _vp, _vp, _vp, _vp,
+                                     _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "mtg_coll_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp, _vp,
+                                         _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(CollObjectiveParams), ctypes.c_int, _vp,
+                                         _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "mtg_min_max_magnitude": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp, _vp,
                                              _vp, _vp, _vp, _vp, _vp]),

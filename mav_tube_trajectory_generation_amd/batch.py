@@ -10,7 +10,8 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import MTGError, check, lib, make_collision_params, make_time_params  # noqa: F401
+from ._abi import (MTGError, check, lib, make_coll_params, make_collision_params,  # noqa: F401
+                   make_time_params)
 
 
 def _ptr(t):
@@ -293,6 +294,84 @@ class LinearPlan:
                                        nx, ny, nz, ctypes.byref(params), _ptr(cost), _ptr(coll),
                                        _ptr(gc), _ptr(gf), _stream(dev)), "mtg_collision_cost")
         return dict(cost=cost, collision=coll, grad_coeffs=gc, grad_free=gf)
+
+    # -- collision-driven objectives (mtg_coll_cost / mtg_coll_optimize) -----
+    def _n_vars(self, mode):
+        return (self.S if mode else 0) + self.D * self.n_free
+
+    def coll_workspace_bytes(self, B, params, mode=0, optimize=False):
+        n = lib().mtg_coll_workspace_bytes(self._h, B, mode, ctypes.byref(params),
+                                           1 if optimize else 0)
+        if n < 0:
+            check(int(n), "mtg_coll_workspace_bytes")
+        return int(n)
+
+    def _coll_inputs(self, fixed_vals, x, times, occupancy, mode):
+        import torch
+        B = x.shape[0]
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        _require(x, (B, self._n_vars(mode)), "x")
+        if mode == 0:
+            _require(times, (B, self.S), "times")
+        if not (isinstance(occupancy, torch.Tensor) and occupancy.is_cuda and
+                occupancy.dtype == torch.float32 and occupancy.dim() == 3 and
+                occupancy.is_contiguous()):
+            raise MTGError("occupancy must be a contiguous float32 CUDA tensor [nz, ny, nx]")
+        return B
+
+    def coll_cost(self, fixed_vals, x, times, occupancy, params, mode=0, raise_ref=None,
+                  grad=True, workspace=None):
+        """objectiveFunctionFreeConstraintsAndCollision (mode 0, x = d_p
+        [B, D*n_free]) or ...AndCollisionAndTime (mode 1, x = [T; d_p]
+        [B, S + D*n_free]) on the device (mtg_coll_cost).  params from
+        make_coll_params; raise_ref [B] the collision raise reference (None:
+        0).  Returns dict(cost, grad, terms [B, 4], collision, status)."""
+        import torch
+        B = self._coll_inputs(fixed_vals, x, times, occupancy, mode)
+        dev = x.device
+        nz, ny, nx = occupancy.shape
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        g = torch.empty((B, self._n_vars(mode)), dtype=torch.float64, device=dev) if grad else None
+        terms = torch.empty((B, 4), dtype=torch.float64, device=dev)
+        coll = torch.empty(B, dtype=torch.int32, device=dev)
+        st = torch.empty(B, dtype=torch.int32, device=dev)
+        nb = self.coll_workspace_bytes(B, params, mode, False)
+        ws = _workspace(workspace, nb, dev)
+        check(lib().mtg_coll_cost(self._h, B, mode, _ptr(fixed_vals), _ptr(x),
+                                  _ptr(times) if mode == 0 else None, _ptr(occupancy), nx, ny,
+                                  nz, ctypes.byref(params), _ptr(raise_ref), _ptr(cost), _ptr(g),
+                                  _ptr(terms), _ptr(coll), _ptr(st), _ptr(ws), nb,
+                                  _stream(dev)), "mtg_coll_cost")
+        return dict(cost=cost, grad=g, terms=terms, collision=coll, status=st)
+
+    def coll_optimize(self, fixed_vals, x0, times, occupancy, params, mode=0, max_evals=25,
+                      lower=None, upper=None, initial_step=None, workspace=None):
+        """Device L-BFGS over the collision objective (mtg_coll_optimize;
+        optimizeFreeConstraintsAndCollision / ...AndTime with NLopt
+        replaced).  Returns dict(x, cost, evals, result, status, terms)."""
+        import torch
+        B = self._coll_inputs(fixed_vals, x0, times, occupancy, mode)
+        dev = x0.device
+        nv = self._n_vars(mode)
+        for a, name in ((lower, "lower"), (upper, "upper"), (initial_step, "initial_step")):
+            if a is not None:
+                _require(a, (B, nv), name)
+        nz, ny, nx = occupancy.shape
+        x = x0.clone()
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        ev = torch.empty(B, dtype=torch.int32, device=dev)
+        res = torch.empty(B, dtype=torch.int32, device=dev)
+        st = torch.empty(B, dtype=torch.int32, device=dev)
+        terms = torch.empty((B, 4), dtype=torch.float64, device=dev)
+        nb = self.coll_workspace_bytes(B, params, mode, True)
+        ws = _workspace(workspace, nb, dev)
+        check(lib().mtg_coll_optimize(self._h, B, mode, _ptr(fixed_vals), _ptr(x),
+                                      _ptr(times) if mode == 0 else None, _ptr(lower),
+                                      _ptr(upper), _ptr(initial_step), _ptr(occupancy), nx, ny,
+                                      nz, ctypes.byref(params), max_evals, _ptr(cost), _ptr(ev),
+                                      _ptr(res), _ptr(st), _ptr(terms), _ptr(ws), nb,
+                                      _stream(dev)), "mtg_coll_optimize")
+        return dict(x=x, cost=cost, evals=ev, result=res, status=st, terms=terms)
 
     # -- host (numpy) API ---------------------------------------------------
     def solve_host(self, fixed_vals, times):

@@ -4,67 +4,18 @@
 // the nearest-occupied-voxel search (findOccupiedVoxels :1920-2018,
 // getDistanceOctree :2031-2043) and getCostPotential (:2660-2684).
 //
-// The reference reads a supereight octree (absent here; parity unpinned).  The
-// map is a caller-supplied dense grid of occupancy log-odds (voxel occupied
-// iff value >= 0, checkIfOccupied :2022-2027), voxel (x, y, z) at index
-// (z ny + y) nx + x; voxels outside the grid are unallocated, i.e. free.
-//
-// One 256-thread workgroup per trajectory.  Thread 0 walks the sample
-// sequence exactly as the reference does (per segment t = 0, dt, ... < T_i by
-// repeated addition; the first sample only seeds the running distance; a
-// sample is evaluated once the path length since the last evaluation reaches
-// map_resolution; time_sum carries over segment ends).  Every evaluated
-// sample is one parallel search: the workgroup scans the box of voxels that
-// overlaps the side^3 box around the sample's voxel (supereight's
-// aabb_aabb_collision, inclusive half-plane test) and reduces the nearest
-// occupied distance from the voxel and from its 6 axis neighbours (the
-// central-difference gradient of the potential, :1850-1876, which reuses the
-// centre's occupied set).  Thread 0 then adds c |v| time_sum to J_c and the
-// eq. (14) gradient terms to dJ/dc (per segment coefficient); a collision
-// (distance - robot_radius <= 0, or a position within one voxel of the map
-// bounds, :1803-1811) ends the walk with J_c = 0 and a zero gradient.  The
-// coefficient gradient is finally mapped to the free derivatives of the plan
-// through A_s^-1(T) (L = A^-1 M, :1650-1656).
+// One 256-thread workgroup per trajectory runs the walk of
+// mtg_collision_device.h (thread 0 steps through the samples, the workgroup
+// searches the voxel box of every evaluated sample).  The coefficient
+// gradient is finally mapped to the free derivatives of the plan through
+// A_s^-1(T) (L = A^-1 M, :1650-1656).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 
-#include "mtg_device.h"
-#include "mtg_internal.h"
+#include "mtg_collision_device.h"
 
 namespace mtg {
-
-constexpr int kCollBlock = 256;
-
-namespace {
-
-// getCostPotential (nonlinear_impl:2660-2684).
-__device__ inline double potential(double d, const mtg_collision_params& p, bool* coll) {
-  d -= p.robot_radius;
-  *coll = false;
-  if (d <= 0.0) {
-    *coll = true;
-    return p.coll_pot_multiplier * (-d) + 0.5 * p.epsilon;
-  }
-  if (d <= p.epsilon) {
-    const double e = d - p.epsilon;
-    return 0.5 / p.epsilon * e * e;
-  }
-  return 0.0;
-}
-
-__device__ inline double wg_min(double x, double* red) {
-  for (int off = 32; off > 0; off >>= 1) x = fmin(x, __shfl_xor(x, off, kWave));
-  const int w = threadIdx.x / kWave;
-  __syncthreads();
-  if ((threadIdx.x & (kWave - 1)) == 0) red[w] = x;
-  __syncthreads();
-  double m = red[0];
-  for (int i = 1; i < kCollBlock / kWave; ++i) m = fmin(m, red[i]);
-  return m;
-}
-
-}  // namespace
 
 template <int N>
 __global__ __launch_bounds__(kCollBlock) void collision_cost_kernel(
@@ -73,13 +24,12 @@ __global__ __launch_bounds__(kCollBlock) void collision_cost_kernel(
     const float* __restrict__ occ, int nx, int ny, int nz, mtg_collision_params p,
     double* __restrict__ cost, int32_t* __restrict__ collision, double* __restrict__ grad_coeffs,
     double* __restrict__ grad_free) {
-  constexpr int D = 3, M = N / 2;
+  constexpr int D = 3;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* c_s = sm;                 // S x D x N coefficients
   double* T_s = c_s + S * D * N;    // S
   double* g_s = T_s + S;            // S x D x N  dJ/dc
-  double* smp = g_s + S * D * N;    // sample: pos[3], vel[3], time_sum, t, seg, flag
-  double* red = smp + 10;           // reduction scratch
+  double* scratch = g_s + S * D * N;
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   for (int i = tid; i < S * D * N; i += kCollBlock) {
@@ -88,172 +38,25 @@ __global__ __launch_bounds__(kCollBlock) void collision_cost_kernel(
   }
   for (int i = tid; i < S; i += kCollBlock) T_s[i] = times[b * S + i];
   __syncthreads();
-  const double res = p.map_resolution, dt = p.coll_check_time_increment;
-  // Thread 0's walk state (nonlinear_impl:1670-1768).
-  int seg = 0;
-  double t = 0.0, time_sum = -1.0, dist_sum = 0.0, J = 0.0;
-  double prev[3] = {0.0, 0.0, 0.0};
-  bool in_seg = false, coll = false;
-  for (;;) {
-    if (tid == 0) {
-      bool emit = false;
-      while (!emit && seg < S) {
-        if (!in_seg) {
-          t = 0.0;
-          in_seg = true;
-        } else {
-          t += dt;
-        }
-        if (!(t < T_s[seg])) {  // segment done: time_sum += -dt + (T_i - t)
-          time_sum += -dt + (T_s[seg] - t);
-          ++seg;
-          in_seg = false;
-          continue;
-        }
-        double pos[3], vel[3];
-        for (int d = 0; d < D; ++d) {
-          const double* cd = c_s + (seg * D + d) * N;
-          double x = cd[N - 1], v = (N - 1) * cd[N - 1];
-          for (int n = N - 2; n >= 0; --n) x = fma(x, t, cd[n]);
-          for (int n = N - 2; n >= 1; --n) v = fma(v, t, n * cd[n]);
-          pos[d] = x;
-          vel[d] = v;
-        }
-        if (time_sum < 0.0) {  // the first sample only seeds the integrals
-          time_sum = 0.0;
-          for (int d = 0; d < D; ++d) prev[d] = pos[d];
-          continue;
-        }
-        time_sum += dt;
-        double dd = 0.0;
-        for (int d = 0; d < D; ++d) dd += (pos[d] - prev[d]) * (pos[d] - prev[d]);
-        dist_sum += sqrt(dd);
-        for (int d = 0; d < D; ++d) prev[d] = pos[d];
-        if (dist_sum < res) continue;
-        for (int d = 0; d < D; ++d) {
-          smp[d] = pos[d];
-          smp[3 + d] = vel[d];
-        }
-        smp[6] = time_sum;
-        smp[7] = t;
-        smp[8] = seg;
-        emit = true;
-      }
-      smp[9] = emit ? 1.0 : 0.0;
-    }
-    __syncthreads();
-    if (smp[9] == 0.0) break;
-    const double px = smp[0], py = smp[1], pz = smp[2];
-    // is_valid_state (:1803-1811): within one voxel of the map bounds.
-    const bool valid = !(px < p.min_bound[0] + res || px > p.max_bound[0] - res ||
-                         py < p.min_bound[1] + res || py > p.max_bound[1] - res ||
-                         pz < p.min_bound[2] + res || pz > p.max_bound[2] - res);
-    // Voxel of the sample: (position / res).cast<int>() truncates toward zero.
-    const int vx = static_cast<int>(px / res), vy = static_cast<int>(py / res),
-              vz = static_cast<int>(pz / res);
-    // Nearest occupied voxel from the centre and its 6 neighbours over the
-    // voxels overlapping the box [v - side/2, v - side/2 + side].
-    const int side = p.box_side, lo_x = vx - side / 2 - 1, lo_y = vy - side / 2 - 1,
-              lo_z = vz - side / 2 - 1, ext = side + 2;
-    double m[7];
-    for (int q = 0; q < 7; ++q) m[q] = HUGE_VAL;
-    if (valid) {
-      const int nbox = ext * ext * ext;
-      for (int i = tid; i < nbox; i += kCollBlock) {
-        const int x = lo_x + i % ext, y = lo_y + (i / ext) % ext, z = lo_z + i / (ext * ext);
-        if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) continue;
-        if (!(occ[(static_cast<int64_t>(z) * ny + y) * nx + x] >= 0.0f)) continue;
-        const double ax = x - vx, ay = y - vy, az = z - vz;
-        m[0] = fmin(m[0], ax * ax + ay * ay + az * az);
-        m[1] = fmin(m[1], (ax + 1) * (ax + 1) + ay * ay + az * az);  // v - e_x
-        m[2] = fmin(m[2], (ax - 1) * (ax - 1) + ay * ay + az * az);  // v + e_x
-        m[3] = fmin(m[3], ax * ax + (ay + 1) * (ay + 1) + az * az);
-        m[4] = fmin(m[4], ax * ax + (ay - 1) * (ay - 1) + az * az);
-        m[5] = fmin(m[5], ax * ax + ay * ay + (az + 1) * (az + 1));
-        m[6] = fmin(m[6], ax * ax + ay * ay + (az - 1) * (az - 1));
-      }
-      for (int q = 0; q < 7; ++q) m[q] = wg_min(m[q], red);
-    }
-    if (tid == 0) {
-      // getDistanceOctree (:2031-2043): min |voxel - v| times res (an empty
-      // set gives max double); invalid states keep distance 0 (:1832-1839).
-      auto dist = [&](double d2) {
-        return d2 == HUGE_VAL ? 1.7976931348623157e308 * res : sqrt(d2) * res;
-      };
-      const double c = potential(valid ? dist(m[0]) : 0.0, p, &coll);
-      if (!coll) {
-        const double ts = smp[6], tt = smp[7];
-        const int s = static_cast<int>(smp[8]);
-        const double* vel = smp + 3;
-        const double vn = sqrt(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
-        J += c * vn * ts;
-        if (vn > 1e-6) {  // :1729-1750 (else the gradient term is dropped)
-          double gp[3];
-          for (int k = 0; k < D; ++k) {
-            bool cl, cr;
-            const double left = potential(dist(m[1 + 2 * k]), p, &cl);
-            const double right = potential(dist(m[2 + 2 * k]), p, &cr);
-            gp[k] = (right - left) / (2.0 * res);
-          }
-          // eq. (14): d/dc_n of vn ts c(pos) with pos = sum c_n t^n,
-          // vel = sum n c_n t^(n-1).
-          for (int k = 0; k < D; ++k) {
-            double* g = g_s + (s * D + k) * N;
-            const double a = vn * ts * gp[k], bcoef = ts * c * vel[k] / vn;
-            double tn = 1.0, tn1 = 0.0;  // t^n, n t^(n-1)
-            for (int n = 0; n < N; ++n) {
-              g[n] += a * tn + bcoef * tn1;
-              tn1 = (n + 1) * tn;
-              tn *= tt;
-            }
-          }
-        }
-        dist_sum = 0.0;
-        time_sum = 0.0;
-      } else {
-        smp[9] = -1.0;  // collision: stop
-      }
-    }
-    __syncthreads();
-    if (smp[9] < 0.0) break;
-  }
-  __syncthreads();
-  const bool hit = smp[9] < 0.0;
+  const bool grad = grad_coeffs || grad_free;
+  double J;
+  bool hit;
+  collision_walk<N>(S, c_s, T_s, occ, nx, ny, nz, p, grad, g_s, scratch, &J, &hit);
   if (tid == 0) {
-    if (cost) cost[b] = hit ? 0.0 : J;
+    if (cost) cost[b] = J;
     if (collision) collision[b] = hit ? 1 : 0;
   }
+  // On a collision the gradient keeps the terms accumulated before it (the
+  // reference's zeroing loop works on copies, :1773-1777).
   if (grad_coeffs)
-    for (int i = tid; i < S * D * N; i += kCollBlock)
-      grad_coeffs[b * S * D * N + i] = hit ? 0.0 : g_s[i];
-  if (grad_free) {
-    // dJ/d(vertex v, derivative j) = sum over the segments s in {v-1, v} of
-    // A_s^-1(T_s)[n][(v - s) M + j] dJ/dc_s[n], A_s^-1(T) = D_T^-1 A(1)^-1 S_T.
-    const double* ai = tab + N * N;
-    for (int i = tid; i < D * np; i += kCollBlock) {
-      const int k = i / np, slot = free_map[i % np];
-      const int v = slot / M, j = slot % M;
-      double acc = 0.0;
-      for (int h = 0; h < 2; ++h) {
-        const int s = v - h;  // h = 0: start vertex of segment v; 1: end of v-1
-        if (s < 0 || s >= S) continue;
-        const double T = T_s[s];
-        double tj = 1.0;
-        for (int q = 0; q < j; ++q) tj *= T;
-        double tinv = 1.0;
-        const double* g = g_s + (s * D + k) * N;
-        for (int n = 0; n < N; ++n) {
-          acc += tinv * ai[n * N + h * M + j] * tj * g[n];
-          tinv /= T;
-        }
-      }
-      grad_free[b * D * np + i] = hit ? 0.0 : acc;
-    }
-  }
+    for (int i = tid; i < S * D * N; i += kCollBlock) grad_coeffs[b * S * D * N + i] = g_s[i];
+  if (grad_free)
+    for (int i = tid; i < D * np; i += kCollBlock)
+      grad_free[b * D * np + i] = coll_grad_free<N>(S, D, np, tab + N * N, free_map, T_s, g_s, i);
 }
 
 size_t collision_lds_bytes(int N, int S) {
-  return sizeof(double) * (2 * S * 3 * N + S + 10 + kCollBlock / kWave);
+  return sizeof(double) * (2 * S * 3 * N + S + kCollScratch);
 }
 
 hipError_t launch_collision_cost(const PlanDev& pl, int64_t B, const double* coeffs,

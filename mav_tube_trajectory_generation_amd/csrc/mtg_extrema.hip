@@ -334,4 +334,33 @@ hipError_t launch_soft_cost(int N, int D, int S, int64_t B, const double* coeffs
 #undef CALL
 }
 
+// Soft-constraint cost of B problems by whichever launch shape fits: all
+// constraints in one launch below kSoftOneLaunchMaxBatch problems (latency
+// bound), else one launch per constraint, the last forming the cost (maxima:
+// B x n scratch).  spec.skip is honoured by both.
+hipError_t launch_soft_cost_any(int N, int D, int S, int64_t B, const double* coeffs,
+                                const double* times, const SoftSpec& spec, double* maxima,
+                                double* cost, hipStream_t st) {
+  if (B < kSoftOneLaunchMaxBatch) {
+    const hipError_t e = launch_soft_cost(N, D, S, B, coeffs, times, spec, maxima, cost, st);
+    if (e != hipErrorNotSupported) return e;
+  }
+  SoftLimits lim{};
+  lim.n = spec.n;
+  for (int c = 0; c < spec.n; ++c) lim.value[c] = spec.limit[c];
+  SoftCostArgs none{};
+  none.skip = spec.skip;
+  none.skip_rep = spec.skip_rep;
+  SoftCostArgs last{cost, lim, spec.weight, spec.maximum_cost};
+  last.skip = spec.skip;
+  last.skip_rep = spec.skip_rep;
+  for (int c = 0; c < spec.n; ++c) {
+    const hipError_t e =
+        launch_max_magnitude(N, D, S, B, spec.derivative[c], coeffs, times, nullptr, maxima,
+                             nullptr, spec.n, c, c == spec.n - 1 ? last : none, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 }  // namespace mtg

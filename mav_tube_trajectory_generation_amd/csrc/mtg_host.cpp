@@ -392,16 +392,21 @@ int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                                             static_cast<hipStream_t>(stream)));
 }
 
+// The map / potential / sampling parameters shared by the collision entry
+// points.
+static bool valid_collision_params(const mtg_collision_params& p, int nx, int ny, int nz) {
+  return p.map_resolution > 0.0 && p.epsilon > 0.0 && p.coll_check_time_increment > 0.0 &&
+         p.robot_radius >= 0.0 && p.box_side >= 1 && p.box_side <= 256 && nx >= 0 && ny >= 0 &&
+         nz >= 0;
+}
+
 int mtg_collision_cost(const mtg_plan* plan, int64_t B, const double* coeffs,
                        const double* times, const float* occupancy, int nx, int ny, int nz,
                        const mtg_collision_params* params, double* cost, int32_t* collision,
                        double* grad_coeffs, double* grad_free, void* stream) {
   if (!plan || !params || B < 0 || B > 0x7fffffff || plan->dev.D != 3) return MTG_ERR_INVALID_ARG;
   const mtg_collision_params& p = *params;
-  if (!(p.map_resolution > 0.0) || !(p.epsilon > 0.0) || !(p.coll_check_time_increment > 0.0) ||
-      !(p.robot_radius >= 0.0) || p.box_side < 1 || p.box_side > 256 || nx < 0 || ny < 0 ||
-      nz < 0)
-    return MTG_ERR_INVALID_ARG;
+  if (!valid_collision_params(p, nx, ny, nz)) return MTG_ERR_INVALID_ARG;
   if (mtg::collision_lds_bytes(plan->dev.N, plan->dev.S) > 65536) return MTG_ERR_UNSUPPORTED;
   if (B == 0) return MTG_OK;
   if (!coeffs || !times || (!occupancy && static_cast<int64_t>(nx) * ny * nz > 0))
@@ -455,24 +460,68 @@ int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeff
   // 69.6 -> 43.8 us at B = 1024, 2 constraints).  Large batches are
   // throughput-bound and pack 3 trajectories per workgroup in the
   // per-constraint kernel (74 vs 48 M evaluations/s at B = 65 536).
-  if (B < mtg::kSoftOneLaunchMaxBatch) {
-    const hipError_t e = mtg::launch_soft_cost(N, D, S, B, coeffs, times, spec, maxima, cost, st);
-    if (e != hipErrorNotSupported) return from_hip(e);
-  }
-  // One launch per constraint, the last one forming the cost (also for
-  // trajectories whose lane groups exceed one workgroup).
-  mtg::SoftLimits lim{};
-  lim.n = n_constraints;
-  for (int c = 0; c < n_constraints; ++c) lim.value[c] = limits[c];
-  const mtg::SoftCostArgs none{};
-  const mtg::SoftCostArgs last{cost, lim, weight, maximum_cost};
-  for (int c = 0; c < n_constraints; ++c) {
-    const int rc = from_hip(mtg::launch_max_magnitude(
-        N, D, S, B, derivatives[c], coeffs, times, nullptr, maxima, nullptr, n_constraints, c,
-        c == n_constraints - 1 ? last : none, st));
-    if (rc) return rc;
-  }
-  return MTG_OK;
+  return from_hip(mtg::launch_soft_cost_any(N, D, S, B, coeffs, times, spec, maxima, cost, st));
+}
+
+static bool valid_coll_params(const mtg_plan* plan, int mode, const mtg_coll_params* p) {
+  if (!plan || !p || (mode != 0 && mode != 1) || plan->dev.D != 3 || plan->dev.np < 1)
+    return false;
+  if (p->lbfgs_memory < 1 || p->lbfgs_memory > 16 || p->n_soft < 0 ||
+      p->n_soft > mtg::kMaxSoftConstraints)
+    return false;
+  if (mode == 1 && !(p->increment_time > 0.0)) return false;
+  for (int c = 0; c < p->n_soft; ++c)
+    if (p->soft_derivative[c] < 0 || p->soft_derivative[c] > mtg::kMaxExtremaDerivative ||
+        plan->dev.N - p->soft_derivative[c] - 1 <= 0 || !(p->soft_limit[c] > 0.0))
+      return false;
+  if (mtg::collision_lds_bytes(plan->dev.N, plan->dev.S) > 65536) return false;
+  return true;
+}
+
+int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
+                                 const mtg_coll_params* params, int optimize) {
+  if (B < 0 || !valid_coll_params(plan, mode, params)) return MTG_ERR_INVALID_ARG;
+  if (mtg::coll_problems(plan->dev, B, mode, *params) > 0x7fffffff) return MTG_ERR_INVALID_ARG;
+  return static_cast<int64_t>(
+      mtg::coll_workspace_bytes(plan->dev, B, mode, *params, optimize != 0));
+}
+
+int mtg_coll_cost(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
+                  const double* x, const double* times, const float* occupancy, int nx,
+                  int ny, int nz, const mtg_coll_params* params, const double* raise_ref,
+                  double* cost, double* grad, double* terms, int32_t* collision,
+                  int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
+  if (B < 0 || !valid_coll_params(plan, mode, params) ||
+      !valid_collision_params(params->coll, nx, ny, nz))
+    return MTG_ERR_INVALID_ARG;
+  if (mtg::coll_problems(plan->dev, B, mode, *params) > 0x7fffffff) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  if (!fixed_vals || !x || (mode == 0 && !times) || !workspace ||
+      (!occupancy && static_cast<int64_t>(nx) * ny * nz > 0))
+    return MTG_ERR_INVALID_ARG;
+  return mtg::coll_cost(plan->dev, B, mode, fixed_vals, x, times, occupancy, nx, ny, nz, *params,
+                        raise_ref, cost, grad, terms, collision, status, workspace,
+                        workspace_bytes, static_cast<hipStream_t>(stream));
+}
+
+int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
+                      double* x_io, const double* times, const double* lower,
+                      const double* upper, const double* initial_step, const float* occupancy,
+                      int nx, int ny, int nz, const mtg_coll_params* params, int max_evals,
+                      double* cost, int32_t* evals, int32_t* result, int32_t* status,
+                      double* terms, void* workspace, size_t workspace_bytes, void* stream) {
+  if (B < 0 || max_evals < 1 || !valid_coll_params(plan, mode, params) ||
+      !valid_collision_params(params->coll, nx, ny, nz))
+    return MTG_ERR_INVALID_ARG;
+  if (mtg::coll_problems(plan->dev, B, mode, *params) > 0x7fffffff) return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  if (!fixed_vals || !x_io || (mode == 0 && !times) || !workspace ||
+      (!occupancy && static_cast<int64_t>(nx) * ny * nz > 0))
+    return MTG_ERR_INVALID_ARG;
+  return mtg::coll_optimize(plan->dev, B, mode, fixed_vals, x_io, times, lower, upper,
+                            initial_step, occupancy, nx, ny, nz, *params, max_evals, cost, evals,
+                            result, status, terms, workspace, workspace_bytes,
+                            static_cast<hipStream_t>(stream));
 }
 
 int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank, double* out,

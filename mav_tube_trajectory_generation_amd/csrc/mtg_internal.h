@@ -188,11 +188,31 @@ struct SoftSpec {
 hipError_t launch_soft_cost(int N, int D, int S, int64_t B, const double* coeffs,
                             const double* times, const SoftSpec& spec, double* maxima,
                             double* cost, hipStream_t st);
+hipError_t launch_soft_cost_any(int N, int D, int S, int64_t B, const double* coeffs,
+                                const double* times, const SoftSpec& spec, double* maxima,
+                                double* cost, hipStream_t st);
 hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
                                 const double* coeffs, const double* times, double* max_time,
                                 double* max_value, int32_t* max_segment, int value_stride,
                                 int value_offset, const SoftCostArgs& soft, hipStream_t st,
                                 const MinOut* mino = nullptr);
+
+// Collision-driven objectives and their optimiser (mtg_coll_opt.hip); return
+// MTG_* codes.  All scratch comes from the caller's workspace.
+size_t coll_workspace_bytes(const PlanDev& pl, int64_t B, int mode, const mtg_coll_params& p,
+                            bool optimiser);
+int64_t coll_problems(const PlanDev& pl, int64_t B, int mode, const mtg_coll_params& p);
+int coll_cost(const PlanDev& pl, int64_t B, int mode, const double* df, const double* x,
+              const double* times, const float* occ, int nx, int ny, int nz,
+              const mtg_coll_params& p, const double* raise_ref, double* cost, double* grad,
+              double* terms, int32_t* collision, int32_t* status, void* workspace,
+              size_t workspace_bytes, hipStream_t st);
+int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, double* x_io,
+                  const double* times, const double* lower, const double* upper,
+                  const double* initial_step, const float* occ, int nx, int ny, int nz,
+                  const mtg_coll_params& p, int max_evals, double* cost, int32_t* evals,
+                  int32_t* result, int32_t* status, double* terms, void* workspace,
+                  size_t workspace_bytes, hipStream_t st);
 
 // Multi-GPU selection (mtg_select.hip).
 hipError_t launch_select_local(const double* costs, int64_t count, int64_t start, int rank,

@@ -2430,21 +2430,9 @@ double potentialAt(const CollMap& mp, const double pos[3], double grad[3], bool*
 }
 }  // namespace
 
-int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
-                       const double* vals, const double* times, const double* dp,
-                       const float* occupancy, int nx, int ny, int nz, const double* params,
-                       int box_side, double* cost, int* collision, double* grad_coeffs,
-                       double* grad_free) {
-  if (D != 3 || !params) return -1;
-  LinearProblem lp;
-  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
-  if (rc) return rc;
-  const int nf = lp.nf, np = lp.np, nall = nf + np;
-  if (np > 0 && !dp) return -1;
-  for (int d = 0; d < D; ++d)
-    for (int i = 0; i < np; ++i) lp.dp[d][i] = dp[d * np + i];
-  lp.updateSegmentsFromCompactConstraints();
-  // L = blockdiag(A_s^-1) M (n_all x (nf + np)).
+// L = blockdiag(A_s^-1) M (n_all x (nf + np)) at the problem's current times.
+static Mat mappingL(const LinearProblem& lp) {
+  const int S = lp.S, N = lp.N, nall = lp.nf + lp.np;
   Mat L(S * N, nall);
   for (int s = 0; s < S; ++s)
     for (int a = 0; a < N; ++a)
@@ -2453,14 +2441,28 @@ int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
         for (int b = 0; b < N; ++b) v += lp.Ainv[s](a, b) * lp.M(s * N + b, j);
         L(s * N + a, j) = v;
       }
-  const CollMap mp{occupancy, nx, ny, nz, params, box_side};
-  const double res = params[0], dt = params[10];
-  std::vector<double> gc(static_cast<size_t>(S) * D * N, 0.0), gf(static_cast<size_t>(D) * np, 0.0);
+  return L;
+}
+
+// The walk of getCostAndGradientCollision (nonlinear_impl:1609-1780) over
+// the problem's coefficients (lp.coeffs) sampled on the segment times `wt`
+// (getSegmentTimes, :1646-1647; the time objective's gradient walks the same
+// coefficients over perturbed times, :2532-2539).  With L the eq. (14)
+// gradient rows accumulate into gc (S x D x N) and gf (D x np).  On a
+// collision the walk stops with J_c = 0; the gradients keep what was
+// accumulated: the zeroing loop of :1773-1777 iterates over copies
+// (`for (Eigen::VectorXd gradients_k : *gradients)`), so it leaves the
+// reference's gradient unchanged.
+static double collisionWalk(const LinearProblem& lp, const Mat* L, const double* wt,
+                            const CollMap& mp, bool* is_coll_out, std::vector<double>* gc,
+                            std::vector<double>* gf) {
+  const int N = lp.N, D = lp.D, S = lp.S, nf = lp.nf, np = lp.np;
+  const double res = mp.prm[0], dt = mp.prm[10];
   double J = 0.0;
   bool is_coll = false;
   double prev[3] = {0, 0, 0}, time_sum = -1.0, dist_sum = 0.0, t = 0.0;
   for (int i = 0; i < S && !is_coll; ++i) {
-    for (t = 0.0; t < times[i]; t += dt) {
+    for (t = 0.0; t < wt[i]; t += dt) {
       double T[32], pos[3] = {0, 0, 0}, vel[3] = {0, 0, 0};
       for (int n = 0; n < N; ++n) T[n] = std::pow(t, n);
       for (int k = 0; k < D; ++k) {
@@ -2481,26 +2483,26 @@ int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
       if (dist_sum < res) continue;
       bool pc = false;
       double gpot[3] = {0, 0, 0};
-      const double c = potentialAt(mp, pos, gpot, &pc);
+      const double c = potentialAt(mp, pos, L ? gpot : nullptr, &pc);
       if (pc) {
         is_coll = true;
         break;
       }
       const double vn = std::sqrt(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
       J += c * vn * time_sum;
-      if (vn > 1e-6) {
+      if (L && vn > 1e-6) {
         // rows T_all L_pp and T_all V_all L_pp of eq. (14)
         std::vector<double> rT(np, 0.0), rV(np, 0.0);
         for (int p2 = 0; p2 < np; ++p2)
           for (int n = 0; n < N; ++n) {
-            rT[p2] += T[n] * L(i * N + n, nf + p2);
-            if (n + 1 < N) rV[p2] += T[n] * (n + 1) * L(i * N + n + 1, nf + p2);
+            rT[p2] += T[n] * (*L)(i * N + n, nf + p2);
+            if (n + 1 < N) rV[p2] += T[n] * (n + 1) * (*L)(i * N + n + 1, nf + p2);
           }
         for (int k = 0; k < D; ++k) {
           const double a = vn * time_sum * gpot[k], bc = time_sum * c * vel[k] / vn;
-          for (int p2 = 0; p2 < np; ++p2) gf[k * np + p2] += a * rT[p2] + bc * rV[p2];
+          for (int p2 = 0; p2 < np; ++p2) (*gf)[k * np + p2] += a * rT[p2] + bc * rV[p2];
           for (int n = 0; n < N; ++n)
-            gc[(static_cast<size_t>(i) * D + k) * N + n] +=
+            (*gc)[(static_cast<size_t>(i) * D + k) * N + n] +=
                 a * T[n] + bc * (n > 0 ? n * T[n - 1] : 0.0);
         }
       }
@@ -2508,17 +2510,420 @@ int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
       time_sum = 0.0;
     }
     if (is_coll) break;
-    time_sum += -dt + (times[i] - t);
+    time_sum += -dt + (wt[i] - t);
   }
-  if (is_coll) {
-    J = 0.0;
-    std::fill(gc.begin(), gc.end(), 0.0);
-    std::fill(gf.begin(), gf.end(), 0.0);
-  }
+  if (is_coll) J = 0.0;
+  *is_coll_out = is_coll;
+  return J;
+}
+
+int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
+                       const double* vals, const double* times, const double* dp,
+                       const float* occupancy, int nx, int ny, int nz, const double* params,
+                       int box_side, double* cost, int* collision, double* grad_coeffs,
+                       double* grad_free) {
+  if (D != 3 || !params) return -1;
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &lp);
+  if (rc) return rc;
+  const int np = lp.np;
+  if (np > 0 && !dp) return -1;
+  for (int d = 0; d < D; ++d)
+    for (int i = 0; i < np; ++i) lp.dp[d][i] = dp[d * np + i];
+  lp.updateSegmentsFromCompactConstraints();
+  const Mat L = mappingL(lp);
+  const CollMap mp{occupancy, nx, ny, nz, params, box_side};
+  std::vector<double> gc(static_cast<size_t>(S) * D * N, 0.0), gf(static_cast<size_t>(D) * np, 0.0);
+  bool is_coll = false;
+  const double J = collisionWalk(lp, &L, times, mp, &is_coll, &gc, &gf);
   if (cost) *cost = J;
   if (collision) *collision = is_coll ? 1 : 0;
   if (grad_coeffs) std::memcpy(grad_coeffs, gc.data(), sizeof(double) * gc.size());
   if (grad_free) std::memcpy(grad_free, gf.data(), sizeof(double) * gf.size());
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// Collision-driven objectives (the reference demo's path, src/main.cpp:77,
+// 104-105), restated step by step:
+//   mode 0  objectiveFunctionFreeConstraintsAndCollision (nonlinear_impl:
+//           1115-1272), x = d_p;
+//   mode 1  objectiveFunctionFreeConstraintsAndCollisionAndTime (:1274-1535),
+//           x = [T; d_p].
+// params (doubles): [0..10] the CollMap layout (res, min[3], max[3], epsilon,
+// robot_radius, coll_pot_multiplier, coll_check_time_increment), [11] w_d,
+// [12] w_c, [13] w_t, [14] w_sc, [15] add_coll_raise, [16] increment_time,
+// [17] soft_constraint_weight, [18] soft maximum_cost, [19] f_rel,
+// [20] f_abs, [21] x_rel, [22] x_abs.
+// iparams: [0] box side, [1] is_collision_safe, [2] is_coll_raise_first_iter,
+// [3] is_simple_numgrad_time, [4] is_simple_numgrad_constraints, [5] n_soft,
+// [6] L-BFGS memory.
+namespace {
+struct CollObjective {
+  LinearProblem lp;
+  CollMap mp;
+  const double* prm;
+  const int* ip;
+  SoftSpec soft;
+  int mode = 0;
+  double Jref0 = 0.0;  // total_cost_iter0_{}
+  double Jlast = 0.0;  // optimization_info_ totals of the previous evaluation
+  bool iter0 = true;
+
+  double softCost() const {
+    double c = 0.0;
+    orc_soft_constraint_cost(lp.N, lp.D, lp.S, lp.coeffs.data(), lp.times.data(), soft.n,
+                             soft.derivatives, soft.limits, soft.weight, soft.maximum_cost,
+                             nullptr, &c);
+    return c;
+  }
+  void setFree(const std::vector<double>& dp) {
+    for (int d = 0; d < lp.D; ++d)
+      for (int i = 0; i < lp.np; ++i) lp.dp[d][i] = dp[d * lp.np + i];
+    lp.updateSegmentsFromCompactConstraints();
+  }
+
+  // The objective at x; grad (nullable) of length nv; terms[4] = w_d J_d,
+  // w_c J_c (raised), w_t J_t, w_sc J_sc.  Returns NaN (no state change)
+  // for a non-positive segment time.
+  double eval(const std::vector<double>& x, double* grad, double* terms, int* collision) {
+    const int S = lp.S, D = lp.D, np = lp.np, nfr = D * np, off = mode ? S : 0;
+    const double h = prm[0], inc = prm[16];
+    const double w_d = prm[11], w_c = prm[12], w_t = prm[13], w_sc = prm[14];
+    if (mode == 1) {  // updateSegmentTimes (:1309)
+      std::vector<double> T(x.begin(), x.begin() + S);
+      for (double t : T)
+        if (!(t > 0.0)) return std::numeric_limits<double>::quiet_NaN();
+      lp.updateSegmentTimes(T);
+    }
+    std::vector<double> dp(x.begin() + off, x.end());
+    setFree(dp);  // setFreeConstraints (:1143, 1310)
+    const Mat L = mappingL(lp);  // L_ = A^-1 M (:539, 1313-1316)
+    std::vector<double> gc(static_cast<size_t>(S) * D * lp.N, 0.0), gf(nfr, 0.0),
+        gd(nfr, 0.0), gsc(nfr, 0.0), gt(S, 0.0);
+    bool coll = false;
+    const double Jc = collisionWalk(lp, grad ? &L : nullptr, lp.times.data(), mp, &coll, &gc, &gf);
+    double Jd = 0.0, Jsc = 0.0, Jt = 0.0;
+    if (!coll) {
+      // getCostAndGradientDerivative (:1537-1606).
+      Jd = lp.costDerivativeJd();
+      if (grad) {
+        const Mat R = lp.constructR();
+        const int nf = lp.nf;
+        for (int d = 0; d < D; ++d)
+          for (int i = 0; i < np; ++i) {
+            double a = 0.0, b = 0.0;
+            for (int j = 0; j < nf; ++j) a += lp.df[d][j] * R(nf + i, j);
+            for (int j = 0; j < np; ++j) b += lp.dp[d][j] * R(nf + j, nf + i);
+            gd[d * np + i] = 2.0 * a + 2.0 * b;
+          }
+      }
+      if (soft.n > 0) {
+        const bool simple = mode == 1 && ip[4];
+        if (simple) {  // getCostAndGradientSoftConstraintsSimple (:2434-2493)
+          Jsc = softCost();
+          if (grad) {
+            for (int i = 0; i < nfr; ++i) {
+              std::vector<double> right = dp;
+              right[i] = dp[i] + h;
+              setFree(right);
+              gsc[i] = (softCost() - Jsc) / h;
+            }
+            setFree(dp);
+          }
+        } else {  // getCostAndGradientSoftConstraints (:2365-2432)
+          if (grad) {
+            for (int i = 0; i < nfr; ++i) {
+              std::vector<double> left = dp, right = dp;
+              left[i] = dp[i] - h;
+              right[i] = dp[i] + h;
+              setFree(left);
+              const double cl = softCost();
+              setFree(right);
+              const double cr = softCost();
+              gsc[i] = (cr - cl) / (2.0 * h);
+            }
+            setFree(dp);
+          }
+          Jsc = softCost();
+        }
+      }
+      if (mode == 1) {
+        // getCostAndGradientTime(Simple) (:2495-2584, 2586-2657): T_n moved
+        // with d held; J_d at the new R, J_c walks the coefficients of T
+        // (L_ is not refreshed) over the new times, J_sc reads the segments
+        // that updateSegmentTimes leaves unchanged.
+        const std::vector<double> T = lp.times;
+        const std::vector<double> coeffs = lp.coeffs;
+        const bool simple_t = ip[3] != 0;
+        auto terms_at = [&](const std::vector<double>& t, double* jd, double* jc, double* jsc) {
+          lp.updateSegmentTimes(t);
+          *jd = lp.costDerivativeJd();
+          bool c2 = false;
+          std::vector<double> dummy_c, dummy_f;
+          *jc = collisionWalk(lp, nullptr, t.data(), mp, &c2, &dummy_c, &dummy_f);
+          // computeMaximumOfMagnitude reads the segments (coefficients and
+          // their own times), which updateSegmentTimes leaves at T.
+          *jsc = Jsc;
+        };
+        if (grad) {
+          for (int n = 0; n < S; ++n) {
+            std::vector<double> big = T;
+            big[n] = T[n] <= 0.1 ? 0.1 : T[n] + inc;
+            double jd_b, jc_b, jsc_b;
+            terms_at(big, &jd_b, &jc_b, &jsc_b);
+            double jd_s = Jd, jc_s = Jc, jsc_s = Jsc, den = inc;
+            if (!simple_t) {
+              std::vector<double> small = T;
+              small[n] = T[n] <= 0.1 ? 0.1 : T[n] - inc;
+              terms_at(small, &jd_s, &jc_s, &jsc_s);
+              den = 2.0 * inc;
+            }
+            gt[n] = w_d * ((jd_b - jd_s) / den) + w_c * ((jc_b - jc_s) / den) +
+                    w_sc * ((jsc_b - jsc_s) / den) + w_t * 1.0;
+          }
+          lp.updateSegmentTimes(T);
+          lp.coeffs = coeffs;
+        }
+        Jt = 0.0;
+        for (double t : T) Jt += t;
+      }
+    }
+    const double ct = w_d * Jd, ctm = w_t * Jt, csc = w_sc * Jsc;
+    double cc = w_c * Jc;
+    const double total = ct + cc + ctm + csc;
+    if (ip[1] && coll) {  // is_collision_safe (:1207-1226, 1432-1452)
+      const double ref = ip[2] ? Jref0 : Jlast;
+      cc = ref - (total - cc) + prm[15];
+    }
+    const double J = ct + cc + ctm + csc;
+    if (iter0) {
+      Jref0 = J;
+      iter0 = false;
+    }
+    Jlast = J;
+    if (terms) {
+      terms[0] = ct;
+      terms[1] = cc;
+      terms[2] = ctm;
+      terms[3] = csc;
+    }
+    if (collision) *collision = coll ? 1 : 0;
+    if (grad) {
+      for (int n = 0; n < off; ++n) grad[n] = gt[n];
+      for (int i = 0; i < nfr; ++i) grad[off + i] = w_d * gd[i] + w_c * gf[i] + w_sc * gsc[i];
+    }
+    return J;
+  }
+};
+
+int setupCollObjective(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                       const double* times, int mode, const float* occ, int nx, int ny, int nz,
+                       const double* params, const int* iparams, const int* soft_derivatives,
+                       const double* soft_limits, CollObjective* o) {
+  if (D != 3 || !params || !iparams || (mode != 0 && mode != 1)) return -1;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times, &o->lp);
+  if (rc) return rc;
+  if (o->lp.np < 1) return -1;
+  o->mp = CollMap{occ, nx, ny, nz, params, iparams[0]};
+  o->prm = params;
+  o->ip = iparams;
+  o->mode = mode;
+  o->soft = SoftSpec{iparams[5], soft_derivatives, soft_limits, params[17], params[18]};
+  return 0;
+}
+
+// NLopt's relstop (util/stop.c).
+bool relstopOracle(double vold, double vnew, double reltol, double abstol) {
+  if (vold == vnew) return true;
+  const double d = std::fabs(vnew - vold);
+  return d < abstol || d < reltol * (std::fabs(vnew) + std::fabs(vold)) * 0.5;
+}
+}  // namespace
+
+int orc_coll_cost(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                  const double* times, int mode, const double* x, const float* occupancy, int nx,
+                  int ny, int nz, const double* params, const int* iparams,
+                  const int* soft_derivatives, const double* soft_limits, double raise_ref,
+                  double* cost, double* grad, double* terms, int* collision) {
+  CollObjective o;
+  int rc = setupCollObjective(N, D, r, S, K, mask, vals, times, mode, occupancy, nx, ny, nz,
+                              params, iparams, soft_derivatives, soft_limits, &o);
+  if (rc) return rc;
+  if (!x) return -1;
+  const int nv = (mode ? S : 0) + D * o.lp.np;
+  o.Jref0 = o.Jlast = raise_ref;
+  const std::vector<double> xv(x, x + nv);
+  const double J = o.eval(xv, grad, terms, collision);
+  if (cost) *cost = J;
+  return 0;
+}
+
+// The mtg_coll_optimize algorithm restated: projected L-BFGS with Armijo
+// backtracking by safeguarded quadratic interpolation, every trial one
+// counted evaluation (NLopt maxeval), NLopt's ftol / xtol tests on accepted
+// steps; it stands in for NLopt's LD_LBFGS (absent; parity unpinned).
+int orc_coll_optimize(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                      const double* times, int mode, const float* occupancy, int nx, int ny,
+                      int nz, const double* params, const int* iparams,
+                      const int* soft_derivatives, const double* soft_limits,
+                      const double* lower, const double* upper, const double* initial_step,
+                      int max_evals, double* x_io, double* cost, int* evals, int* result,
+                      double* terms) {
+  CollObjective o;
+  int rc = setupCollObjective(N, D, r, S, K, mask, vals, times, mode, occupancy, nx, ny, nz,
+                              params, iparams, soft_derivatives, soft_limits, &o);
+  if (rc) return rc;
+  if (!x_io || max_evals < 1) return -1;
+  const int nv = (mode ? S : 0) + D * o.lp.np;
+  const int m = iparams[6];
+  if (m < 1 || m > 16) return -1;
+  auto lo = [&](int i) { return lower ? lower[i] : -HUGE_VAL; };
+  auto hi = [&](int i) { return upper ? upper[i] : HUGE_VAL; };
+  std::vector<double> x(nv), g(nv), xt(nv), G(nv), d(nv);
+  double step0 = 0.0;
+  for (int i = 0; i < nv; ++i) {
+    x[i] = std::min(std::max(x_io[i], lo(i)), hi(i));
+    step0 = std::max(step0, std::fabs(initial_step ? initial_step[i] : 0.1 * std::fabs(x_io[i])));
+  }
+  std::vector<std::vector<double>> Sh(m, std::vector<double>(nv)), Yh = Sh;
+  std::vector<double> rho(m);
+  int cnt = 0, head = 0;
+  double best_terms[4] = {NAN, NAN, NAN, NAN}, tt[4];
+  auto held = [&](int i) {
+    return (x[i] <= lo(i) && g[i] > 0.0) || (x[i] >= hi(i) && g[i] < 0.0);
+  };
+  // Two-loop recursion on the free variables (see coll direction on the
+  // device); returns max |q|.
+  auto direction = [&](bool reset) {
+    if (reset) cnt = head = 0;
+    std::vector<double> q(nv);
+    double qmax = 0.0;
+    for (int i = 0; i < nv; ++i) {
+      q[i] = held(i) ? 0.0 : g[i];
+      qmax = std::max(qmax, std::fabs(q[i]));
+    }
+    if (!(qmax > 0.0)) return qmax;
+    std::vector<double> a(m);
+    for (int c = 0; c < cnt; ++c) {
+      const int k = (head - 1 - c + m) % m;
+      double sq = 0.0;
+      for (int i = 0; i < nv; ++i) sq += Sh[k][i] * q[i];
+      a[c] = rho[k] * sq;
+      for (int i = 0; i < nv; ++i) q[i] -= a[c] * Yh[k][i];
+    }
+    double gamma;
+    if (cnt > 0) {
+      const int k = (head - 1 + m) % m;
+      double sy = 0.0, yy = 0.0;
+      for (int i = 0; i < nv; ++i) {
+        sy += Sh[k][i] * Yh[k][i];
+        yy += Yh[k][i] * Yh[k][i];
+      }
+      gamma = sy / yy;
+    } else {
+      gamma = (step0 > 0.0 ? step0 : 1.0) / qmax;
+    }
+    for (int i = 0; i < nv; ++i) q[i] *= gamma;
+    for (int c = cnt - 1; c >= 0; --c) {
+      const int k = (head - 1 - c + m) % m;
+      double yr = 0.0;
+      for (int i = 0; i < nv; ++i) yr += Yh[k][i] * q[i];
+      const double beta = rho[k] * yr;
+      for (int i = 0; i < nv; ++i) q[i] += (a[c] - beta) * Sh[k][i];
+    }
+    double gp = 0.0;
+    for (int i = 0; i < nv; ++i) {
+      d[i] = held(i) ? 0.0 : -q[i];
+      gp += g[i] * d[i];
+    }
+    if (!(gp < 0.0)) {
+      cnt = head = 0;
+      const double g0 = (step0 > 0.0 ? step0 : 1.0) / qmax;
+      for (int i = 0; i < nv; ++i) d[i] = held(i) ? 0.0 : -g0 * g[i];
+    }
+    return qmax;
+  };
+  double f = o.eval(x, g.data(), tt, nullptr);
+  int n_eval = 1, res = 0;
+  double alpha = 1.0;
+  if (!std::isfinite(f)) {
+    res = -1;
+  } else {
+    std::copy(tt, tt + 4, best_terms);
+    if (!(direction(true) > 0.0)) res = 1;
+  }
+  while (res == 0) {
+    if (n_eval >= max_evals) {
+      res = 5;
+      break;
+    }
+    bool moved = false;
+    for (int i = 0; i < nv; ++i) {
+      xt[i] = std::min(std::max(x[i] + alpha * d[i], lo(i)), hi(i));
+      moved = moved || xt[i] != x[i];
+    }
+    if (!moved) {
+      res = 4;
+      break;
+    }
+    const double J = o.eval(xt, G.data(), tt, nullptr);
+    ++n_eval;
+    double dd = 0.0;
+    for (int i = 0; i < nv; ++i) dd += g[i] * (xt[i] - x[i]);
+    if (std::isfinite(J) && J < f && J <= f + 1e-4 * dd) {
+      double sy = 0.0, ss = 0.0, yy = 0.0;
+      bool xstop = true;
+      for (int i = 0; i < nv; ++i) {
+        const double s2 = xt[i] - x[i], y = G[i] - g[i];
+        sy += s2 * y;
+        ss += s2 * s2;
+        yy += y * y;
+        xstop = xstop && relstopOracle(x[i], xt[i], params[21], params[22]);
+      }
+      const bool fstop = relstopOracle(f, J, params[19], params[20]);
+      if (sy > 1e-12 * std::sqrt(ss * yy)) {
+        for (int i = 0; i < nv; ++i) {
+          Sh[head][i] = xt[i] - x[i];
+          Yh[head][i] = G[i] - g[i];
+        }
+        rho[head] = 1.0 / sy;
+        head = (head + 1) % m;
+        cnt = std::min(cnt + 1, m);
+      }
+      x = xt;
+      g = G;
+      f = J;
+      std::copy(tt, tt + 4, best_terms);
+      if (fstop) {
+        res = 3;
+      } else if (xstop) {
+        res = 4;
+      } else {
+        if (!(direction(false) > 0.0)) res = 1;
+        alpha = 1.0;
+      }
+    } else {
+      double an = 0.5 * alpha;
+      const double den = 2.0 * (J - f - dd);
+      if (std::isfinite(J) && den > 0.0)
+        an = std::min(std::max(-dd * alpha / den, 0.1 * alpha), 0.5 * alpha);
+      alpha = an;
+      if (alpha < 1e-10) {
+        if (cnt > 0) {
+          if (!(direction(true) > 0.0)) res = 1;
+          alpha = 1.0;
+        } else {
+          res = 4;
+        }
+      }
+    }
+  }
+  if (std::isfinite(f)) std::copy(x.begin(), x.end(), x_io);
+  if (cost) *cost = f;
+  if (evals) *evals = n_eval;
+  if (result) *result = res;
+  if (terms) std::copy(best_terms, best_terms + 4, terms);
   return 0;
 }
 

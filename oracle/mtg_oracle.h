@@ -271,6 +271,27 @@ int orc_collision_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
                        int box_side, double* cost, int* collision, double* grad_coeffs,
                        double* grad_free);
 
+// Collision-driven objectives of the reference demo (mtg_coll_cost /
+// mtg_coll_optimize; see mtg_oracle.cpp for the params / iparams layout):
+// mode 0 objectiveFunctionFreeConstraintsAndCollision (nonlinear_impl:
+// 1115-1272), x = d_p (D x np); mode 1 ...AndCollisionAndTime (:1274-1535),
+// x = [T; d_p].  times: setup times (mode 0: the segment times).
+// raise_ref: total_cost_iter0_ / last total for the collision raise rule.
+// grad: nv, terms: 4 (nullable).
+int orc_coll_cost(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                  const double* times, int mode, const double* x, const float* occupancy, int nx,
+                  int ny, int nz, const double* params, const int* iparams,
+                  const int* soft_derivatives, const double* soft_limits, double raise_ref,
+                  double* cost, double* grad, double* terms, int* collision);
+// The mtg_coll_optimize algorithm (projected L-BFGS) on that objective.
+int orc_coll_optimize(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                      const double* times, int mode, const float* occupancy, int nx, int ny,
+                      int nz, const double* params, const int* iparams,
+                      const int* soft_derivatives, const double* soft_limits,
+                      const double* lower, const double* upper, const double* initial_step,
+                      int max_evals, double* x_io, double* cost, int* evals, int* result,
+                      double* terms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -528,3 +528,93 @@ def collision_cost(N, r, vertices, times, dp, occupancy, params, box_side=20):
                                 _d(prm), box_side, _d(cost), ctypes.byref(coll), _d(gc), _d(gf)),
            "collision_cost")
     return float(cost[0]), coll.value, gc, gf
+
+
+# Defaults of NonlinearOptimizationParameters for the collision objectives
+# (polynomial_optimization_nonlinear.h:46-84), the same keys as the product's
+# COLL_DEFAULTS.
+COLL_DEFAULTS = dict(map_resolution=0.0, min_bound=(0.0, 0.0, 0.0), max_bound=(0.0, 0.0, 0.0),
+                     epsilon=0.5, robot_radius=0.5, coll_pot_multiplier=1.0,
+                     coll_check_time_increment=0.1, box_side=20, w_d=0.1, w_c=10.0, w_t=1.0,
+                     w_sc=1.0, is_collision_safe=True, is_coll_raise_first_iter=True,
+                     add_coll_raise=0.0, simple_numgrad_time=False,
+                     simple_numgrad_constraints=False, increment_time=0.1, soft=(),
+                     soft_weight=100.0, soft_maximum_cost=1.0e12, f_rel=0.05, f_abs=-1.0,
+                     x_rel=-1.0, x_abs=-1.0, lbfgs_memory=10)
+
+
+def _coll_arrays(params):
+    d = dict(COLL_DEFAULTS, **params)
+    prm = np.array([d["map_resolution"], *d["min_bound"], *d["max_bound"], d["epsilon"],
+                    d["robot_radius"], d["coll_pot_multiplier"], d["coll_check_time_increment"],
+                    d["w_d"], d["w_c"], d["w_t"], d["w_sc"], d["add_coll_raise"],
+                    d["increment_time"], d["soft_weight"], d["soft_maximum_cost"], d["f_rel"],
+                    d["f_abs"], d["x_rel"], d["x_abs"]], dtype=np.float64)
+    soft = list(d["soft"] or [])
+    ip = np.array([d["box_side"], int(d["is_collision_safe"]), int(d["is_coll_raise_first_iter"]),
+                   int(d["simple_numgrad_time"]), int(d["simple_numgrad_constraints"]), len(soft),
+                   d["lbfgs_memory"]], dtype=np.int32)
+    der = np.array([s[0] for s in soft] + [0], dtype=np.int32)
+    lim = np.array([s[1] for s in soft] + [1.0], dtype=np.float64)
+    return prm, ip, der, lim
+
+
+_COLL_COMMON = [ctypes.c_int] * 5 + [_u8p, _dp, _dp, ctypes.c_int]
+
+
+def coll_cost(N, r, vertices, times, mode, x, occupancy, params, raise_ref=0.0):
+    """orc_coll_cost: objectiveFunctionFreeConstraintsAndCollision (mode 0,
+    x = d_p flattened D x np) / ...AndCollisionAndTime (mode 1, x = [T; d_p])
+    on a dense grid.  Returns (J, grad [nv], terms [4], collision)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    occ = np.ascontiguousarray(occupancy, dtype=np.float32)
+    nz, ny, nx = occ.shape
+    prm, ip, der, lim = _coll_arrays(params)
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    cost = np.zeros(1)
+    grad = np.zeros(x.size)
+    terms = np.zeros(4)
+    coll = ctypes.c_int()
+    L = lib()
+    L.orc_coll_cost.argtypes = _COLL_COMMON + [
+        _dp, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _ip,
+        _ip, _dp, ctypes.c_double, _dp, _dp, _dp, ctypes.POINTER(ctypes.c_int)]
+    _check(L.orc_coll_cost(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p), _d(vertices.vals),
+                           _d(times), mode, _d(x),
+                           occ.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), nx, ny, nz,
+                           _d(prm), ip.ctypes.data_as(_ip), der.ctypes.data_as(_ip), _d(lim),
+                           float(raise_ref), _d(cost), _d(grad), _d(terms), ctypes.byref(coll)),
+           "coll_cost")
+    return float(cost[0]), grad, terms, coll.value
+
+
+def coll_optimize(N, r, vertices, times, mode, x0, occupancy, params, max_evals, lower=None,
+                  upper=None, initial_step=None):
+    """orc_coll_optimize: the mtg_coll_optimize algorithm (projected L-BFGS)
+    on the collision objective.  Returns (x, J, evals, result, terms)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    occ = np.ascontiguousarray(occupancy, dtype=np.float32)
+    nz, ny, nx = occ.shape
+    prm, ip, der, lim = _coll_arrays(params)
+    x = np.array(x0, dtype=np.float64).reshape(-1)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    opt = [None if a is None else np.ascontiguousarray(a, dtype=np.float64).reshape(-1)
+           for a in (lower, upper, initial_step)]
+    cost = np.zeros(1)
+    terms = np.zeros(4)
+    ev, res = ctypes.c_int(), ctypes.c_int()
+    L = lib()
+    L.orc_coll_optimize.argtypes = _COLL_COMMON + [
+        ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _ip, _ip,
+        _dp, _dp, _dp, _dp, ctypes.c_int, _dp, _dp, ctypes.POINTER(ctypes.c_int),
+        ctypes.POINTER(ctypes.c_int), _dp]
+    _check(L.orc_coll_optimize(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                               _d(vertices.vals), _d(times), mode,
+                               occ.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), nx, ny, nz,
+                               _d(prm), ip.ctypes.data_as(_ip), der.ctypes.data_as(_ip),
+                               _d(lim), *[None if a is None else _d(a) for a in opt],
+                               max_evals, _d(x), _d(cost), ctypes.byref(ev), ctypes.byref(res),
+                               _d(terms)),
+           "coll_optimize")
+    return x, float(cost[0]), ev.value, res.value, terms

@@ -700,6 +700,15 @@ TEST(gpu, SoftConstraintTimeCost) {
   // the objective has no soft term, a feasible start stays feasible.
   NonlinearOptimizationParameters hard = p;
   hard.use_soft_constraints = false;
+  {
+    // With the default LN_SBPLX the inequality is refused, as NLopt's
+    // add_inequality_constraint throws (nonlinear_impl:862-872).
+    PolynomialOptimizationNonLinear<10> sbplx(f.D, hard);
+    sbplx.setupFromVertices(vs, times,
+                            std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}), 4);
+    EXPECT_TRUE(!sbplx.addMaximumMagnitudeConstraint(derivative_order::VELOCITY, 1.0));
+  }
+  hard.algorithm = nlopt::LN_COBYLA;  // takes inequality constraints
   PolynomialOptimizationNonLinear<10> opt2(f.D, hard);
   opt2.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}),
                          4);
@@ -1028,6 +1037,164 @@ TEST(gpu, OptimizeTimeAndFreeConstraints) {
   EXPECT_TRUE(oev == info.n_iterations);
   EXPECT_LE(relErr(J1, oJ), 1e-6);
   EXPECT_LE(relErr(t1, ot), 1e-6);
+}
+
+// The reference demo (src/main.cpp:15-126): kOptimizeFreeConstraintsAndCollision
+// with LD_LBFGS and main.cpp's parameters, here over a synthetic forest (the
+// demo's supereight map is a private file, main.cpp:17-19).  optimize() runs
+// mtg_coll_optimize (device L-BFGS in place of NLopt): it lowers the objective
+// from the QCQP start and takes the same steps as the oracle port; likewise
+// the time variant kOptimizeFreeConstraintsAndCollisionAndTime.
+std::vector<float> demoForest(int* nx, int* ny, int* nz) {
+  *nx = 120;
+  *ny = 120;
+  *nz = 90;
+  const double res = 0.1, r = 0.25;
+  const double trees[][2] = {{3.73, 6.57}, {4.28, 3.60}, {6.74, 2.78}, {8.5, 8.5},
+                             {9.5, 4.0},   {6.0, 9.0},   {2.0, 2.5}};
+  std::vector<float> occ(static_cast<size_t>(*nx) * *ny * *nz, -1.0f);
+  for (int z = 0; z < *nz; ++z)
+    for (int y = 0; y < *ny; ++y)
+      for (int x = 0; x < *nx; ++x)
+        for (const auto& c : trees) {
+          const double dx = (x + 0.5) * res - c[0], dy = (y + 0.5) * res - c[1];
+          if (dx * dx + dy * dy <= r * r) occ[(static_cast<size_t>(z) * *ny + y) * *nx + x] = 1.0f;
+        }
+  return occ;
+}
+
+NonlinearOptimizationParameters demoParameters() {  // main.cpp:75-110
+  NonlinearOptimizationParameters p;
+  p.solve_with_position_constraint = true;
+  p.objective = NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndCollision;
+  p.print_debug_info = false;
+  p.max_iterations = 25;
+  p.max_time = -1;
+  p.f_rel = 0.000001;
+  p.x_rel = 0.01;
+  p.use_soft_constraints = false;
+  p.soft_constraint_weight = 100.0;
+  p.time_penalty = 500.0;
+  p.initial_stepsize_rel = 0.1;
+  p.inequality_constraint_tolerance = 0.1;
+  p.weights.w_d = 50;
+  p.weights.w_c = 50;
+  p.weights.w_t = 0.1;
+  p.weights.w_sc = 1.0;
+  p.use_numeric_grad = false;
+  p.use_continous_distance = false;
+  p.increment_time = 0.000001;
+  p.epsilon = 0.3;
+  p.coll_pot_multiplier = 20.0;
+  p.is_collision_safe = true;
+  p.is_simple_numgrad_time = true;
+  p.is_simple_numgrad_constraints = true;
+  p.coll_check_time_increment = 0.1;
+  p.is_coll_raise_first_iter = true;
+  p.robot_radius = 0.15;
+  p.add_coll_raise = 0.0000001;
+  p.algorithm = static_cast<nlopt::algorithm>(11);
+  p.random_seed = 12345678;
+  p.map_resolution = 0.1;
+  VectorXd lo(3), hi(3);
+  lo[0] = 1.4; lo[1] = 1.4; lo[2] = 3.9;
+  hi[0] = 11.3; hi[1] = 11.3; hi[2] = 8.8;
+  p.min_bound = lo;
+  p.max_bound = hi;
+  p.side = 5;
+  return p;
+}
+
+TEST(gpu, DemoCollisionObjective) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> times = estimateSegmentTimesNfabian(vs, 2.0, 2.0, 6.5);
+  const std::vector<std::pair<double, double>> radii(4, {0.15, 0.15});
+  int nx, ny, nz;
+  const std::vector<float> occ = demoForest(&nx, &ny, &nz);
+  Dense d = toDense(vs, 5);
+  for (int v = 1; v < d.S; ++v)
+    for (int k = 0; k < 5; ++k) d.mask[v * 5 + k] = 0;
+  for (int with_time = 0; with_time < 2; ++with_time) {
+    NonlinearOptimizationParameters p = demoParameters();
+    if (with_time)
+      p.objective = NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndCollisionAndTime;
+    PolynomialOptimizationNonLinear<10> opt(3, p);
+    opt.setOctree(nullptr);  // source compatibility: the map comes from setOccupancyGrid
+    EXPECT_TRUE(opt.setupFromVertices(vs, times, radii, 4));
+    opt.setOccupancyGrid(occ, nx, ny, nz);
+    // The start the optimiser uses: the tube QCQP (main.cpp sets
+    // solve_with_position_constraint).
+    PolynomialOptimizationConstrained<10> qp(3);
+    qp.setupFromVertices(vs, times, radii, 4);
+    EXPECT_TRUE(qp.solveQCQP() == 0);
+    std::vector<VectorXd> fc;
+    qp.getFreeConstraints(&fc);
+    std::vector<double> x0;
+    if (with_time) x0 = times;
+    for (const VectorXd& v : fc)
+      for (long i = 0; i < v.size(); ++i) x0.push_back(v[i]);
+    const double prm[23] = {0.1, 1.4, 1.4, 3.9, 11.3, 11.3, 8.8, 0.3, 0.15, 20.0, 0.1,
+                            50.0, 50.0, 0.1, 1.0, 1e-7, 1e-6, 100.0, 1e12, 1e-6, -1.0, 0.01,
+                            -1.0};
+    const int ip[7] = {20, 1, 1, 1, 1, 0, 10};
+    double J0 = 0.0;
+    int c0 = 1;
+    EXPECT_TRUE(orc_coll_cost(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), times.data(),
+                              with_time, x0.data(), occ.data(), nx, ny, nz, prm, ip, nullptr,
+                              nullptr, 0.0, &J0, nullptr, nullptr, &c0) == 0);
+    EXPECT_TRUE(c0 == 0);
+    const int res = opt.optimize();
+    EXPECT_TRUE(res == nlopt::FTOL_REACHED || res == nlopt::XTOL_REACHED ||
+                res == nlopt::MAXEVAL_REACHED || res == nlopt::SUCCESS);
+    const OptimizationInfo info = opt.getOptimizationInfo();
+    const double J1 = info.cost_trajectory + info.cost_collision + info.cost_time +
+                      info.cost_soft_constraints;
+    EXPECT_TRUE(J1 < J0);
+    EXPECT_TRUE(info.n_iterations >= 2 && info.n_iterations <= 25);
+    if (with_time) {
+      // main.cpp's increment_time = 1e-6: the reference's forward difference
+      // of J_d over it is rounding noise (~1e-4 relative), so the port's path
+      // parts from the device's; descent and the T >= 0.1 bounds only.
+      std::vector<double> t1;
+      opt.getConstrainedOptimizationRef().getSegmentTimes(&t1);
+      for (double ti : t1) EXPECT_TRUE(ti >= 0.1);
+      std::printf("  collision+time: J %.6g -> %.6g in %d evaluations (result %d)\n", J0, J1,
+                  info.n_iterations, res);
+      continue;
+    }
+    // Oracle port from the same start with the reference's bounds and steps.
+    const size_t nv = x0.size();
+    std::vector<double> lo(nv, -HUGE_VAL), hi(nv, HUGE_VAL), step(nv), ox = x0;
+    for (size_t i = 0; i < nv; ++i) {
+      const double a = std::fabs(x0[i]);
+      step[i] = (!with_time && a > 5) ? p.initial_stepsize_position : 0.1 * a;
+      if (with_time && i < 4) lo[i] = 0.1;
+    }
+    double oJ = 0.0, oterms[4];
+    int oev = 0, ores = 0;
+    EXPECT_TRUE(orc_coll_optimize(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), times.data(),
+                                  with_time, occ.data(), nx, ny, nz, prm, ip, nullptr, nullptr,
+                                  lo.data(), hi.data(), step.data(), 25, ox.data(), &oJ, &oev,
+                                  &ores, oterms) == 0);
+    EXPECT_TRUE(oev == info.n_iterations);
+    EXPECT_TRUE(ores == res);
+    EXPECT_LE(relErr(J1, oJ), 1e-6);
+    std::vector<VectorXd> f1;
+    opt.getConstrainedOptimizationRef().getFreeConstraints(&f1);
+    std::vector<double> x1;
+    if (with_time) opt.getConstrainedOptimizationRef().getSegmentTimes(&x1);
+    for (const VectorXd& v : f1)
+      for (long i = 0; i < v.size(); ++i) x1.push_back(v[i]);
+    EXPECT_LE(relErr(x1, ox), 1e-6);
+    // The trajectory keeps the start / end constraints (makeStartOrEnd).
+    Trajectory traj;
+    opt.getTrajectory(&traj);
+    EXPECT_LE(std::fabs(traj.evaluate(0.0, 0)[0] - 2.7), 1e-8);
+    EXPECT_LE(std::fabs(traj.evaluate(traj.getMaxTime(), 0)[1] - 2.2), 1e-8);
+    std::printf("  %s: J %.6g -> %.6g in %d evaluations (result %d; oracle %.6g, %d)\n",
+                with_time ? "collision+time" : "collision", J0, J1, info.n_iterations, res, oJ,
+                oev);
+  }
 }
 
 int main(int argc, char** argv) {

@@ -1,0 +1,314 @@
+"""CPU tests that pin the oracle restatement of the collision-driven objectives
+(the reference demo's path, src/main.cpp:77, 104-105):
+objectiveFunctionFreeConstraintsAndCollision (nonlinear_impl:1115-1272) and
+...AndCollisionAndTime (:1274-1535) with getCostAndGradientCollision
+(:1609-1780), getCostAndGradientSoftConstraints(Simple) (:2365-2493) and
+getCostAndGradientTime(Simple) (:2495-2657).
+
+supereight and NLopt are absent: the map is a dense grid and
+the optimiser a projected L-BFGS, so parity with the reference's octree and
+LD_LBFGS is unpinned.  What is pinned here:
+  * the collision walk against an independent NumPy restatement written from
+    the reference's loop (sampling, distance-triggered evaluation, the voxel
+    box search, the potential and the eq. (14) gradient);
+  * the objective's composition: on an empty map it is w_d J_d (+ w_t sum T)
+    with J_d = 2 computeCost() and the gradients of the free-derivative and
+    time-allocation restatements (orc_free_cost, orc_time_cost grad_mode 1);
+  * the J_d gradient against central differences;
+  * the collision raise rule and the reference's partial gradient on a
+    collision;
+  * the soft-constraint gradient as the central difference of the soft cost.
+"""
+import numpy as np
+import pytest
+
+import numpy_ref
+from coll_fixture import (MAIN_RADII, D, M, N, R, coll_params, forest_map, main_problem)
+from helpers import rel_err
+
+
+def _walk_numpy(coeffs, times, occ, prm, side=20):
+    """getCostAndGradientCollision's walk (nonlinear_impl:1667-1759) with
+    getCostAndGradientPotentialOctree (:1782-1917) on a dense grid: returns
+    (J_c, collision, dJ_c/dc [S, 3, N])."""
+    res, dt = prm["map_resolution"], prm["coll_check_time_increment"]
+    mn, mx = np.array(prm["min_bound"]), np.array(prm["max_bound"])
+    eps, rad, mult = prm["epsilon"], prm["robot_radius"], prm["coll_pot_multiplier"]
+    nz, ny, nx = occ.shape
+    S = len(times)
+    gc = np.zeros((S, 3, N))
+
+    def potential(d):
+        d = d - rad
+        if d <= 0.0:
+            return mult * (-d) + 0.5 * eps, True
+        if d <= eps:
+            return 0.5 / eps * (d - eps) ** 2, False
+        return 0.0, False
+
+    def occupied_in_box(v):
+        lo = v - side // 2  # findOccupiedVoxels: voxels overlapping [lo, lo + side]
+        pts = []
+        a = np.maximum(lo - 1, 0)
+        b = np.minimum(lo + side, np.array([nx, ny, nz]) - 1)
+        if np.any(a > b):
+            return np.zeros((0, 3))
+        sub = occ[a[2]:b[2] + 1, a[1]:b[1] + 1, a[0]:b[0] + 1]
+        zz, yy, xx = np.nonzero(sub >= 0.0)
+        pts = np.stack([xx + a[0], yy + a[1], zz + a[2]], axis=1)
+        return pts.astype(float)
+
+    def dist(c, pts):
+        if len(pts) == 0:
+            return np.finfo(float).max * res
+        return np.min(np.sqrt(np.sum((pts - c) ** 2, axis=1))) * res
+
+    J, coll = 0.0, False
+    prev = np.zeros(3)
+    time_sum, dist_sum, t = -1.0, 0.0, 0.0
+    for i in range(S):
+        t = 0.0
+        while t < times[i]:
+            Tv = np.array([t ** n for n in range(N)])
+            pos = np.array([Tv @ coeffs[i, k] for k in range(3)])
+            vel = np.array([sum(Tv[n] * (n + 1) * coeffs[i, k, n + 1] for n in range(N - 1))
+                            for k in range(3)])
+            if time_sum < 0:
+                time_sum = 0.0
+                prev = pos
+                t += dt
+                continue
+            time_sum += dt
+            dist_sum += np.linalg.norm(pos - prev)
+            prev = pos
+            if dist_sum < res:
+                t += dt
+                continue
+            valid = not (np.any(pos < mn + res) or np.any(pos > mx - res))
+            v = np.trunc(pos / res).astype(int)
+            pts = occupied_in_box(v)
+            c, hit = potential(dist(v, pts) if valid else 0.0)
+            if hit:
+                coll = True
+                break
+            vn = np.linalg.norm(vel)
+            J += c * vn * time_sum
+            if vn > 1e-6:
+                gp = np.zeros(3)
+                for k in range(3):
+                    e = np.zeros(3, int)
+                    e[k] = 1
+                    left = potential(dist(v - e, pts) if valid else 0.0)[0]
+                    right = potential(dist(v + e, pts) if valid else 0.0)[0]
+                    gp[k] = (right - left) / (2.0 * res)
+                dT = np.array([n * t ** (n - 1) if n > 0 else 0.0 for n in range(N)])
+                for k in range(3):
+                    gc[i, k] += vn * time_sum * gp[k] * Tv + time_sum * c * vel[k] / vn * dT
+            dist_sum = 0.0
+            time_sum = 0.0
+            t += dt
+        if coll:
+            break
+        time_sum += -dt + (times[i] - t)
+    return (0.0 if coll else J), coll, gc
+
+
+def _free_grad_from_coeff_grad(gc, times, free_slots):
+    """dJ/dd_p = sum over the segments touching the free vertex derivative
+    of A_s^-1(T_s)[:, column] . dJ/dc_s (L = A^-1 M, :1650-1656)."""
+    out = np.zeros((3, len(free_slots)))
+    for p, (v, j) in enumerate(free_slots):
+        for h, s in ((0, v), (1, v - 1)):
+            if 0 <= s < len(times):
+                Ai = np.linalg.inv(numpy_ref.mapping_matrix(N, times[s]))
+                out[:, p] += gc[s] @ Ai[:, h * M + j]
+    return out
+
+
+def _free_slots(vt):
+    return [(v, k) for v in range(vt.S + 1) for k in range(M) if not vt.mask[v, k]]
+
+
+def test_collision_walk_matches_numpy_restatement(oracle):
+    """The oracle's collision cost and both gradients against the NumPy
+    restatement on the demo geometry over the synthetic forest, at the QCQP
+    start (potential non-zero, no collision) and at shifted paths that hit a
+    tree (collision: J_c = 0, gradient partial)."""
+    _, vt, t, x0 = main_problem()
+    occ = forest_map()
+    prm = dict(coll_params(), box_side=20)
+    np_ = vt.S - 1
+    outcomes = []
+    for shift in (0.0, 0.05, 0.3):
+        x = x0.copy().reshape(3, -1)
+        x[0, 0::M] += shift  # move the intermediate positions in x
+        x = x.reshape(-1)
+        J, c, gc, gf = oracle.collision_cost(N, R, vt, t, x.reshape(3, -1), occ, prm)
+        coeffs = _coeffs_of(vt, t, x)
+        Jn, cn, gcn = _walk_numpy(coeffs, t, occ, prm)
+        assert c == int(cn)
+        assert abs(J - Jn) <= 1e-9 * max(abs(Jn), 1e-12)
+        assert np.max(np.abs(gc - gcn)) <= 1e-8 * max(np.max(np.abs(gcn)), 1e-12)
+        gfn = _free_grad_from_coeff_grad(gcn, t, _free_slots(vt))
+        assert np.max(np.abs(gf - gfn)) <= 1e-6 * max(np.max(np.abs(gfn)), 1e-12)
+        outcomes.append((c, J))
+    assert outcomes[0][0] == 0 and outcomes[0][1] > 0.0  # potential felt, no collision
+    assert any(c for c, _ in outcomes)  # and a collision
+
+
+def _coeffs_of(vt, t, x):
+    """Segment coefficients c_s = A_s^-1 [d(s); d(s+1)] of the tube-pattern
+    problem at d_p = x (fixed values from the vertices, free ones from x in
+    (vertex, derivative) order per dimension), NumPy from the definition."""
+    S = vt.S
+    d = np.zeros((S + 1, M, 3))
+    free = np.asarray(x).reshape(3, -1)
+    p = 0
+    for v in range(S + 1):
+        for k in range(M):
+            if vt.mask[v, k]:
+                d[v, k] = vt.vals[v, k]
+            else:
+                d[v, k] = free[:, p]
+                p += 1
+    c = np.zeros((S, 3, N))
+    for s in range(S):
+        Ai = np.linalg.inv(numpy_ref.mapping_matrix(N, t[s]))
+        for k in range(3):
+            c[s, k] = Ai @ np.concatenate([d[s, :, k], d[s + 1, :, k]])
+    return c
+
+
+def _empty_map():
+    return np.full((4, 4, 4), -1.0, np.float32)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_objective_without_obstacles_is_the_derivative_cost(oracle, mode):
+    """No occupied voxel: J_c = 0, so J = w_d J_d (+ w_t sum T) and the
+    gradient is w_d dJ_d/dd_p (the free-derivative restatement) and, for the
+    times, w_d dJ_d/dT_n + w_t with d held (orc_time_cost grad_mode 1 at the
+    linear solution)."""
+    _, vt, t, x0 = main_problem()
+    prm = coll_params(min_bound=(-100.0,) * 3, max_bound=(100.0,) * 3, increment_time=0.1,
+                      simple_numgrad_time=False)
+    if mode == 0:
+        x = x0
+    else:
+        lin = oracle.linear_solve(N, R, vt, t)
+        x = np.concatenate([t, lin["dp"].reshape(-1)])
+    J, g, terms, c = oracle.coll_cost(N, R, vt, t, mode, x, _empty_map(), prm)
+    assert c == 0 and terms[1] == 0.0
+    dp = x[mode * vt.S:].reshape(3, -1)
+    Jd, gd = oracle.free_cost(N, R, vt, t, dp, mode=0)
+    assert rel_err(terms[0], prm["w_d"] * Jd) <= 1e-12
+    # Same R, summed in another order: agreement to the cancellation in R d
+    # (at the linear solution of mode 1 the gradient itself cancels to ~0, so
+    # the scale is the gradient at the QCQP start).
+    scale = prm["w_d"] * np.max(np.abs(oracle.free_cost(N, R, vt, t, x0.reshape(3, -1))[1]))
+    assert np.max(np.abs(g[mode * vt.S:] - prm["w_d"] * gd.reshape(-1))) <= 1e-8 * scale
+    if mode == 1:
+        assert rel_err(terms[2], prm["w_t"] * np.sum(t)) <= 1e-15
+        _, gt = oracle.time_cost(N, R, vt, t, grad_mode=1, w_d=prm["w_d"], w_t=prm["w_t"])
+        assert np.max(np.abs(g[:vt.S] - gt)) <= 1e-6 * np.max(np.abs(gt))
+
+
+def test_derivative_gradient_matches_central_differences(oracle):
+    """On an empty map the objective is the quadratic w_d d^T R d, so its
+    gradient equals central differences to rounding."""
+    _, vt, t, x0 = main_problem()
+    prm = coll_params(min_bound=(-100.0,) * 3, max_bound=(100.0,) * 3)
+    J, g, _, _ = oracle.coll_cost(N, R, vt, t, 0, x0, _empty_map(), prm)
+    for i in range(0, x0.size, 4):
+        h = 1e-4 * (1.0 + abs(x0[i]))
+        xp, xm = x0.copy(), x0.copy()
+        xp[i] += h
+        xm[i] -= h
+        Jp = oracle.coll_cost(N, R, vt, t, 0, xp, _empty_map(), prm)[0]
+        Jm = oracle.coll_cost(N, R, vt, t, 0, xm, _empty_map(), prm)[0]
+        fd = (Jp - Jm) / (2.0 * h)
+        assert abs(fd - g[i]) <= 1e-6 * max(abs(g[i]), 1e-3 * np.max(np.abs(g))), i
+
+
+@pytest.mark.parametrize("first_iter", [True, False])
+def test_collision_raise_rule(oracle, first_iter):
+    """A colliding point (a tree across the path): J_d, J_sc, J_t are not
+    evaluated, J = raise_ref + add_coll_raise (is_collision_safe), the time
+    gradient is zero and the derivative gradient is w_c times the collision
+    gradient the walk accumulated before the hit (the reference's zeroing at
+    nonlinear_impl:1773-1777 works on copies)."""
+    _, vt, t, x0 = main_problem()
+    occ = forest_map(near=((3.2, 7.0),))  # on the first segment
+    prm = coll_params(is_coll_raise_first_iter=first_iter, add_coll_raise=0.25)
+    for mode in (0, 1):
+        x = x0 if mode == 0 else np.concatenate([t, x0])
+        J, g, terms, c = oracle.coll_cost(N, R, vt, t, mode, x, occ, prm, raise_ref=7.5)
+        assert c == 1
+        assert J == 7.5 + 0.25
+        assert terms[0] == 0.0 and terms[2] == 0.0 and terms[3] == 0.0
+        Jc, cc, _, gf = oracle.collision_cost(N, R, vt, t, x0.reshape(3, -1), occ, prm)
+        assert cc == 1 and Jc == 0.0
+        assert np.all(g[:mode * vt.S] == 0.0)
+        assert np.allclose(g[mode * vt.S:], prm["w_c"] * gf.reshape(-1), rtol=1e-14, atol=0.0)
+
+
+def test_soft_gradient_is_the_central_difference_of_the_soft_cost(oracle):
+    """getCostAndGradientSoftConstraints (:2365-2432): dJ_sc/dd_p by central
+    differences with step map_resolution, recomputed here from the
+    free-derivative restatement's soft cost (orc_free_cost with and without
+    the constraints)."""
+    _, vt, t, x0 = main_problem()
+    lim = [(1, 1.0), (2, 1.5)]
+    prm = coll_params(min_bound=(-100.0,) * 3, max_bound=(100.0,) * 3, soft=lim,
+                      soft_weight=10.0)
+    J, g, terms, _ = oracle.coll_cost(N, R, vt, t, 0, x0, _empty_map(), prm)
+    Jd, gd = oracle.free_cost(N, R, vt, t, x0.reshape(3, -1), mode=0)
+    h = prm["map_resolution"]
+
+    def soft(x):
+        with_soft = oracle.free_cost(N, R, vt, t, x.reshape(3, -1), mode=0, soft=lim,
+                                     soft_weight=10.0)[0]
+        return with_soft - oracle.free_cost(N, R, vt, t, x.reshape(3, -1), mode=0)[0]
+
+    assert rel_err(terms[3], prm["w_sc"] * soft(x0)) <= 1e-9
+    for i in range(0, x0.size, 5):
+        xp, xm = x0.copy(), x0.copy()
+        xp[i] += h
+        xm[i] -= h
+        gsc = (soft(xp) - soft(xm)) / (2.0 * h)
+        want = prm["w_d"] * gd.reshape(-1)[i] + prm["w_sc"] * gsc
+        assert abs(g[i] - want) <= 1e-6 * max(abs(want), 1.0), i
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_lbfgs_port_descends_within_bounds(oracle, mode):
+    """The optimiser port (orc_coll_optimize, the mtg_coll_optimize
+    algorithm): J falls from the QCQP start on the forest, bounds hold, and at
+    most max_evals evaluations run."""
+    _, vt, t, x0 = main_problem()
+    occ = forest_map()
+    prm = coll_params()
+    x = x0 if mode == 0 else np.concatenate([t, x0])
+    lo = np.full(x.size, -np.inf)
+    if mode == 1:
+        lo[:vt.S] = 0.1
+    J0 = oracle.coll_cost(N, R, vt, t, mode, x, occ, prm)[0]
+    xo, Jo, ev, res, terms = oracle.coll_optimize(N, R, vt, t, mode, x, occ, prm, 25, lower=lo)
+    assert Jo < 0.6 * J0
+    assert 1 <= ev <= 25 and res in (1, 3, 4, 5)
+    assert np.all(xo >= lo)
+    assert rel_err(np.sum(terms), Jo) <= 1e-12
+    Jchk = oracle.coll_cost(N, R, vt, t, mode, xo, occ, prm)[0]
+    assert rel_err(Jchk, Jo) <= 1e-12
+
+
+def test_main_problem_fixture(oracle):
+    """The demo's QCQP start satisfies its tube (radius 0.15) and the map
+    leaves it collision-free with a non-zero potential."""
+    v, vt, t, x0 = main_problem()
+    res = oracle.tube_residuals(N, R, v, t, MAIN_RADII, x0)
+    assert np.max(res) <= 1e-8
+    J, c, _, _ = oracle.collision_cost(N, R, vt, t, x0.reshape(3, -1), forest_map(),
+                                       coll_params())
+    assert c == 0 and J > 0.0
+    assert D == 3
