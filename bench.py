@@ -50,7 +50,7 @@ def parse():
                    help="linear: include the device selection step (RCCL all-gather + argmin, "
                         "always on at --gpus > 1) also on one GPU")
     p.add_argument("--kernel", default="auto",
-                   choices=["auto", "generic", "standard", "lane"],
+                   choices=["auto", "generic", "standard", "lane", "lane_pair"],
                    help="linear-solve kernel (mtg_plan_set_kernel); auto picks by batch size")
     p.add_argument("--soft", action="store_true",
                    help="time workload: soft constraints max|v| <= 3, max|a| <= 5 in the objective")
@@ -298,11 +298,28 @@ def main():
 
     if wl == "linear":
         out = plan.solve(fixed_d, times_d, free=False)
+        shard_start = shard_range(global_batch, world, rank)[0]
+        sel_ws = plan.select_workspace(B, dev)
+        sel_res = torch.empty(3, dtype=torch.float64, device=dev)
+
+        def step_selected():
+            # The solve with the shard's argmin fused into its launch, then
+            # (world > 1) the RCCL all-gather of the triples and the global
+            # argmin kernel; on one GPU without a process group the all-gather
+            # of one triple is the identity and only the global kernel runs.
+            plan.solve_select(fixed_d, times_d, shard_start, rank, sel_ws, out=out)
+            if select:
+                return select_best_device(None, global_batch, local_triple=out["triple"])
+            from mav_tube_trajectory_generation_amd._abi import check as _chk, lib as _lib
+            from mav_tube_trajectory_generation_amd.batch import _ptr, _stream
+            _chk(_lib().mtg_select_global(_ptr(out["triple"]), 1, _ptr(sel_res), _stream(dev)),
+                 "mtg_select_global")
+            return sel_res
 
         def step():
+            if select:
+                return step_selected()
             plan.solve(fixed_d, times_d, free=False, out=out)
-            if select:  # local argmin kernel, RCCL all-gather, global argmin kernel
-                return select_best_device(out["cost"], global_batch)
             return None
 
         bytes_per_traj = (D * nf + S) * 8 + (S * D * N + 1) * 8 + 4  # + status
@@ -507,6 +524,32 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # One GPU: also time the selection-inclusive step (the step every rank runs
+    # at --gpus > 1, minus the all-gather), so the scaling curve's N = 1 and
+    # N > 1 points can be compared step for step.
+    selection_ms = None
+    if wl == "linear" and not select:
+        for _ in range(3):
+            step_selected()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        try:
+            gs = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gs):
+                for _ in range(args.steps):
+                    step_selected()
+            e0.record(stream)
+            gs.replay()
+            e1.record(stream)
+        except Exception:  # eager fallback
+            torch.cuda.synchronize(dev)
+            e0.record(stream)
+            for _ in range(args.steps):
+                step_selected()
+            e1.record(stream)
+        torch.cuda.synchronize(dev)
+        selection_ms = e0.elapsed_time(e1) / args.steps
+
     counted = useful_per_step if useful_per_step is not None else units_per_step
     total_units = counted * args.steps * world
     value = total_units / elapsed
@@ -530,8 +573,9 @@ def main():
     roof["kernel_ms"] = kernel_ms
     roof["kernel_timing"] = timing
     if select and wl == "linear":
-        roof["kernel_timing"] += ("; per-step device time includes the selection (local argmin "
-                                  "kernel, RCCL all-gather, global argmin kernel)")
+        roof["kernel_timing"] += ("; per-step device time includes the selection (solve with the "
+                                  "shard's argmin fused into its launch, RCCL all-gather, global "
+                                  "argmin kernel)")
 
     if rank == 0:
         cpu = None
@@ -546,6 +590,10 @@ def main():
                "selection": bool(select and wl == "linear")}
         if useful_per_step is not None:
             cfg["converged_per_step"] = useful_per_step
+        if selection_ms is not None:
+            # device ms per step of solve + fused shard argmin + global argmin
+            cfg["selection_step_ms"] = selection_ms
+            cfg["selection_overhead_ms"] = selection_ms - kernel_ms
         line = {
             "metric": metric,
             "value": value,

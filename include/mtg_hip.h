@@ -99,12 +99,16 @@ int mtg_plan_destroy(mtg_plan* plan);
  * mtg_plan_kernel returns the forced kernel, or for AUTO the wavefront
  * kernel (GENERIC or STANDARD); mtg_plan_kernel_for_batch the kernel a
  * solve of B trajectories runs.  The time, free-derivative and sampling
- * entry points treat LANE like STANDARD. */
+ * entry points treat LANE like STANDARD.  LANE_PAIR (same coverage as LANE)
+ * gives each (trajectory, dimension) two lanes that eliminate the vertex
+ * chain from both ends toward the middle vertex (a twisted factorisation):
+ * half the dependent chain and twice the wavefronts of LANE. */
 enum {
   MTG_KERNEL_AUTO = 0,
   MTG_KERNEL_GENERIC = 1,
   MTG_KERNEL_STANDARD = 2,
-  MTG_KERNEL_LANE = 3
+  MTG_KERNEL_LANE = 3,
+  MTG_KERNEL_LANE_PAIR = 4
 };
 int mtg_plan_set_kernel(mtg_plan* plan, int kernel);
 int mtg_plan_kernel(const mtg_plan* plan);
@@ -600,6 +604,23 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
  * each, stream-ordered, graph-capturable. */
 int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank, double* out,
                      void* stream);
+
+/* The solve and the shard's selection in one launch: mtg_linear_solve, and
+ * the launch's last workgroup reduces the per-workgroup best trajectories to
+ * mtg_select_local's triple (cost, start + index, rank) in `triple` (device,
+ * 3 doubles), with the same ordering rules.  `cost` must be non-NULL.
+ * workspace: caller-owned device memory of at least
+ * mtg_select_workspace_bytes(plan, B) bytes, zero-filled once before its
+ * first use (the launch re-arms it); one solve at a time may use it.  The
+ * generic-pattern kernel falls back to a separate selection launch.  A step
+ * of the multi-GPU path is then this call, the RCCL all-gather of the
+ * triples, and mtg_select_global. */
+int64_t mtg_select_workspace_bytes(const mtg_plan* plan, int64_t B);
+int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                            const double* times, double* coeffs, double* cost,
+                            double* free_vals, int32_t* status, int64_t start, int rank,
+                            double* triple, void* workspace, size_t workspace_bytes,
+                            void* stream);
 int mtg_select_global(const double* triples, int world, double* out, void* stream);
 
 /* ------------------------------------------------------------------------

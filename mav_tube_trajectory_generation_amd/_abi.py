@@ -197,6 +197,10 @@ SIGNATURES = {
                                               _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "mtg_select_local": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "mtg_select_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64]),
+    "mtg_linear_solve_select": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                               ctypes.c_int64, ctypes.c_int, _vp, _vp,
+                                               ctypes.c_size_t, _vp]),
     "mtg_select_global": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.c_void_p]),
     "mtg_sample_trajectories": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,

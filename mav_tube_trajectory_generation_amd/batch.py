@@ -76,7 +76,7 @@ class LinearPlan:
         check(lib().mtg_plan_counts(self._h, ctypes.byref(nf), ctypes.byref(np_)), "counts")
         self.n_fixed, self.n_free = nf.value, np_.value
 
-    KERNELS = {"auto": 0, "generic": 1, "standard": 2, "lane": 3}
+    KERNELS = {"auto": 0, "generic": 1, "standard": 2, "lane": 3, "lane_pair": 4}
     _NAMES = {v: k for k, v in KERNELS.items()}
 
     def set_kernel(self, which):
@@ -137,6 +137,42 @@ class LinearPlan:
         check(lib().mtg_linear_solve(self._h, B, _ptr(fixed_vals), _ptr(times), _ptr(o["coeffs"]),
                                      _ptr(o.get("cost")), _ptr(o.get("free")),
                                      _ptr(o.get("status")), _stream(dev)), "mtg_linear_solve")
+        return o
+
+    def select_workspace(self, B, device):
+        """Zeroed workspace of solve_select for B trajectories."""
+        import torch
+        n = lib().mtg_select_workspace_bytes(self._h, B)
+        if n < 0:
+            check(int(n), "mtg_select_workspace_bytes")
+        return torch.zeros(int(n), dtype=torch.uint8, device=device)
+
+    def solve_select(self, fixed_vals, times, start, rank, workspace, out=None, free=False,
+                     status=True):
+        """solve() with the shard's selection fused into the same launch
+        (mtg_linear_solve_select): adds "triple" = (cost, start + index,
+        rank), the select_local rule, as a float64 device tensor [3].
+        workspace from select_workspace(B)."""
+        import torch
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        dev = times.device
+        o = out or {}
+        if "coeffs" not in o:
+            o["coeffs"] = torch.empty((B, self.S, self.D, self.N), dtype=torch.float64, device=dev)
+        if "cost" not in o:
+            o["cost"] = torch.empty(B, dtype=torch.float64, device=dev)
+        if free and "free" not in o:
+            o["free"] = torch.empty((B, self.D, self.n_free), dtype=torch.float64, device=dev)
+        if status and "status" not in o:
+            o["status"] = torch.empty(B, dtype=torch.int32, device=dev)
+        if "triple" not in o:
+            o["triple"] = torch.empty(3, dtype=torch.float64, device=dev)
+        check(lib().mtg_linear_solve_select(
+            self._h, B, _ptr(fixed_vals), _ptr(times), _ptr(o["coeffs"]), _ptr(o["cost"]),
+            _ptr(o.get("free")), _ptr(o.get("status")), int(start), int(rank), _ptr(o["triple"]),
+            _ptr(workspace), workspace.numel(), _stream(dev)), "mtg_linear_solve_select")
         return o
 
     def coefficients(self, fixed_vals, free_vals, times):

@@ -273,7 +273,7 @@ int mtg_plan_destroy(mtg_plan* plan) {
 }
 
 int mtg_plan_set_kernel(mtg_plan* plan, int kernel) {
-  if (!plan || kernel < MTG_KERNEL_AUTO || kernel > MTG_KERNEL_LANE)
+  if (!plan || kernel < MTG_KERNEL_AUTO || kernel > MTG_KERNEL_LANE_PAIR)
     return MTG_ERR_INVALID_ARG;
   if (kernel == MTG_KERNEL_STANDARD && !plan->dev.std_pattern) return MTG_ERR_UNSUPPORTED;
   if (kernel >= MTG_KERNEL_LANE) {
@@ -530,6 +530,46 @@ int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank
     return MTG_ERR_INVALID_ARG;
   return from_hip(mtg::launch_select_local(costs, count, start, rank, out,
                                            static_cast<hipStream_t>(stream)));
+}
+
+// Workspace of the fused selection: the counter, then the per-workgroup
+// (cost, index) partials, 256-byte aligned.
+static size_t select_ws_layout(const mtg_plan* plan, int64_t B, size_t* off_cost,
+                               size_t* off_idx) {
+  const int64_t parts = mtg::select_partials(plan->dev, B);
+  *off_cost = 256;
+  *off_idx = *off_cost + ((sizeof(double) * static_cast<size_t>(parts) + 255) & ~size_t(255));
+  return *off_idx + sizeof(int64_t) * static_cast<size_t>(parts);
+}
+
+int64_t mtg_select_workspace_bytes(const mtg_plan* plan, int64_t B) {
+  if (!plan || B < 0) return MTG_ERR_INVALID_ARG;
+  size_t a, b;
+  return static_cast<int64_t>(select_ws_layout(plan, B, &a, &b));
+}
+
+int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                            const double* times, double* coeffs, double* cost,
+                            double* free_vals, int32_t* status, int64_t start, int rank,
+                            double* triple, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+  if (!plan || B < 0 || B > 0x7fffffff || start < 0 || rank < 0 || !triple)
+    return MTG_ERR_INVALID_ARG;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  if (B == 0) return from_hip(mtg::launch_select_local(nullptr, 0, start, rank, triple, st));
+  if (!fixed_vals || !times || !coeffs || !cost || !workspace) return MTG_ERR_INVALID_ARG;
+  size_t oc, oi;
+  if (select_ws_layout(plan, B, &oc, &oi) > workspace_bytes) return MTG_ERR_INVALID_ARG;
+  char* w = static_cast<char*>(workspace);
+  mtg::SelectArgs sel;
+  sel.start = start;
+  sel.rank = rank;
+  sel.out = triple;
+  sel.counter = reinterpret_cast<unsigned*>(w);
+  sel.part_cost = reinterpret_cast<double*>(w + oc);
+  sel.part_idx = reinterpret_cast<int64_t*>(w + oi);
+  return from_hip(mtg::launch_linear_solve(plan->dev, B, fixed_vals, times, coeffs, cost,
+                                           free_vals, status, st, sel));
 }
 
 int mtg_select_global(const double* triples, int world, double* out, void* stream) {

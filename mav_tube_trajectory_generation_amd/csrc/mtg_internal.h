@@ -26,6 +26,21 @@ struct PlanDev {
   int kernel;              // MTG_KERNEL_* choice (mtg_plan_set_kernel)
 };
 
+// Selection fused into a solve kernel's epilogue (mtg_select_device.h):
+// the shard's (cost, start + index, rank) triple into out[3]; counter (zero
+// between launches) and the per-workgroup partials come from the caller's
+// workspace.  out == nullptr: no selection.
+struct SelectArgs {
+  int64_t start = 0;
+  int rank = 0;
+  double* out = nullptr;
+  unsigned* counter = nullptr;
+  double* part_cost = nullptr;
+  int64_t* part_idx = nullptr;
+};
+// Workgroups of the fused solve (the partial slots the workspace needs).
+int64_t select_partials(const PlanDev& pl, int64_t B);
+
 // Standard-pattern linear solve (mtg_linear_std.hip).
 constexpr int kMaxStdS = 64;
 // Lane linear solve for large batches (mtg_linear_lane.hip): one
@@ -37,11 +52,21 @@ struct PlanDev;
 bool has_linear_lane(const PlanDev& pl);
 hipError_t launch_linear_solve_lane(const PlanDev& pl, int64_t B, const double* df,
                                     const double* times, double* coeffs, double* cost,
-                                    double* free_vals, int32_t* status, hipStream_t st);
+                                    double* free_vals, int32_t* status, hipStream_t st,
+                                    const SelectArgs& sel = SelectArgs{});
+int64_t lane_blocks(int64_t B);
+// Two lanes per (trajectory, dimension), twisted elimination
+// (mtg_linear_lane2.hip); same coverage as the lane kernel.
+hipError_t launch_linear_solve_lane2(const PlanDev& pl, int64_t B, const double* df,
+                                     const double* times, double* coeffs, double* cost,
+                                     double* free_vals, int32_t* status, hipStream_t st,
+                                     const SelectArgs& sel = SelectArgs{});
+int64_t lane2_blocks(int64_t B);
 int linear_kernel_for_batch(const PlanDev& pl, int64_t B);
 hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
                                    const double* times, double* coeffs, double* cost,
-                                   double* free_vals, int32_t* status, hipStream_t st);
+                                   double* free_vals, int32_t* status, hipStream_t st,
+                                   const SelectArgs& sel = SelectArgs{});
 size_t linear_std_lds_bytes(int N, int S, int D);
 // Standard-pattern time kernels (mtg_time_std.hip): N = 10, r = 2..4, D = 1..3.
 bool has_time_std(const PlanDev& pl);
@@ -74,7 +99,8 @@ inline bool use_std_kernel(const PlanDev& pl) {
 
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,
-                               double* free_vals, int32_t* status, hipStream_t st);
+                               double* free_vals, int32_t* status, hipStream_t st,
+                               const SelectArgs& sel = SelectArgs{});
 hipError_t launch_coeffs_from_constraints(const PlanDev& pl, int64_t B, const double* df,
                                           const double* dp, const double* times,
                                           double* coeffs, double* cost, int32_t* status,

@@ -493,17 +493,38 @@ int linear_kernel_for_batch(const PlanDev& pl, int64_t B) {
   return use_std_kernel(pl) ? MTG_KERNEL_STANDARD : MTG_KERNEL_GENERIC;
 }
 
+int64_t select_partials(const PlanDev& pl, int64_t B) {
+  const int k = linear_kernel_for_batch(pl, B);
+  if (k == MTG_KERNEL_LANE) return lane_blocks(B);
+  if (k == MTG_KERNEL_LANE_PAIR) return lane2_blocks(B);
+  return B;  // one workgroup per trajectory
+}
+
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,
-                               double* free_vals, int32_t* status, hipStream_t st) {
+                               double* free_vals, int32_t* status, hipStream_t st,
+                               const SelectArgs& sel) {
   const int k = linear_kernel_for_batch(pl, B);
   if (k == MTG_KERNEL_LANE)
-    return launch_linear_solve_lane(pl, B, df, times, coeffs, cost, free_vals, status, st);
+    return launch_linear_solve_lane(pl, B, df, times, coeffs, cost, free_vals, status, st, sel);
+  if (k == MTG_KERNEL_LANE_PAIR)
+    return launch_linear_solve_lane2(pl, B, df, times, coeffs, cost, free_vals, status, st, sel);
   if (use_std_kernel(pl))
-    return launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st);
+    return launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st, sel);
+  // The generic kernel has no fused epilogue: a separate selection launch.
+  hipError_t e;
 #define CALL(n) launch_linear_n<n>(pl, B, df, times, coeffs, cost, free_vals, status, st)
-  MTG_DISPATCH_N(pl.N, CALL)
+  switch (pl.N) {
+    case 4: e = CALL(4); break;
+    case 6: e = CALL(6); break;
+    case 8: e = CALL(8); break;
+    case 10: e = CALL(10); break;
+    case 12: e = CALL(12); break;
+    default: return hipErrorInvalidValue;
+  }
 #undef CALL
+  if (e != hipSuccess || !sel.out) return e;
+  return launch_select_local(cost, B, sel.start, sel.rank, sel.out, st);
 }
 
 hipError_t launch_coeffs_from_constraints(const PlanDev& pl, int64_t B, const double* df,

@@ -36,6 +36,7 @@
 
 #include <cmath>
 
+#include "mtg_select_device.h"
 #include "mtg_std_device.h"
 
 namespace mtg {
@@ -381,7 +382,7 @@ template <int N, int R, int D, int S, int ND>
 __global__ __launch_bounds__(kWave) void linear_lane_kernel(
     int64_t B, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     const double* __restrict__ times, double* __restrict__ coeffs, double* __restrict__ cost,
-    double* __restrict__ free_vals, int32_t* __restrict__ status) {
+    double* __restrict__ free_vals, int32_t* __restrict__ status, SelectArgs sel) {
   constexpr int LPT = D / ND;          // lanes per trajectory
   constexpr int TPW = kWave / LPT;     // trajectories per wavefront
   const int lane = threadIdx.x;
@@ -404,6 +405,9 @@ __global__ __launch_bounds__(kWave) void linear_lane_kernel(
     if (cost) cost[b] = cpart;
     if (status) status[b] = st == 1 ? MTG_TRAJ_BAD_TIME : (st == 2 ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
   }
+  // Fused selection: the wave's best trajectory is this workgroup's partial.
+  if (sel.out)
+    select_epilogue(sel, cpart, act && part == 0 ? b : -1, blockIdx.x, gridDim.x, B);
 }
 
 namespace {
@@ -411,21 +415,21 @@ namespace {
 template <int N, int R, int D, int S, int ND>
 hipError_t launch_lane(int64_t B, const double* tab, const double* df, const double* times,
                        double* coeffs, double* cost, double* free_vals, int32_t* status,
-                       hipStream_t st) {
+                       hipStream_t st, const SelectArgs& sel) {
   constexpr int TPW = kWave / (D / ND);
   const int64_t blocks = (B + TPW - 1) / TPW;
   hipLaunchKernelGGL((linear_lane_kernel<N, R, D, S, ND>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kWave), 0, st, B, tab, df, times, coeffs, cost, free_vals, status);
+                     dim3(kWave), 0, st, B, tab, df, times, coeffs, cost, free_vals, status, sel);
   return hipGetLastError();
 }
 
 template <int ND>
 hipError_t launch_lane_s(int S, int64_t B, const double* tab, const double* df,
                          const double* times, double* coeffs, double* cost, double* free_vals,
-                         int32_t* status, hipStream_t st) {
+                         int32_t* status, hipStream_t st, const SelectArgs& sel) {
   switch (S) {
 #define MTG_LANE_S(SS) \
-    case SS: return launch_lane<10, 4, 3, SS, ND>(B, tab, df, times, coeffs, cost, free_vals, status, st);
+    case SS: return launch_lane<10, 4, 3, SS, ND>(B, tab, df, times, coeffs, cost, free_vals, status, st, sel);
     MTG_LANE_S(2) MTG_LANE_S(3) MTG_LANE_S(4) MTG_LANE_S(5) MTG_LANE_S(6) MTG_LANE_S(7)
     MTG_LANE_S(8) MTG_LANE_S(9) MTG_LANE_S(10) MTG_LANE_S(11) MTG_LANE_S(12)
 #undef MTG_LANE_S
@@ -442,9 +446,15 @@ bool has_linear_lane(const PlanDev& pl) {
 
 hipError_t launch_linear_solve_lane(const PlanDev& pl, int64_t B, const double* df,
                                     const double* times, double* coeffs, double* cost,
-                                    double* free_vals, int32_t* status, hipStream_t st) {
+                                    double* free_vals, int32_t* status, hipStream_t st,
+                                    const SelectArgs& sel) {
   if (!has_linear_lane(pl)) return hipErrorInvalidValue;
-  return launch_lane_s<1>(pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
+  return launch_lane_s<1>(pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st, sel);
+}
+
+int64_t lane_blocks(int64_t B) {
+  constexpr int TPW = kWave / 3;  // N = 10, D = 3, one dimension per lane
+  return (B + TPW - 1) / TPW;
 }
 
 }  // namespace mtg

@@ -8,7 +8,9 @@ broadcast of the winning trajectory's coefficients from its owner.
 
 Two selection paths:
   select_best_device  each rank reduces its shard to one (cost, global index,
-                      rank) triple on the device, the triples are all-gathered
+                      rank) triple on the device (fused into the solve launch
+                      by LinearPlan.solve_select, or one extra launch), the
+                      triples are all-gathered
                       (24 B per rank) and reduced again on the device: on GPU
                       tensors one HIP launch each (mtg_select_local /
                       mtg_select_global) around the RCCL all-gather; on CPU
@@ -90,14 +92,17 @@ def local_best(local_costs, global_batch, group=None):
     return out
 
 
-def select_best_device(local_costs, global_batch, group=None):
+def select_best_device(local_costs, global_batch, group=None, local_triple=None):
     """Global argmin over all shards without a host sync.  Returns a float64
     device tensor [3] = (cost, global index, owner rank), identical on every
     rank.  Ties go to the lowest global index (shards are contiguous and in
     rank order, so the first rank holding the minimum); if every cost is NaN
-    or +inf the winner is global index 0, as a single-process argmin."""
+    or +inf the winner is global index 0, as a single-process argmin.
+    local_triple: this rank's triple already reduced (the fused
+    LinearPlan.solve_select); local_costs is then not read."""
     world = dist.get_world_size(group)
-    mine = local_best(local_costs, global_batch, group)
+    mine = local_triple if local_triple is not None else \
+        local_best(local_costs, global_batch, group)
     flat = torch.empty(world * 3, dtype=torch.float64, device=mine.device)
     dist.all_gather_into_tensor(flat, mine, group=group)
     if flat.is_cuda:  # one HIP launch (mtg_select_global)

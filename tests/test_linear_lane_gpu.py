@@ -1,5 +1,6 @@
-"""The lane linear kernel (mtg_linear_lane.hip, LANE: one (trajectory,
-dimension) per lane) against the wavefront standard-pattern kernel and the
+"""The lane linear kernels (mtg_linear_lane.hip, LANE: one (trajectory,
+dimension) per lane; mtg_linear_lane2.hip, LANE_PAIR: two lanes per
+(trajectory, dimension), twisted elimination) against the wavefront standard-pattern kernel and the
 oracle, and AUTO's choice by batch size."""
 import numpy as np
 import pytest
@@ -22,8 +23,8 @@ def _solve(ctx, dev, mask, fixed, times, kernel):
     return plan, {k: v.cpu().numpy() for k, v in out.items()}
 
 
-@pytest.mark.parametrize("kernel", ["lane"])
-@pytest.mark.parametrize("S", [2, 3, 4, 7, 10, 12])
+@pytest.mark.parametrize("kernel", ["lane", "lane_pair"])
+@pytest.mark.parametrize("S", list(range(2, 13)))
 def test_lane_kernels_match_wavefront_kernel(ctx, dev, oracle, kernel, S):
     """Same inputs as the wavefront kernel, a batch that is not a multiple of
     the trajectories per wavefront (21): coefficients, d_p and cost to
@@ -46,7 +47,7 @@ def test_lane_kernels_match_wavefront_kernel(ctx, dev, oracle, kernel, S):
         assert rel_err(out["cost"][b], o["cost"]) <= REL_TOL, b
 
 
-@pytest.mark.parametrize("kernel", ["lane"])
+@pytest.mark.parametrize("kernel", ["lane", "lane_pair"])
 def test_lane_kernels_bad_time(ctx, dev, kernel):
     import mav_tube_trajectory_generation_amd as mtg
     S, B = 5, 70
@@ -80,6 +81,8 @@ def test_auto_selection_by_batch(ctx):
     assert p2.kernel_for_batch(65536) == "standard"
     with pytest.raises(mtg.MTGError):
         p2.set_kernel("lane")
+    with pytest.raises(mtg.MTGError):
+        p2.set_kernel("lane_pair")
     m20, _, _, _ = mtg.generate_random_problems(N, D, 20, 1, seed0=1)
     p3 = mtg.LinearPlan(ctx, N, D, R, 20, m20)
     assert p3.kernel_for_batch(65536) == "standard"

@@ -115,3 +115,58 @@ def test_select_best_device_one_rank_rccl(ctx, dev):
     finally:
         if created:
             dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kernel", ["standard", "lane", "lane_pair", "generic"])
+def test_solve_select_fused(ctx, dev, kernel):
+    """mtg_linear_solve_select: the shard's triple formed in the solve's own
+    launch (last-workgroup reduction of per-workgroup partials) equals the
+    selection rule on the costs the same launch wrote, with NaN costs (bad
+    times), ties (duplicated trajectories) and repeated launches on one
+    workspace (the counter re-arms); inside a captured graph as well."""
+    import mav_tube_trajectory_generation_amd as mtg
+    N, D, S, B = 10, 3, 10, 3000
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=400)
+    plan = mtg.LinearPlan(ctx, N, D, 4, S, mask).set_kernel(kernel)
+    ref = plan.solve(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev))
+    c0 = ref["cost"].cpu().numpy()
+    best = int(np.argmin(c0))
+    # Ties: copies of the best trajectory after it and before it.
+    for j in (best + 7) % B, (best + 1500) % B:
+        fixed[j] = fixed[best]
+        times[j] = times[best]
+    times[5, 2] = -1.0  # a bad time: NaN cost, never selected
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    ws = plan.select_workspace(B, dev)
+    for rep in range(3):
+        out = plan.solve_select(fd, td, 1000, 2, ws)
+        torch.cuda.synchronize(dev)
+        c = out["cost"].cpu().numpy()
+        assert np.isnan(c[5])
+        got = tuple(out["triple"].cpu().numpy())
+        assert _same(got, _ref_local(c, 1000, 2)), (rep, got, _ref_local(c, 1000, 2))
+        assert got[1] - 1000 == min(best, (best + 7) % B, (best + 1500) % B)
+    # Captured graph: new costs after a change of the inputs.
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = plan.solve_select(fd, td, 0, 0, ws, out=out)
+    td[best, :] *= 3.0
+    td[(best + 7) % B, :] *= 3.0
+    td[(best + 1500) % B, :] *= 3.0
+    g.replay()
+    torch.cuda.synchronize(dev)
+    c = out["cost"].cpu().numpy()
+    assert _same(tuple(out["triple"].cpu().numpy()), _ref_local(c, 0, 0))
+
+
+def test_solve_select_all_bad_and_empty(ctx, dev):
+    import mav_tube_trajectory_generation_amd as mtg
+    N, D, S, B = 10, 3, 4, 70
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=9)
+    plan = mtg.LinearPlan(ctx, N, D, 4, S, mask)
+    times[:] = -1.0
+    ws = plan.select_workspace(B, dev)
+    out = plan.solve_select(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev),
+                            50, 1, ws)
+    # every cost NaN: the shard's first index, cost +inf
+    assert tuple(out["triple"].cpu().numpy()) == (math.inf, 50.0, 1.0)
