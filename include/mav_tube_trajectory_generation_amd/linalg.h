@@ -2,11 +2,15 @@
 // Eigen::VectorXd / Eigen::MatrixXd of the reference's public API
 // (vertex.h:45, polynomial.h:61; Eigen is not available in this image,
 // SURVEY.md §8b).  Only the operations the API surface needs; column vectors,
-// row-major matrices, operator()(i, j) indexing as in Eigen.
+// and matrices stored column-major as Eigen's default MatrixXd is, so a
+// caller copying getM() / getA() / getAInverse() / getMpinv() through
+// data() reads the same order it would from Eigen; operator()(i, j)
+// indexing as in Eigen.
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_LINALG_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_LINALG_H_
 
 #include <cmath>
+#include <complex>
 #include <cstddef>
 #include <initializer_list>
 #include <ostream>
@@ -114,6 +118,37 @@ inline std::ostream& operator<<(std::ostream& os, const VectorXd& v) {
   return os;
 }
 
+// Complex column vector (Eigen::VectorXcd of Polynomial::getRoots,
+// polynomial.h:153; findRootsJenkinsTraub, rpoly_ak1.h:26).
+class VectorXcd {
+ public:
+  typedef std::complex<double> Scalar;
+  VectorXcd() {}
+  explicit VectorXcd(long n) : v_(static_cast<size_t>(n)) {}
+  long size() const { return static_cast<long>(v_.size()); }
+  long rows() const { return size(); }
+  void resize(long n) { v_.assign(static_cast<size_t>(n), Scalar()); }
+  Scalar& operator[](long i) { return v_[static_cast<size_t>(i)]; }
+  const Scalar& operator[](long i) const { return v_[static_cast<size_t>(i)]; }
+  Scalar& operator()(long i) { return v_[static_cast<size_t>(i)]; }
+  const Scalar& operator()(long i) const { return v_[static_cast<size_t>(i)]; }
+  Scalar* data() { return v_.data(); }
+  const Scalar* data() const { return v_.data(); }
+  VectorXd real() const {
+    VectorXd r(size());
+    for (long i = 0; i < size(); ++i) r[i] = v_[static_cast<size_t>(i)].real();
+    return r;
+  }
+  VectorXd imag() const {
+    VectorXd r(size());
+    for (long i = 0; i < size(); ++i) r[i] = v_[static_cast<size_t>(i)].imag();
+    return r;
+  }
+
+ private:
+  std::vector<Scalar> v_;
+};
+
 class MatrixXd {
  public:
   MatrixXd() {}
@@ -134,8 +169,9 @@ class MatrixXd {
   void setZero() {
     for (double& e : a_) e = 0.0;
   }
-  double& operator()(long i, long j) { return a_[static_cast<size_t>(i * c_ + j)]; }
-  double operator()(long i, long j) const { return a_[static_cast<size_t>(i * c_ + j)]; }
+  // Column-major: entry (i, j) at data()[j * rows() + i] (Eigen's default).
+  double& operator()(long i, long j) { return a_[static_cast<size_t>(j * r_ + i)]; }
+  double operator()(long i, long j) const { return a_[static_cast<size_t>(j * r_ + i)]; }
   double* data() { return a_.data(); }
   const double* data() const { return a_.data(); }
 

@@ -13,6 +13,7 @@
 #include "mav_tube_trajectory_generation_amd/check.h"
 #include "mav_tube_trajectory_generation_amd/linalg.h"
 #include "mav_tube_trajectory_generation_amd/motion_defines.h"
+#include "mav_tube_trajectory_generation_amd/rpoly/rpoly_ak1.h"
 
 namespace mav_trajectory_generation {
 
@@ -109,6 +110,48 @@ class Polynomial {
     for (int i = 0; i < N_; ++i) c[i] = coefficients_[i];
     *out = Polynomial(c);
     return true;
+  }
+
+  // All complex roots of p^(derivative) (polynomial.cpp:28-30), by the
+  // root finder of rpoly/rpoly_ak1.h.
+  bool getRoots(int derivative, VectorXcd* roots) const {
+    return findRootsJenkinsTraub(getCoefficients(derivative), roots);
+  }
+
+  // t_start, t_end and the real roots (|Im| <= DBL_EPSILON) inside
+  // [t_start, t_end], in that order (polynomial.cpp:32-63).
+  static bool selectMinMaxCandidatesFromRoots(double t_start, double t_end,
+                                              const VectorXcd& roots_derivative_of_derivative,
+                                              std::vector<double>* candidates) {
+    MTG_CHECK(candidates != nullptr, "candidates must not be null");
+    if (t_start > t_end) {
+      internal::warn("t_start is greater than t_end.");
+      return false;
+    }
+    candidates->clear();
+    candidates->push_back(t_start);
+    candidates->push_back(t_end);
+    for (long i = 0; i < roots_derivative_of_derivative.size(); ++i) {
+      const std::complex<double>& r = roots_derivative_of_derivative[i];
+      if (std::abs(r.imag()) > std::numeric_limits<double>::epsilon()) continue;
+      if (r.real() < t_start || r.real() > t_end) continue;
+      candidates->push_back(r.real());
+    }
+    return true;
+  }
+
+  // Extrema of p^(derivative) among t_start, t_end and the given roots of
+  // p^(derivative+1) (polynomial.cpp:65-80).
+  bool selectMinMaxFromRoots(double t_start, double t_end, int derivative,
+                             const VectorXcd& roots_derivative_of_derivative,
+                             std::pair<double, double>* minimum,
+                             std::pair<double, double>* maximum) const {
+    MTG_CHECK(minimum != nullptr && maximum != nullptr, "outputs must not be null");
+    std::vector<double> candidates;
+    if (!selectMinMaxCandidatesFromRoots(t_start, t_end, roots_derivative_of_derivative,
+                                         &candidates))
+      return false;
+    return selectMinMaxFromCandidates(candidates, derivative, minimum, maximum);
   }
 
   // Extrema of p^(derivative) on [t_start, t_end] (polynomial.cpp:32-143):

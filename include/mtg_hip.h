@@ -605,15 +605,17 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
 int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank, double* out,
                      void* stream);
 
-/* The solve and the shard's selection in one launch: mtg_linear_solve, and
- * the launch's last workgroup reduces the per-workgroup best trajectories to
+/* The solve and the shard's selection: mtg_linear_solve, then
  * mtg_select_local's triple (cost, start + index, rank) in `triple` (device,
- * 3 doubles), with the same ordering rules.  `cost` must be non-NULL.
- * workspace: caller-owned device memory of at least
- * mtg_select_workspace_bytes(plan, B) bytes, zero-filled once before its
- * first use (the launch re-arms it); one solve at a time may use it.  The
- * generic-pattern kernel falls back to a separate selection launch.  A step
- * of the multi-GPU path is then this call, the RCCL all-gather of the
+ * 3 doubles), with the same ordering rules.  The lane kernels write each
+ * workgroup's best (cost, index) in their epilogue and one single-workgroup
+ * launch reduces those partials; the wavefront kernels (one trajectory per
+ * workgroup) are followed by the same reduction over the costs.  Two
+ * stream-ordered launches, no atomics, graph-capturable.  `cost` must be
+ * non-NULL.  workspace: caller-owned device memory of at least
+ * mtg_select_workspace_bytes(plan, B) bytes (0 for the wavefront kernels;
+ * NULL allowed then), no initialisation; one solve at a time may use it.  A
+ * step of the multi-GPU path is then this call, the RCCL all-gather of the
  * triples, and mtg_select_global. */
 int64_t mtg_select_workspace_bytes(const mtg_plan* plan, int64_t B);
 int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed_vals,

@@ -140,18 +140,20 @@ class LinearPlan:
         return o
 
     def select_workspace(self, B, device):
-        """Zeroed workspace of solve_select for B trajectories."""
+        """Workspace of solve_select for B trajectories (per-workgroup
+        partials of the lane kernels; empty for the wavefront kernels)."""
         import torch
         n = lib().mtg_select_workspace_bytes(self._h, B)
         if n < 0:
             check(int(n), "mtg_select_workspace_bytes")
-        return torch.zeros(int(n), dtype=torch.uint8, device=device)
+        return torch.empty(int(n), dtype=torch.uint8, device=device)
 
     def solve_select(self, fixed_vals, times, start, rank, workspace, out=None, free=False,
                      status=True):
-        """solve() with the shard's selection fused into the same launch
-        (mtg_linear_solve_select): adds "triple" = (cost, start + index,
-        rank), the select_local rule, as a float64 device tensor [3].
+        """solve() followed by the shard's selection (mtg_linear_solve_select:
+        lane kernels reduce per-workgroup partials written by the solve's
+        epilogue): adds "triple" = (cost, start + index, rank), the
+        select_local rule, as a float64 device tensor [3].
         workspace from select_workspace(B)."""
         import torch
         B = times.shape[0]

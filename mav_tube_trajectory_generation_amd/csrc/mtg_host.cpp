@@ -537,9 +537,9 @@ int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank
 static size_t select_ws_layout(const mtg_plan* plan, int64_t B, size_t* off_cost,
                                size_t* off_idx) {
   const int64_t parts = mtg::select_partials(plan->dev, B);
-  *off_cost = 256;
-  *off_idx = *off_cost + ((sizeof(double) * static_cast<size_t>(parts) + 255) & ~size_t(255));
-  return *off_idx + sizeof(int64_t) * static_cast<size_t>(parts);
+  *off_cost = 0;
+  *off_idx = (sizeof(double) * static_cast<size_t>(parts) + 255) & ~size_t(255);
+  return parts > 0 ? *off_idx + sizeof(int64_t) * static_cast<size_t>(parts) : 0;
 }
 
 int64_t mtg_select_workspace_bytes(const mtg_plan* plan, int64_t B) {
@@ -557,15 +557,15 @@ int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed
     return MTG_ERR_INVALID_ARG;
   const hipStream_t st = static_cast<hipStream_t>(stream);
   if (B == 0) return from_hip(mtg::launch_select_local(nullptr, 0, start, rank, triple, st));
-  if (!fixed_vals || !times || !coeffs || !cost || !workspace) return MTG_ERR_INVALID_ARG;
+  if (!fixed_vals || !times || !coeffs || !cost) return MTG_ERR_INVALID_ARG;
   size_t oc, oi;
-  if (select_ws_layout(plan, B, &oc, &oi) > workspace_bytes) return MTG_ERR_INVALID_ARG;
+  const size_t need = select_ws_layout(plan, B, &oc, &oi);
+  if (need > workspace_bytes || (need > 0 && !workspace)) return MTG_ERR_INVALID_ARG;
   char* w = static_cast<char*>(workspace);
   mtg::SelectArgs sel;
   sel.start = start;
   sel.rank = rank;
   sel.out = triple;
-  sel.counter = reinterpret_cast<unsigned*>(w);
   sel.part_cost = reinterpret_cast<double*>(w + oc);
   sel.part_idx = reinterpret_cast<int64_t*>(w + oi);
   return from_hip(mtg::launch_linear_solve(plan->dev, B, fixed_vals, times, coeffs, cost,

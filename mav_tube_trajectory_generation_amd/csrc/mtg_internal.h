@@ -27,14 +27,13 @@ struct PlanDev {
 };
 
 // Selection fused into a solve kernel's epilogue (mtg_select_device.h):
-// the shard's (cost, start + index, rank) triple into out[3]; counter (zero
-// between launches) and the per-workgroup partials come from the caller's
-// workspace.  out == nullptr: no selection.
+// the shard's (cost, start + index, rank) triple into out[3]; the lane
+// kernels write per-workgroup partials (caller's workspace) that one small
+// launch reduces.  out == nullptr: no selection.
 struct SelectArgs {
   int64_t start = 0;
   int rank = 0;
   double* out = nullptr;
-  unsigned* counter = nullptr;
   double* part_cost = nullptr;
   int64_t* part_idx = nullptr;
 };
@@ -65,8 +64,7 @@ int64_t lane2_blocks(int64_t B);
 int linear_kernel_for_batch(const PlanDev& pl, int64_t B);
 hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
                                    const double* times, double* coeffs, double* cost,
-                                   double* free_vals, int32_t* status, hipStream_t st,
-                                   const SelectArgs& sel = SelectArgs{});
+                                   double* free_vals, int32_t* status, hipStream_t st);
 size_t linear_std_lds_bytes(int N, int S, int D);
 // Standard-pattern time kernels (mtg_time_std.hip): N = 10, r = 2..4, D = 1..3.
 bool has_time_std(const PlanDev& pl);
@@ -243,6 +241,10 @@ int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, doub
 // Multi-GPU selection (mtg_select.hip).
 hipError_t launch_select_local(const double* costs, int64_t count, int64_t start, int rank,
                                double* out, hipStream_t st);
+// Reduction of n (cost, index) partials (idx == nullptr: index = position)
+// to the triple of mtg_select_local over a shard of `count` trajectories.
+hipError_t launch_select_reduce(const double* cost, const int64_t* idx, int64_t n, int64_t count,
+                                int64_t start, int rank, double* out, hipStream_t st);
 hipError_t launch_select_global(const double* triples, int world, double* out, hipStream_t st);
 
 }  // namespace mtg

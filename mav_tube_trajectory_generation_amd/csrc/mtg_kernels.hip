@@ -497,7 +497,7 @@ int64_t select_partials(const PlanDev& pl, int64_t B) {
   const int k = linear_kernel_for_batch(pl, B);
   if (k == MTG_KERNEL_LANE) return lane_blocks(B);
   if (k == MTG_KERNEL_LANE_PAIR) return lane2_blocks(B);
-  return B;  // one workgroup per trajectory
+  return 0;  // one trajectory per workgroup: the costs are the partials
 }
 
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
@@ -505,14 +505,26 @@ hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                double* free_vals, int32_t* status, hipStream_t st,
                                const SelectArgs& sel) {
   const int k = linear_kernel_for_batch(pl, B);
-  if (k == MTG_KERNEL_LANE)
-    return launch_linear_solve_lane(pl, B, df, times, coeffs, cost, free_vals, status, st, sel);
-  if (k == MTG_KERNEL_LANE_PAIR)
-    return launch_linear_solve_lane2(pl, B, df, times, coeffs, cost, free_vals, status, st, sel);
-  if (use_std_kernel(pl))
-    return launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st, sel);
-  // The generic kernel has no fused epilogue: a separate selection launch.
+  // Lane kernels: per-workgroup partials in the epilogue, then one small
+  // reduction launch.  Wavefront kernels (one trajectory per workgroup): the
+  // reduction reads the costs.
+  if (k == MTG_KERNEL_LANE || k == MTG_KERNEL_LANE_PAIR) {
+    const hipError_t e =
+        k == MTG_KERNEL_LANE
+            ? launch_linear_solve_lane(pl, B, df, times, coeffs, cost, free_vals, status, st, sel)
+            : launch_linear_solve_lane2(pl, B, df, times, coeffs, cost, free_vals, status, st,
+                                        sel);
+    if (e != hipSuccess || !sel.out) return e;
+    const int64_t n = k == MTG_KERNEL_LANE ? lane_blocks(B) : lane2_blocks(B);
+    return launch_select_reduce(sel.part_cost, sel.part_idx, n, B, sel.start, sel.rank, sel.out,
+                                st);
+  }
   hipError_t e;
+  if (use_std_kernel(pl)) {
+    e = launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st);
+    if (e != hipSuccess || !sel.out) return e;
+    return launch_select_local(cost, B, sel.start, sel.rank, sel.out, st);
+  }
 #define CALL(n) launch_linear_n<n>(pl, B, df, times, coeffs, cost, free_vals, status, st)
   switch (pl.N) {
     case 4: e = CALL(4); break;

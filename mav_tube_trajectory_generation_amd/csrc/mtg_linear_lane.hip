@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kWave) void linear_lane_kernel(
   }
   // Fused selection: the wave's best trajectory is this workgroup's partial.
   if (sel.out)
-    select_epilogue(sel, cpart, act && part == 0 ? b : -1, blockIdx.x, gridDim.x, B);
+    select_partial(sel, cpart, act && part == 0 ? b : -1, blockIdx.x);
 }
 
 namespace {

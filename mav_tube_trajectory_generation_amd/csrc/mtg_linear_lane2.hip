@@ -111,52 +111,49 @@ __device__ inline void ldlt_apply(const double (&l)[MF][MF], const double (&inv)
   }
 }
 
-// The value of the partner lane (lane ^ 1) by DPP quad_perm [1, 0, 3, 2].
-__device__ inline double partner(double x) {
-  const long long u = __builtin_bit_cast(long long, x);
-  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(u), 0xB1, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(u >> 32), 0xB1, 0xf, 0xf, false);
-  return stdp::join64(lo, hi);
-}
-
-template <int N, int R, int D, int S>
-struct PairSolve {
+// One half of the twisted elimination for one (trajectory, dimension):
+// BW = false eliminates forward over v = 1 .. MID-1 (step k: v = 1 + k),
+// BW = true backward over v = S-1 .. MID+1 (step k: v = S - 1 - k).  The
+// direction is a template parameter: each wave of the kernel runs one
+// direction, so every index is compile-time and no lane selects.
+template <int N, int R, int D, int S, bool BW>
+struct Half {
   static constexpr int M = N / 2, MF = M - 1;
   static constexpr int NF = 2 * M + S - 1;     // fixed derivatives per dimension
   static constexpr int NL = MF * (MF - 1) / 2;
+  static constexpr int NT = MF * (MF + 1) / 2;  // lower triangle of a block
   static constexpr int MID = S / 2;             // middle vertex, 1 <= MID <= S-1
-  static constexpr int NFW = MID - 1;           // forward steps (v = 1 .. MID-1)
-  static constexpr int NBW = S - 1 - MID;       // backward steps (v = S-1 .. MID+1)
-  static constexpr int NST = NFW > NBW ? NFW : NBW;
-  static constexpr int NSEG = (MID > S - MID ? MID : S - MID);  // segments per lane, at most
+  static constexpr int NST = BW ? S - 1 - MID : MID - 1;  // elimination steps
+  static constexpr int NSEG = BW ? S - MID : MID;         // segments of this half
+  static constexpr int NSTc = NST > 0 ? NST : 1;
 
   __device__ static constexpr int ex(int a, int b) { return 1 - 2 * R + a % M + b % M; }
+  __device__ static constexpr int vert(int k) { return BW ? S - 1 - k : 1 + k; }
 
-  // The lane's step k: its vertex v (forward 1+k, backward S-1-k) and the
-  // compile-time indices of the neighbouring data, selected by h.
+  double T[S], x0[M], xS[M], pos[S + 1];
+  double Lf[NSTc][NL > 0 ? NL : 1], If[NSTc][MF], z[NSTc][MF];
+  double Zp[MF][MF], Gp[MF][MF], zp[MF];
+  double pmin;
+  bool bad;
+
   // Coupling toward the next vertex of the sweep: forward C_v = H01(T_v),
-  // backward C_(v-1)^T = H01(T_(v-1))^T.
-  __device__ static void coupling(bool bw, const Pw<N, R>& Pl, const Pw<N, R>& Pr,
-                                  double (&G)[MF][MF]) {
+  // backward C_(v-1)^T = H01(T_(v-1))^T; P: powers of that segment's time.
+  __device__ static void coupling(const Pw<N, R>& P, double (&G)[MF][MF]) {
     constexpr HTab<N, R> kH{};
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
       for (int j = 0; j < MF; ++j) {
         const int e = ex(i + 1, j + 1);
-        const double f = kH.v[(i + 1) * N + M + j + 1] * Pr[e];
-        const double b = kH.v[(j + 1) * N + M + i + 1] * Pl[e];
-        G[i][j] = bw ? b : f;
+        G[i][j] = BW ? kH.v[(j + 1) * N + M + i + 1] * P[e] : kH.v[(i + 1) * N + M + j + 1] * P[e];
       }
   }
 
   // A_v (lower triangle) and b_v for vertex v with left / right segment
   // powers Pl (T_(v-1)) and Pr (T_v) and positions of v-1, v, v+1;
   // left_end / right_end: vertex v-1 / v+1 is the fully fixed start / end.
-  __device__ static void assemble(const Pw<N, R>& Pl, const Pw<N, R>& Pr, double pm, double p0,
-                                  double pp, bool left_end, bool right_end,
-                                  const double (&x0)[M], const double (&xS)[M],
-                                  double (&A)[MF][MF], double (&rr)[MF]) {
+  __device__ void assemble(const Pw<N, R>& Pl, const Pw<N, R>& Pr, int v, bool left_end,
+                           bool right_end, double (&A)[MF][MF], double (&rr)[MF]) const {
     constexpr HTab<N, R> kH{};
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
@@ -169,16 +166,17 @@ struct PairSolve {
       const double cprev = kH.v[(M + k) * N] * Pl[ex(k, 0)];
       const double cpos = fma(kH.v[(M + k) * N + M], Pl[ex(k, 0)], kH.v[k * N] * Pr[ex(k, 0)]);
       const double cnext = kH.v[k * N + M] * Pr[ex(k, 0)];
-      double s = cpos * p0;
-      s = fma(cprev, pm, s);
-      s = fma(cnext, pp, s);
-      double el = 0.0, er = 0.0;
+      double s = cpos * pos[v];
+      s = fma(cprev, pos[v - 1], s);
+      s = fma(cnext, pos[v + 1], s);
+      if (left_end) {
 #pragma unroll
-      for (int l = 1; l < M; ++l) {
-        el = fma(kH.v[(M + k) * N + l] * Pl[ex(k, l)], x0[l], el);
-        er = fma(kH.v[k * N + M + l] * Pr[ex(k, l)], xS[l], er);
+        for (int l = 1; l < M; ++l) s = fma(kH.v[(M + k) * N + l] * Pl[ex(k, l)], x0[l], s);
       }
-      s += (left_end ? el : 0.0) + (right_end ? er : 0.0);
+      if (right_end) {
+#pragma unroll
+        for (int l = 1; l < M; ++l) s = fma(kH.v[k * N + M + l] * Pr[ex(k, l)], xS[l], s);
+      }
       rr[i] = -s;
     }
   }
@@ -213,73 +211,40 @@ struct PairSolve {
     return stdp::Solver<N, R, D>::q_form(hh) * P[1 - 2 * R];
   }
 
-  // h = 0 forward lane, 1 backward lane of (trajectory b, dimension d).
-  // Returns 0 ok, 1 bad time, 2 not SPD; *cost_part = this lane's share.
-  __device__ static int run(int64_t b, int d, int h, const double* __restrict__ fixed_vals,
-                            const double* __restrict__ times, double* __restrict__ coeffs,
-                            double* __restrict__ free_vals, double* cost_part) {
-    const bool bw = h != 0;
-    double T[S];
-    bool bad = false;
+  __device__ void load(int64_t b, int d, const double* __restrict__ fixed_vals,
+                       const double* __restrict__ times) {
+    bad = false;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       T[s] = times[b * S + s];
       bad = bad || !(T[s] > 0.0) || !(T[s] < 1e300);
     }
-    double x0[M], xS[M], pos[S + 1];
-    {
-      const double* fb = fixed_vals + (b * D + d) * NF;
+    const double* fb = fixed_vals + (b * D + d) * NF;
 #pragma unroll
-      for (int k = 0; k < M; ++k) {
-        x0[k] = fb[k];
-        xS[k] = fb[M + S - 1 + k];
-      }
-      pos[0] = x0[0];
-      pos[S] = xS[0];
-#pragma unroll
-      for (int v = 1; v < S; ++v) pos[v] = fb[M + v - 1];
+    for (int k = 0; k < M; ++k) {
+      x0[k] = fb[k];
+      xS[k] = fb[M + S - 1 + k];
     }
-    double* cb = coeffs ? coeffs + b * S * D * N : nullptr;
-    if (bad) {
-      if (!cb) {
-        *cost_part = NAN;
-        return 1;
-      }
-      // Each lane of the pair writes half of the dimension's coefficients.
+    pos[0] = x0[0];
+    pos[S] = xS[0];
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-        if ((s < MID) != bw) {
-#pragma unroll
-          for (int i = 0; i < N; ++i) cb[(s * D + d) * N + i] = NAN;
-        }
-      *cost_part = NAN;
-      return 1;
-    }
+    for (int v = 1; v < S; ++v) pos[v] = fb[M + v - 1];
+  }
 
-    // ---- elimination over the lane's half ----------------------------------
-    // Step k: vertex v = 1 + k (forward) or S - 1 - k (backward); the left
-    // segment of v is v-1, the right v.  Kept per step: LDL^T factors of
-    // the Schur complement and z = S^-1 r; G is recomputed in the back pass.
-    double Lf[NST > 0 ? NST : 1][NL > 0 ? NL : 1], If[NST > 0 ? NST : 1][MF];
-    double z[NST > 0 ? NST : 1][MF];
-    double Zp[MF][MF], Gp[MF][MF], zp[MF];  // previous step's Z, G, z
-    double pmin = 1.0;
+  // Elimination over the half.  Kept per step: the LDL^T factors of the
+  // Schur complement and z = S^-1 r; the coupling is recomputed in the back
+  // pass.  Leaves the last step's Z = S^-1 G, G and z for the middle.
+  __device__ void eliminate() {
+    pmin = 1.0;
 #pragma unroll
     for (int k = 0; k < NST; ++k) {
-      const bool act = bw ? (k < NBW) : (k < NFW);
-      // Compile-time indices of the forward (f) and backward (b) vertex.
-      const int vf = 1 + k, vb = S - 1 - k;
-      const double tl = bw ? T[vb - 1 >= 0 ? vb - 1 : 0] : T[vf - 1];
-      const double tr = bw ? T[vb < S ? vb : S - 1] : T[vf < S ? vf : S - 1];
+      const int v = vert(k);
       Pw<N, R> Pl, Pr;
-      Pl.set(tl);
-      Pr.set(tr);
-      const double pm = bw ? pos[vb - 1 >= 0 ? vb - 1 : 0] : pos[vf - 1];
-      const double p0 = bw ? pos[vb >= 0 ? vb : 0] : pos[vf <= S ? vf : S];
-      const double pp = bw ? pos[vb + 1 <= S ? vb + 1 : S] : pos[vf + 1 <= S ? vf + 1 : S];
+      Pl.set(T[v - 1]);
+      Pr.set(T[v]);
       double A[MF][MF], rr[MF], G[MF][MF];
-      assemble(Pl, Pr, pm, p0, pp, !bw && k == 0, bw && k == 0, x0, xS, A, rr);
-      coupling(bw, Pl, Pr, G);
+      assemble(Pl, Pr, v, !BW && k == 0, BW && k == 0, A, rr);
+      coupling(BW ? Pl : Pr, G);
       if (k > 0) {
         // S_v = A_v - Gp^T Zp;  r_v = b_v - Gp^T z_prev
 #pragma unroll
@@ -298,9 +263,7 @@ struct PairSolve {
         }
       }
       double l[MF][MF];
-      double pk = 1.0;
-      ldlt<MF>(A, l, If[k], pk);
-      if (act) pmin = fmin(pmin, pk);
+      ldlt<MF>(A, l, If[k], pmin);
       {
         int q = 0;
 #pragma unroll
@@ -315,24 +278,22 @@ struct PairSolve {
 #pragma unroll
         for (int i = 0; i < MF; ++i) col[i] = G[i][c];
         ldlt_apply<MF>(l, If[k], col, xc);
-        // A lane past its last step (the shorter half of an odd S) keeps the
-        // state of its last real step for the middle vertex.
 #pragma unroll
-        for (int i = 0; i < MF; ++i) Zp[i][c] = act ? xc[i] : Zp[i][c];
+        for (int i = 0; i < MF; ++i) Zp[i][c] = xc[i];
       }
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
-        zp[i] = act ? z[k][i] : zp[i];
+        zp[i] = z[k][i];
 #pragma unroll
-        for (int j = 0; j < MF; ++j) Gp[i][j] = act ? G[i][j] : Gp[i][j];
+        for (int j = 0; j < MF; ++j) Gp[i][j] = G[i][j];
       }
     }
+  }
 
-    // ---- middle vertex -------------------------------------------------------
-    // Each lane's Schur term Gp^T Zp (and Gp^T z) at MID from its last step;
-    // the partner's arrives by DPP.  S_mid = A_mid - term_f - term_b.
-    const int nsteps = bw ? NBW : NFW;
-    double Tm[MF][MF], Rm[MF];
+  // This half's Schur terms at the middle vertex: Gp^T Zp (lower
+  // triangle, row-major) and Gp^T z.
+  __device__ void terms(double (&tm)[NT], double (&rm)[MF]) const {
+    int q = 0;
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
 #pragma unroll
@@ -340,39 +301,39 @@ struct PairSolve {
         double s = 0.0;
 #pragma unroll
         for (int m = 0; m < MF; ++m) s = fma(Gp[m][i], Zp[m][j], s);
-        Tm[i][j] = nsteps > 0 ? s : 0.0;
+        tm[q++] = NST > 0 ? s : 0.0;
       }
       double s = 0.0;
 #pragma unroll
       for (int m = 0; m < MF; ++m) s = fma(Gp[m][i], zp[m], s);
-      Rm[i] = nsteps > 0 ? s : 0.0;
+      rm[i] = NST > 0 ? s : 0.0;
     }
+  }
+
+  // Middle vertex from the forward (tf, rf) and backward (tb, rb) terms,
+  // S_mid = (A_mid - T_f) - T_b in that order on both waves (bit-identical
+  // middle values), then the back substitution outward fused with the
+  // coefficients and cost of the half's segments.  Returns the cost share.
+  __device__ double finish(int64_t b, int d, const double (&tf)[NT], const double (&rf)[MF],
+                           const double (&tb)[NT], const double (&rb)[MF],
+                           double* __restrict__ cb, double* __restrict__ free_vals) {
     double Amid[MF][MF], rmid[MF];
     {
+      double tl = T[MID - 1], tr = T[MID];
+      asm volatile("" : "+v"(tl), "+v"(tr));
       Pw<N, R> Pl, Pr;
-      Pl.set(T[MID - 1]);
-      Pr.set(T[MID]);
-      assemble(Pl, Pr, pos[MID - 1], pos[MID], pos[MID + 1], MID == 1, MID == S - 1, x0, xS,
-               Amid, rmid);
+      Pl.set(tl);
+      Pr.set(tr);
+      assemble(Pl, Pr, MID, MID == 1, MID == S - 1, Amid, rmid);
     }
+    {
+      int q = 0;
 #pragma unroll
-    for (int i = 0; i < MF; ++i) {
+      for (int i = 0; i < MF; ++i) {
 #pragma unroll
-      for (int j = 0; j <= i; ++j) Amid[i][j] = (Amid[i][j] - Tm[i][j]) - partner(Tm[i][j]);
-      rmid[i] = (rmid[i] - Rm[i]) - partner(Rm[i]);
-    }
-    // Both lanes form the same sum, in the same order, from the forward
-    // lane's point of view: make them bit-identical by taking the forward
-    // lane's result.
-#pragma unroll
-    for (int i = 0; i < MF; ++i) {
-#pragma unroll
-      for (int j = 0; j <= i; ++j) {
-        const double o = partner(Amid[i][j]);
-        Amid[i][j] = bw ? o : Amid[i][j];
+        for (int j = 0; j <= i; ++j, ++q) Amid[i][j] = (Amid[i][j] - tf[q]) - tb[q];
+        rmid[i] = (rmid[i] - rf[i]) - rb[i];
       }
-      const double o = partner(rmid[i]);
-      rmid[i] = bw ? o : rmid[i];
     }
     double xm[MF];
     {
@@ -380,143 +341,181 @@ struct PairSolve {
       ldlt<MF>(Amid, l, inv, pmin);
       ldlt_apply<MF>(l, inv, rmid, xm);
     }
-    const int np = (S - 1) * MF;
-    if (free_vals && !bw) {
+    constexpr int np = (S - 1) * MF;
+    if (free_vals && !BW) {
 #pragma unroll
       for (int i = 0; i < MF; ++i) free_vals[(b * D + d) * np + (MID - 1) * MF + i] = xm[i];
     }
-
-    // ---- back substitution outward, fused with the segments -----------------
-    // Segment j of the lane (j = 0 next to MID): near vertex x_near (x_MID,
-    // then the previous step's x), far vertex = the lane's step k = nsteps-1-j
-    // (x_far = z_k - S_k^-1 (G_k x_near)) or the fixed end when j = nsteps.
+    // Segment j of the half (j = 0 next to MID): near vertex x_near (x_MID,
+    // then the previous far vertex), far vertex = step k = NST-1-j
+    // (x_far = z_k - S_k^-1 (G_k x_near)) or the fixed end when j = NST.
     double acc = 0.0;
     double xn[MF];
 #pragma unroll
     for (int i = 0; i < MF; ++i) xn[i] = xm[i];
 #pragma unroll
     for (int j = 0; j < NSEG; ++j) {
-      const int nseg = bw ? S - MID : MID;
-      const bool seg_act = j < nseg;
-      const int kf = NFW - 1 - j, kb = NBW - 1 - j;  // the lane's far step (< 0: fixed end)
-      const bool far_fixed = bw ? kb < 0 : kf < 0;
+      const int k = NST - 1 - j;
+      // segment s between vertices s and s+1: forward far = s, near = s+1;
+      // backward near = s, far = s+1
+      const int s = BW ? MID + j : MID - 1 - j;
+      // Recompute the powers: CSE with the elimination's copies would keep
+      // them live across the whole kernel.
+      double ts = T[s];
+      asm volatile("" : "+v"(ts));
+      Pw<N, R> P;
+      P.set(ts);
       double xf[MF];
-      if (NST > 0) {
-        const int kfc = kf >= 0 ? kf : 0, kbc = kb >= 0 ? kb : 0;
-        // Powers of the far step's coupling segment: forward C_v with
-        // v = 1 + kf (segment v = MID-1-j .. its right = T[v]); backward
-        // C_(v-1)^T with v = S-1-kb (segment v-1 = MID + j).
-        double t = bw ? T[MID + j < S ? MID + j : S - 1] : T[MID - 1 - j >= 0 ? MID - 1 - j : 0];
-        asm volatile("" : "+v"(t));  // recompute the powers, do not keep the forward copies
-        Pw<N, R> Pc;
-        Pc.set(t);
+      if (k >= 0) {
+        // The step's coupling lives on segment s as well: forward C_v with
+        // v = s + 1 - 1 ... = the far vertex's right segment (s), backward
+        // C_(v-1)^T with v - 1 = s.
         double G[MF][MF];
-        coupling(bw, Pc, Pc, G);
-        double l[MF][MF], inv[MF], zk[MF];
+        coupling(P, G);
+        double l[MF][MF];
         int q = 0;
 #pragma unroll
         for (int i = 1; i < MF; ++i)
 #pragma unroll
-          for (int jj = 0; jj < i; ++jj) {
-            l[i][jj] = bw ? Lf[kbc][q] : Lf[kfc][q];
-            ++q;
-          }
-#pragma unroll
-        for (int i = 0; i < MF; ++i) {
-          inv[i] = bw ? If[kbc][i] : If[kfc][i];
-          zk[i] = bw ? z[kbc][i] : z[kfc][i];
-        }
+          for (int jj = 0; jj < i; ++jj) l[i][jj] = Lf[k >= 0 ? k : 0][q++];
         double gx[MF], w[MF];
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-          double s = 0.0;
+          double t = 0.0;
 #pragma unroll
-          for (int m = 0; m < MF; ++m) s = fma(G[i][m], xn[m], s);
-          gx[i] = s;
+          for (int m = 0; m < MF; ++m) t = fma(G[i][m], xn[m], t);
+          gx[i] = t;
         }
-        ldlt_apply<MF>(l, inv, gx, w);
+        ldlt_apply<MF>(l, If[k >= 0 ? k : 0], gx, w);
 #pragma unroll
-        for (int i = 0; i < MF; ++i) xf[i] = zk[i] - w[i];
+        for (int i = 0; i < MF; ++i) xf[i] = z[k >= 0 ? k : 0][i] - w[i];
       } else {
 #pragma unroll
-        for (int i = 0; i < MF; ++i) xf[i] = 0.0;
-      }
-      // Segment index, times and vertex data.
-      const int sf = MID - 1 - j, sb = MID + j;
-      const int s = bw ? sb : sf;
-      const double ts = bw ? T[sb < S ? sb : S - 1] : T[sf >= 0 ? sf : 0];
-      Pw<N, R> P;
-      P.set(ts);
-      double e_near[M], e_far[M];
-      // positions: forward near = vertex s+1, far = s; backward near = s,
-      // far = s+1
-      e_near[0] = bw ? pos[sb <= S ? sb : S] : pos[sf + 1 >= 0 ? sf + 1 : 0];
-      e_far[0] = bw ? pos[sb + 1 <= S ? sb + 1 : S] : pos[sf >= 0 ? sf : 0];
-#pragma unroll
-      for (int i = 0; i < MF; ++i) {
-        e_near[i + 1] = xn[i];
-        e_far[i + 1] = far_fixed ? (bw ? xS[i + 1] : x0[i + 1]) : xf[i];
+        for (int i = 0; i < MF; ++i) xf[i] = BW ? xS[i + 1] : x0[i + 1];
       }
       double e0[M], e1[M];
+      e0[0] = pos[s];
+      e1[0] = pos[s + 1];
 #pragma unroll
-      for (int i = 0; i < M; ++i) {
-        e0[i] = bw ? e_near[i] : e_far[i];
-        e1[i] = bw ? e_far[i] : e_near[i];
+      for (int i = 0; i < MF; ++i) {
+        e0[i + 1] = BW ? xn[i] : xf[i];
+        e1[i + 1] = BW ? xf[i] : xn[i];
       }
-      if (seg_act) {
-        acc += segment(e0, e1, P, cb ? cb + (s * D + d) * N : nullptr);
-        if (!far_fixed && free_vals) {
-          const int vfar = bw ? s + 1 : s;
+      acc += segment(e0, e1, P, cb ? cb + (s * D + d) * N : nullptr);
+      if (k >= 0 && free_vals) {
+        const int vfar = BW ? s + 1 : s;
 #pragma unroll
-          for (int i = 0; i < MF; ++i) free_vals[(b * D + d) * np + (vfar - 1) * MF + i] = xf[i];
-        }
+        for (int i = 0; i < MF; ++i) free_vals[(b * D + d) * np + (vfar - 1) * MF + i] = xf[i];
       }
 #pragma unroll
       for (int i = 0; i < MF; ++i) xn[i] = xf[i];
     }
-    *cost_part = acc;
-    return pmin > 0.0 ? 0 : 2;
+    return acc;
+  }
+
+  // NaN coefficients of the half's segments (bad segment time).
+  __device__ void write_bad(int d, double* __restrict__ cb) const {
+    if (!cb) return;
+#pragma unroll
+    for (int j = 0; j < NSEG; ++j) {
+      const int s = BW ? MID + j : MID - 1 - j;
+#pragma unroll
+      for (int i = 0; i < N; ++i) cb[(s * D + d) * N + i] = NAN;
+    }
   }
 };
 
-}  // namespace lane2
-
-// Lanes (trajectory t, dimension d, half h) = t * 2D + 2d + h; 10
-// trajectories per wavefront at D = 3.
-template <int N, int R, int D, int S>
-__global__ __launch_bounds__(kWave) void linear_lane2_kernel(
+// One wave's half of the workgroup: wave 0 forward, wave 1 backward, same
+// lane -> (trajectory, dimension) map.  The two exchange their Schur terms
+// at the middle vertex through LDS; wave 1 then hands its cost shares and
+// status to wave 0, which forms the per-trajectory cost and status.
+template <int N, int R, int D, int S, bool BW>
+__device__ __attribute__((always_inline)) inline void lane2_half(
     int64_t B, const double* __restrict__ fixed_vals, const double* __restrict__ times,
     double* __restrict__ coeffs, double* __restrict__ cost, double* __restrict__ free_vals,
-    int32_t* __restrict__ status, SelectArgs sel) {
-  constexpr int LPT = 2 * D;        // lanes per trajectory
-  constexpr int TPW = kWave / LPT;  // trajectories per wavefront
-  const int lane = threadIdx.x;
-  const int tl = lane / LPT, r = lane - tl * LPT;
-  const int d = r >> 1, h = r & 1;
+    int32_t* __restrict__ status, const SelectArgs& sel, double* xch, double* cxch, int* sxch) {
+  using H = Half<N, R, D, S, BW>;
+  constexpr int NT = H::NT, MF = H::MF;
+  constexpr int TPW = kWave / D;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int tl = lane / D, d = lane - tl * D;
   const int64_t b = static_cast<int64_t>(blockIdx.x) * TPW + tl;
   const bool act = tl < TPW && b < B;
-  double cpart = 0.0;
-  int st = 0;
-  // Lanes of a pair must run together (DPP exchange at the middle vertex):
-  // inactive lanes run a valid dummy problem (trajectory 0) and discard it.
-  {
-    double dummy = 0.0;
-    st = lane2::PairSolve<N, R, D, S>::run(act ? b : 0, act ? d : 0, h, fixed_vals, times,
-                                           act ? coeffs : nullptr, act ? free_vals : nullptr,
-                                           act ? &cpart : &dummy);
-  }
-  double tot = 0.0;
+  // Inactive lanes run trajectory 0 with no outputs: every lane reaches the
+  // barriers with defined data.
+  const int64_t bb = act ? b : 0;
+  H h;
+  h.load(bb, d, fixed_vals, times);
+  h.eliminate();
+  double tm[NT], rm[MF];
+  h.terms(tm, rm);
+  constexpr int W = NT + MF;
+  double* mine = xch + (BW ? 1 : 0) * W * kWave;
+  double* other = xch + (BW ? 0 : 1) * W * kWave;
 #pragma unroll
-  for (int p = 0; p < LPT; ++p) tot += __shfl(cpart, tl * LPT + p);
+  for (int q = 0; q < NT; ++q) mine[q * kWave + lane] = tm[q];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) mine[(NT + i) * kWave + lane] = rm[i];
+  __syncthreads();
+  double to[NT], ro[MF];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) to[q] = other[q * kWave + lane];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) ro[i] = other[(NT + i) * kWave + lane];
+  double* cb = (act && coeffs) ? coeffs + b * S * D * N : nullptr;
+  double* fv = act ? free_vals : nullptr;
+  double part;
+  if (BW)
+    part = h.finish(bb, d, to, ro, tm, rm, cb, fv);
+  else
+    part = h.finish(bb, d, tm, rm, to, ro, cb, fv);
+  int st = h.bad ? 1 : (h.pmin > 0.0 ? 0 : 2);
+  if (h.bad) {
+    h.write_bad(d, cb);
+    part = NAN;
+  }
+  if (BW) {
+    cxch[lane] = part;
+    sxch[lane] = st;
+  }
+  __syncthreads();
+  if (BW) return;
+  part += cxch[lane];
+  st = max(st, sxch[lane]);
+  double tot = 0.0;
   int stt = 0;
 #pragma unroll
-  for (int p = 0; p < LPT; ++p) stt = max(stt, __shfl(st, tl * LPT + p));
-  if (act && r == 0) {
+  for (int p = 0; p < D; ++p) {
+    tot += __shfl(part, tl * D + p);
+    stt = max(stt, __shfl(st, tl * D + p));
+  }
+  if (act && d == 0) {
     if (cost) cost[b] = tot;
     if (status)
       status[b] = stt == 1 ? MTG_TRAJ_BAD_TIME : (stt == 2 ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
   }
-  if (sel.out) select_epilogue(sel, tot, act && r == 0 ? b : -1, blockIdx.x, gridDim.x, B);
+  if (sel.out) select_partial(sel, tot, act && d == 0 ? b : -1, blockIdx.x);
+}
+
+}  // namespace lane2
+
+// Workgroup = 2 waves (forward, backward) over 21 trajectories x 3
+// dimensions; the direction is wave-uniform.
+template <int N, int R, int D, int S>
+__global__ __launch_bounds__(2 * kWave) void linear_lane2_kernel(
+    int64_t B, const double* __restrict__ fixed_vals, const double* __restrict__ times,
+    double* __restrict__ coeffs, double* __restrict__ cost, double* __restrict__ free_vals,
+    int32_t* __restrict__ status, SelectArgs sel) {
+  using H = lane2::Half<N, R, D, S, false>;
+  __shared__ double xch[2 * (H::NT + H::MF) * kWave];
+  __shared__ double cxch[kWave];
+  __shared__ int sxch[kWave];
+  if (threadIdx.x < kWave)
+    lane2::lane2_half<N, R, D, S, false>(B, fixed_vals, times, coeffs, cost, free_vals, status,
+                                         sel, xch, cxch, sxch);
+  else
+    lane2::lane2_half<N, R, D, S, true>(B, fixed_vals, times, coeffs, cost, free_vals, status,
+                                        sel, xch, cxch, sxch);
 }
 
 namespace {
@@ -525,17 +524,17 @@ template <int N, int R, int D, int S>
 hipError_t launch_lane2(int64_t B, const double* df, const double* times, double* coeffs,
                         double* cost, double* free_vals, int32_t* status, hipStream_t st,
                         const SelectArgs& sel) {
-  constexpr int TPW = kWave / (2 * D);
+  constexpr int TPW = kWave / D;
   const int64_t blocks = (B + TPW - 1) / TPW;
   hipLaunchKernelGGL((linear_lane2_kernel<N, R, D, S>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kWave), 0, st, B, df, times, coeffs, cost, free_vals, status, sel);
+                     dim3(2 * kWave), 0, st, B, df, times, coeffs, cost, free_vals, status, sel);
   return hipGetLastError();
 }
 
 }  // namespace
 
 int64_t lane2_blocks(int64_t B) {
-  constexpr int TPW = kWave / 6;
+  constexpr int TPW = kWave / 3;
   return (B + TPW - 1) / TPW;
 }
 

@@ -9,7 +9,6 @@
 
 #include <cmath>
 
-#include "mtg_select_device.h"
 #include "mtg_std_device.h"
 
 namespace mtg {
@@ -22,7 +21,7 @@ template <int N, int R, int D>
 __global__ __launch_bounds__(kWave) void linear_std_kernel(
     int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     const double* __restrict__ times, double* __restrict__ coeffs, double* __restrict__ cost,
-    double* __restrict__ free_vals, int32_t* __restrict__ status, int64_t B, SelectArgs sel) {
+    double* __restrict__ free_vals, int32_t* __restrict__ status) {
   using Sv = stdp::Solver<N, R, D>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int64_t b = blockIdx.x;
@@ -54,7 +53,6 @@ __global__ __launch_bounds__(kWave) void linear_std_kernel(
     for (int i = lane; i < per; i += kWave) coeffs[b * per + i] = NAN;
     if (cost && lane == 0) cost[b] = NAN;
     if (status && lane == 0) status[b] = MTG_TRAJ_BAD_TIME;
-    if (sel.out) select_epilogue(sel, NAN, lane == 0 ? b : -1, b, B, B);
     return;
   }
   sv.assemble(tab);
@@ -72,32 +70,28 @@ __global__ __launch_bounds__(kWave) void linear_std_kernel(
     }
   }
   if (status && lane == 0) status[b] = not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK;
-  // Fused selection (the shard's argmin; one trajectory per workgroup).
-  if (sel.out) select_epilogue(sel, J, lane == 0 ? b : -1, b, B, B);
   MTG_STAMP(6);
 }
 
 template <int N, int R, int D>
 static hipError_t launch_std_nrd(int S, int64_t B, const double* tab, const double* df,
                                  const double* times, double* coeffs, double* cost,
-                                 double* free_vals, int32_t* status, hipStream_t st,
-                                 const SelectArgs& sel) {
+                                 double* free_vals, int32_t* status, hipStream_t st) {
   const size_t lds = linear_std_lds_bytes(N, S, D);
   hipLaunchKernelGGL((linear_std_kernel<N, R, D>), dim3(static_cast<unsigned>(B)), dim3(kWave),
-                     lds, st, S, tab, df, times, coeffs, cost, free_vals, status, B, sel);
+                     lds, st, S, tab, df, times, coeffs, cost, free_vals, status);
   return hipGetLastError();
 }
 
 template <int N, int R>
 static hipError_t launch_std_nr(int D, int S, int64_t B, const double* tab, const double* df,
                                 const double* times, double* coeffs, double* cost,
-                                double* free_vals, int32_t* status, hipStream_t st,
-                                const SelectArgs& sel) {
+                                double* free_vals, int32_t* status, hipStream_t st) {
   switch (D) {
-    case 1: return launch_std_nrd<N, R, 1>(S, B, tab, df, times, coeffs, cost, free_vals, status, st, sel);
-    case 2: return launch_std_nrd<N, R, 2>(S, B, tab, df, times, coeffs, cost, free_vals, status, st, sel);
-    case 3: return launch_std_nrd<N, R, 3>(S, B, tab, df, times, coeffs, cost, free_vals, status, st, sel);
-    case 4: return launch_std_nrd<N, R, 4>(S, B, tab, df, times, coeffs, cost, free_vals, status, st, sel);
+    case 1: return launch_std_nrd<N, R, 1>(S, B, tab, df, times, coeffs, cost, free_vals, status, st);
+    case 2: return launch_std_nrd<N, R, 2>(S, B, tab, df, times, coeffs, cost, free_vals, status, st);
+    case 3: return launch_std_nrd<N, R, 3>(S, B, tab, df, times, coeffs, cost, free_vals, status, st);
+    case 4: return launch_std_nrd<N, R, 4>(S, B, tab, df, times, coeffs, cost, free_vals, status, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -106,12 +100,12 @@ template <int N>
 static hipError_t launch_std_n(int r, int D, int S, int64_t B, const double* tab,
                                const double* df, const double* times, double* coeffs,
                                double* cost, double* free_vals, int32_t* status,
-                               hipStream_t st, const SelectArgs& sel) {
+                               hipStream_t st) {
 #define MTG_STD_R(RR)                                                                  \
   case RR:                                                                            \
     if constexpr (RR < N / 2)                                                         \
       return launch_std_nr<N, RR>(D, S, B, tab, df, times, coeffs, cost, free_vals,   \
-                                  status, st, sel);                                   \
+                                  status, st);                                        \
     return hipErrorInvalidValue;
   switch (r) {
     MTG_STD_R(0)
@@ -127,14 +121,13 @@ static hipError_t launch_std_n(int r, int D, int S, int64_t B, const double* tab
 
 hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
                                    const double* times, double* coeffs, double* cost,
-                                   double* free_vals, int32_t* status, hipStream_t st,
-                                   const SelectArgs& sel) {
+                                   double* free_vals, int32_t* status, hipStream_t st) {
   switch (pl.N) {
-    case 4: return launch_std_n<4>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st, sel);
-    case 6: return launch_std_n<6>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st, sel);
-    case 8: return launch_std_n<8>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st, sel);
-    case 10: return launch_std_n<10>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st, sel);
-    case 12: return launch_std_n<12>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st, sel);
+    case 4: return launch_std_n<4>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
+    case 6: return launch_std_n<6>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
+    case 8: return launch_std_n<8>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
+    case 10: return launch_std_n<10>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
+    case 12: return launch_std_n<12>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
     default: return hipErrorInvalidValue;
   }
 }

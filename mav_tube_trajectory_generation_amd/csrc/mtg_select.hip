@@ -1,7 +1,7 @@
 // mtg_select.hip — the selection step of the multi-GPU path (SURVEY.md §8e,
 // BASELINE config 4: shards solve independently, the ranks all-gather their
 // costs for selection).  Each rank reduces its shard to one (cost, global
-// index, rank) triple with select_local_kernel; after the all-gather of the
+// index, rank) triple with select_reduce_kernel; after the all-gather of the
 // triples (RCCL over xGMI, 24 B per rank) select_global_kernel picks the
 // winner.  One launch each, so the whole step stays a handful of launches
 // that a HIP graph can hold.
@@ -17,50 +17,61 @@
 #include <cmath>
 
 #include "mtg_internal.h"
+#include "mtg_select_device.h"
 
 namespace mtg {
 
-constexpr int kSelBlock = 1024;
+constexpr int kSelBlock = 256;
 
-__global__ __launch_bounds__(kSelBlock) void select_local_kernel(const double* __restrict__ costs,
-                                                                 int64_t count, int64_t start,
-                                                                 int rank, double* __restrict__ out) {
-  __shared__ double vs[kSelBlock];
-  __shared__ int64_t is[kSelBlock];
-  const int tid = threadIdx.x;
-  double best = HUGE_VAL;
-  int64_t bi = count > 0 ? 0 : -1;
-  for (int64_t i = tid; i < count; i += kSelBlock) {
-    double v = costs[i];
-    if (v != v) v = HUGE_VAL;
-    if (v < best || (v == best && i < bi)) {
-      best = v;
-      bi = i;
+// (cost, index) pairs c[0..n), idx[0..n) (idx == nullptr: index = position)
+// to the shard's triple.  One workgroup: each thread scans a strided share
+// with eight loads in flight, then a wave minimum by shuffles and one LDS
+// step across the four waves.
+__global__ __launch_bounds__(kSelBlock) void select_reduce_kernel(
+    const double* __restrict__ c, const int64_t* __restrict__ idx, int64_t n, int64_t count,
+    int64_t start, int rank, double* __restrict__ out) {
+  __shared__ double ws_c[kSelBlock / 64];
+  __shared__ int64_t ws_i[kSelBlock / 64];
+  double bc = HUGE_VAL;
+  int64_t bi = INT64_MAX;
+  constexpr int kU = 8;
+  for (int64_t k0 = threadIdx.x; k0 < n; k0 += kSelBlock * kU) {
+    double pc[kU];
+    int64_t pi[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t k = k0 + u * kSelBlock;
+      pc[u] = k < n ? c[k] : HUGE_VAL;
+      pi[u] = k < n ? (idx ? idx[k] : k) : INT64_MAX;
     }
-  }
-  if (bi < 0 && count > 0) bi = count;  // no element seen by this thread
-  vs[tid] = best;
-  is[tid] = (count > 0 && tid >= count) ? count : bi;
-  __syncthreads();
-  for (int w = kSelBlock / 2; w > 0; w >>= 1) {
-    if (tid < w) {
-      const double v = vs[tid + w];
-      const int64_t j = is[tid + w];
-      if (v < vs[tid] || (v == vs[tid] && j < is[tid])) {
-        vs[tid] = v;
-        is[tid] = j;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const double v = pc[u] != pc[u] ? HUGE_VAL : pc[u];  // NaN never wins
+      if (sel_better(v, pi[u], bc, bi)) {
+        bc = v;
+        bi = pi[u];
       }
     }
-    __syncthreads();
   }
-  if (tid == 0) {
-    const bool empty = count <= 0;
-    // All +inf: the first element (a single-process argmin's answer).
-    const int64_t idx = empty ? -1 : (is[0] >= count ? 0 : is[0]);
-    out[0] = empty ? HUGE_VAL : vs[0];
-    out[1] = empty ? -1.0 : static_cast<double>(idx + start);
-    out[2] = static_cast<double>(rank);
+  sel_wave_min(bc, bi);
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    ws_c[w] = bc;
+    ws_i[w] = bi;
   }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+#pragma unroll
+  for (int q = 1; q < kSelBlock / 64; ++q)
+    if (sel_better(ws_c[q], ws_i[q], bc, bi)) {
+      bc = ws_c[q];
+      bi = ws_i[q];
+    }
+  const bool empty = count <= 0;
+  const int64_t at = (bi >= count || bi < 0) ? 0 : bi;  // all +inf: the first index
+  out[0] = empty ? HUGE_VAL : bc;
+  out[1] = empty ? -1.0 : static_cast<double>(at + start);
+  out[2] = static_cast<double>(rank);
 }
 
 __global__ void select_global_kernel(const double* __restrict__ triples, int world,
@@ -83,8 +94,13 @@ __global__ void select_global_kernel(const double* __restrict__ triples, int wor
 
 hipError_t launch_select_local(const double* costs, int64_t count, int64_t start, int rank,
                                double* out, hipStream_t st) {
-  hipLaunchKernelGGL(select_local_kernel, dim3(1), dim3(kSelBlock), 0, st, costs, count, start,
-                     rank, out);
+  return launch_select_reduce(costs, nullptr, count, count, start, rank, out, st);
+}
+
+hipError_t launch_select_reduce(const double* cost, const int64_t* idx, int64_t n, int64_t count,
+                                int64_t start, int rank, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(select_reduce_kernel, dim3(1), dim3(kSelBlock), 0, st, cost, idx,
+                     n > 0 ? n : 0, count, start, rank, out);
   return hipGetLastError();
 }
 

@@ -1,11 +1,15 @@
 // mtg_select_device.h — the selection step of the multi-GPU path (SURVEY.md
 // 8e) fused into the epilogue of a solve kernel: every workgroup publishes
-// the (cost, index) of the best trajectory it solved, and the last workgroup
-// to finish (a device-scope atomic counter) reduces those partials to the
-// shard's (cost, global index, rank) triple, with the ordering of
-// select_local_kernel (mtg_select.hip): NaN never wins, the lowest index wins
-// ties, all +inf gives the shard's first index.  It replaces the separate
-// single-workgroup launch that scanned the whole shard after the solve.
+// the (cost, index) of the best trajectory it solved, and one small launch
+// reduces those partials to the shard's (cost, global index, rank) triple,
+// with the ordering of select_local_kernel (mtg_select.hip): NaN never wins,
+// the lowest index wins ties, all +inf gives the shard's first index.
+//
+// A last-workgroup-done reduction (release fence + device-scope atomic
+// counter in every workgroup) was measured first: on gfx950 the per-
+// workgroup fence and same-address atomic serialise at ~40 ns per workgroup
+// (24.6 us over the solve at 1,024 workgroups, 131 us at 3,121), far more
+// than the second launch costs.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,58 +39,20 @@ __device__ inline void sel_wave_min(double& c, int64_t& i) {
   }
 }
 
-// Called by all 64 threads of every workgroup (one wave) after the
+// Called by all 64 threads of the first wave of every workgroup after the
 // workgroup's costs are written: (c, i) is this lane's candidate (i < 0:
-// none; NaN allowed), `block` the workgroup's partial slot, `nblocks` the
-// grid size.  The last workgroup writes sel.out = (cost, start + index, rank)
-// and re-arms the counter.
-__device__ inline void select_epilogue(const SelectArgs& sel, double c, int64_t i, int64_t block,
-                                       int64_t nblocks, int64_t count) {
-  __shared__ int last;
+// none; NaN allowed), `block` the workgroup's partial slot.  Lane 0 writes
+// the workgroup's best (cost, index) to the partial arrays; the reduction of
+// the partials is a separate one-workgroup launch (select_partials_kernel,
+// mtg_select.hip) on the same stream, so the kernel boundary orders the
+// partials before it without any fence or atomic.
+__device__ inline void select_partial(const SelectArgs& sel, double c, int64_t i, int64_t block) {
   if (c != c || i < 0) c = HUGE_VAL;
   if (i < 0) i = INT64_MAX;
   sel_wave_min(c, i);
-  if (threadIdx.x == 0) {
+  if ((threadIdx.x & 63) == 0) {
     sel.part_cost[block] = c;
     sel.part_idx[block] = i;
-    __threadfence();  // the partial is visible device-wide before the count
-    const unsigned prev = atomicAdd(sel.counter, 1u);
-    last = prev == static_cast<unsigned>(nblocks - 1) ? 1 : 0;
-  }
-  __syncthreads();
-  if (!last) return;
-  // Acquire side: the agent-scope fence invalidates this CU's vector L1, so
-  // the plain loads below read the other workgroups' partials from L2.  They
-  // are independent, so eight are issued before any is used (device-scope
-  // atomic loads here were serialised by the compiler: ~1 us each).
-  __threadfence();
-  double bc = HUGE_VAL;
-  int64_t bi = INT64_MAX;
-  constexpr int kU = 8;
-  for (int64_t k0 = threadIdx.x; k0 < nblocks; k0 += 64 * kU) {
-    double pc[kU];
-    int64_t pi[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t k = k0 + u * 64;
-      pc[u] = k < nblocks ? sel.part_cost[k] : HUGE_VAL;
-      pi[u] = k < nblocks ? sel.part_idx[k] : INT64_MAX;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (sel_better(pc[u], pi[u], bc, bi)) {
-        bc = pc[u];
-        bi = pi[u];
-      }
-  }
-  sel_wave_min(bc, bi);
-  if (threadIdx.x == 0) {
-    const bool empty = count <= 0;
-    const int64_t idx = (bi >= count || bi < 0) ? 0 : bi;  // all +inf: the first index
-    sel.out[0] = empty ? HUGE_VAL : bc;
-    sel.out[1] = empty ? -1.0 : static_cast<double>(idx + sel.start);
-    sel.out[2] = static_cast<double>(sel.rank);
-    *sel.counter = 0u;  // every workgroup has counted: re-arm for the next launch
   }
 }
 

@@ -96,6 +96,14 @@ double relErr(const std::vector<double>& a, const std::vector<double>& b) {
 }
 double relErr(double a, double b) { return std::fabs(a - b) / std::max(std::fabs(b), 1e-300); }
 
+// Row-major copy of a (column-major, as Eigen) MatrixXd, the oracle's order.
+std::vector<double> rowMajor(const MatrixXd& m) {
+  std::vector<double> r;
+  for (long i = 0; i < m.rows(); ++i)
+    for (long j = 0; j < m.cols(); ++j) r.push_back(m(i, j));
+  return r;
+}
+
 // Dense oracle vertex form (mask[v*K+k], vals[(v*K+k)*D+d]).
 struct Dense {
   int S, D, K;
@@ -208,12 +216,31 @@ TEST(host, AMatrixInversion) {
   }
 }
 
+// MatrixXd stores column-major as Eigen's default MatrixXd does: data()
+// lists column 0 first, so Eigen-style .data() copies keep their meaning.
+TEST(host, MatrixXdColumnMajor) {
+  MatrixXd m(2, 3);
+  for (long i = 0; i < 2; ++i)
+    for (long j = 0; j < 3; ++j) m(i, j) = 10.0 * i + j;
+  const double want[6] = {0, 10, 1, 11, 2, 12};
+  for (int k = 0; k < 6; ++k) EXPECT_TRUE(m.data()[k] == want[k]);
+  const MatrixXd t = m.transpose();
+  EXPECT_TRUE(t.rows() == 3 && t.cols() == 2 && t(2, 1) == 12.0 && t.data()[1] == 1.0);
+  // the mapping matrix A(T) (linear_impl:132-150): row 0 is (1, 0, ..., 0)
+  // and column 0 is (1, 0, 0, 0, 0, 1, 0, 0, 0, 0) at T = 1, so data()[0..9]
+  // is column 0
+  PolynomialOptimization<10>::SquareMatrix A;
+  PolynomialOptimization<10>::setupMappingMatrix(1.0, &A);
+  for (int i = 0; i < 10; ++i) EXPECT_TRUE(A.data()[i] == A(i, 0));
+  EXPECT_TRUE(A.data()[5] == 1.0 && A.data()[10] == 0.0);
+}
+
 TEST(host, QuadraticCostJacobianMatchesOracle) {
   for (int r = 0; r < 5; ++r)
     for (double t : {0.1, 1.0, 3.7, 12.0}) {
       PolynomialOptimization<10>::SquareMatrix Q;
       PolynomialOptimization<10>::computeQuadraticCostJacobian(r, t, &Q);
-      std::vector<double> q(100), got(Q.data(), Q.data() + 100);
+      std::vector<double> q(100), got = rowMajor(Q);
       orc_segment_matrices(10, r, t, q.data(), nullptr, nullptr, nullptr);
       EXPECT_LE(relErr(got, q), 1e-14);
     }
@@ -226,8 +253,8 @@ TEST(host, MappingMatrixMatchesOracle) {
     PolynomialOptimization<10>::invertMappingMatrix(A, &Ai);
     std::vector<double> a(100), ai(100);
     orc_segment_matrices(10, 4, t, nullptr, a.data(), ai.data(), nullptr);
-    EXPECT_LE(relErr(std::vector<double>(A.data(), A.data() + 100), a), 0.0);
-    EXPECT_LE(relErr(std::vector<double>(Ai.data(), Ai.data() + 100), ai), 1e-13);
+    EXPECT_LE(relErr(rowMajor(A), a), 0.0);
+    EXPECT_LE(relErr(rowMajor(Ai), ai), 1e-13);
   }
 }
 
@@ -384,14 +411,18 @@ TEST(gpu, AccessorsMatchOracle) {
   opt.getA(&gA);
   opt.getAInverse(&gAi);
   opt.getMpinv(&gMp);
-  auto vec = [](const MatrixXd& m) {
-    return std::vector<double>(m.data(), m.data() + m.rows() * m.cols());
-  };
-  EXPECT_LE(relErr(vec(gR), R), 1e-9);
-  EXPECT_TRUE(vec(gM) == M);
-  EXPECT_LE(relErr(vec(gA), A), 1e-15);
-  EXPECT_LE(relErr(vec(gAi), Ai), 1e-12);
-  EXPECT_TRUE(vec(gMp) == Mp);
+  EXPECT_LE(relErr(rowMajor(gR), R), 1e-9);
+  EXPECT_TRUE(rowMajor(gM) == M);
+  EXPECT_LE(relErr(rowMajor(gA), A), 1e-15);
+  EXPECT_LE(relErr(rowMajor(gAi), Ai), 1e-12);
+  EXPECT_TRUE(rowMajor(gMp) == Mp);
+  // data() lists the entries column by column, as Eigen's getM().data() does
+  bool col_major = true;
+  for (size_t i = 0; i < na; ++i)
+    for (size_t j = 0; j < n; ++j) col_major = col_major && gM.data()[j * na + i] == M[i * n + j];
+  for (size_t i = 0; i < nc; ++i)
+    for (size_t j = 0; j < nc; ++j) col_major = col_major && gA.data()[j * nc + i] == gA(i, j);
+  EXPECT_TRUE(col_major);
 }
 
 TEST(gpu, StaleCostAfterTimeUpdate) {

@@ -119,11 +119,11 @@ def test_select_best_device_one_rank_rccl(ctx, dev):
 
 @pytest.mark.parametrize("kernel", ["standard", "lane", "lane_pair", "generic"])
 def test_solve_select_fused(ctx, dev, kernel):
-    """mtg_linear_solve_select: the shard's triple formed in the solve's own
-    launch (last-workgroup reduction of per-workgroup partials) equals the
-    selection rule on the costs the same launch wrote, with NaN costs (bad
-    times), ties (duplicated trajectories) and repeated launches on one
-    workspace (the counter re-arms); inside a captured graph as well."""
+    """mtg_linear_solve_select: the shard's triple (lane kernels: per-
+    workgroup partials from the solve's epilogue, then one reduction launch)
+    equals the selection rule on the costs the same solve wrote, with NaN
+    costs (bad times), ties (duplicated trajectories) and repeated launches on
+    one uninitialised workspace; inside a captured graph as well."""
     import mav_tube_trajectory_generation_amd as mtg
     N, D, S, B = 10, 3, 10, 3000
     mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=400)
@@ -138,6 +138,7 @@ def test_solve_select_fused(ctx, dev, kernel):
     times[5, 2] = -1.0  # a bad time: NaN cost, never selected
     fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
     ws = plan.select_workspace(B, dev)
+    ws.fill_(0xFF)  # no initialisation needed
     for rep in range(3):
         out = plan.solve_select(fd, td, 1000, 2, ws)
         torch.cuda.synchronize(dev)

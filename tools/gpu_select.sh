@@ -4,7 +4,7 @@
 # (65536) batches.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_select_gpu.py tests/test_linear_gpu.py tests/test_linear_lane_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_select.log 2>&1 || { echo "pytest failed"; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_select_gpu.py tests/test_linear_gpu.py tests/test_linear_lane_gpu.py tests/test_cpp_api.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_select.log 2>&1 || { echo "pytest failed"; exit 1; }
 echo "pytest ok"
 timeout -k 10 300 python bench.py > gpurun_out/bench_linear.json 2> gpurun_out/bench_linear.err || exit 1
 for k in lane lane_pair; do
