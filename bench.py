@@ -300,21 +300,18 @@ def main():
         out = plan.solve(fixed_d, times_d, free=False)
         shard_start = shard_range(global_batch, world, rank)[0]
         sel_ws = plan.select_workspace(B, dev)
-        sel_res = torch.empty(3, dtype=torch.float64, device=dev)
 
         def step_selected():
-            # The solve with the shard's argmin fused into its launch, then
+            # The solve with the shard's argmin (lane kernels: per-workgroup
+            # partials from the solve's epilogue, one reduction launch), then
             # (world > 1) the RCCL all-gather of the triples and the global
-            # argmin kernel; on one GPU without a process group the all-gather
-            # of one triple is the identity and only the global kernel runs.
+            # argmin kernel.  On one GPU without a process group the
+            # all-gather and the global argmin of one triple are the identity:
+            # the shard's triple is the winner.
             plan.solve_select(fixed_d, times_d, shard_start, rank, sel_ws, out=out)
             if select:
                 return select_best_device(None, global_batch, local_triple=out["triple"])
-            from mav_tube_trajectory_generation_amd._abi import check as _chk, lib as _lib
-            from mav_tube_trajectory_generation_amd.batch import _ptr, _stream
-            _chk(_lib().mtg_select_global(_ptr(out["triple"]), 1, _ptr(sel_res), _stream(dev)),
-                 "mtg_select_global")
-            return sel_res
+            return out["triple"]
 
         def step():
             if select:

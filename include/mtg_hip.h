@@ -92,17 +92,19 @@ int mtg_plan_destroy(mtg_plan* plan);
  * createRandomVertices / makeStartOrEnd, vertex.cpp:27-82, 147-153) and
  * 2 <= S <= 64, else the generic kernel.  Among the standard-pattern kernels
  * it picks by batch size: STANDARD (one wavefront per trajectory, lowest
- * latency) below 4096 trajectories, LANE (one (trajectory, dimension) per
- * lane, highest throughput) from 4096; LANE covers N = 10, r = 4, D = 3,
- * 2 <= S <= 12.  GENERIC forces the generic kernel (parity cross-checks);
- * STANDARD / LANE fail with MTG_ERR_UNSUPPORTED where they do not apply.
- * mtg_plan_kernel returns the forced kernel, or for AUTO the wavefront
- * kernel (GENERIC or STANDARD); mtg_plan_kernel_for_batch the kernel a
- * solve of B trajectories runs.  The time, free-derivative and sampling
- * entry points treat LANE like STANDARD.  LANE_PAIR (same coverage as LANE)
- * gives each (trajectory, dimension) two lanes that eliminate the vertex
- * chain from both ends toward the middle vertex (a twisted factorisation):
- * half the dependent chain and twice the wavefronts of LANE. */
+ * latency) below 4096 trajectories, LANE_PAIR from 4096.  LANE gives each
+ * (trajectory, dimension) one lane that walks the whole vertex chain;
+ * LANE_PAIR gives it two lanes in two wavefronts of one workgroup that
+ * eliminate the chain from both ends toward the middle vertex (a twisted
+ * factorisation, Schur terms exchanged through LDS): half the chain per lane
+ * (13.8 vs 15.6 us at B = 8192, equal at 65536).  Both cover N = 10, r = 4,
+ * D = 3, 2 <= S <= 12.  GENERIC forces the generic kernel (parity
+ * cross-checks); STANDARD / LANE / LANE_PAIR fail with MTG_ERR_UNSUPPORTED
+ * where they do not apply.  mtg_plan_kernel returns the forced kernel, or
+ * for AUTO the wavefront kernel (GENERIC or STANDARD);
+ * mtg_plan_kernel_for_batch the kernel a solve of B trajectories runs.  The
+ * time, free-derivative and sampling entry points treat LANE and LANE_PAIR
+ * like STANDARD. */
 enum {
   MTG_KERNEL_AUTO = 0,
   MTG_KERNEL_GENERIC = 1,

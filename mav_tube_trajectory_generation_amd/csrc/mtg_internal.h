@@ -44,7 +44,8 @@ int64_t select_partials(const PlanDev& pl, int64_t B);
 constexpr int kMaxStdS = 64;
 // Lane linear solve for large batches (mtg_linear_lane.hip): one
 // (trajectory, dimension) per lane; standard pattern, N = 10, r = 4, D = 3,
-// 2 <= S <= kMaxLaneS.  AUTO runs it from kLaneMinBatch trajectories.
+// 2 <= S <= kMaxLaneS.  AUTO runs the two-lane variant (mtg_linear_lane2.hip)
+// from kLaneMinBatch trajectories.
 constexpr int kMaxLaneS = 12;
 constexpr int64_t kLaneMinBatch = 4096;
 struct PlanDev;

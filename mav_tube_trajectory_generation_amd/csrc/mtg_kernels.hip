@@ -487,7 +487,7 @@ static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* 
 int linear_kernel_for_batch(const PlanDev& pl, int64_t B) {
   if (pl.kernel != MTG_KERNEL_AUTO) return pl.kernel;
   if (!pl.std_pattern) return MTG_KERNEL_GENERIC;
-  if (has_linear_lane(pl) && B >= kLaneMinBatch) return MTG_KERNEL_LANE;
+  if (has_linear_lane(pl) && B >= kLaneMinBatch) return MTG_KERNEL_LANE_PAIR;
   // The same test launch_linear_solve applies (std_pattern already implies
   // S <= kMaxStdS), so the reported kernel is the one that runs.
   return use_std_kernel(pl) ? MTG_KERNEL_STANDARD : MTG_KERNEL_GENERIC;

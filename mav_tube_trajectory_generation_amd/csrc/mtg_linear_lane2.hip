@@ -4,22 +4,23 @@
 //
 // linear_lane_kernel (mtg_linear_lane.hip) gives every (trajectory,
 // dimension) one lane, which walks the whole block recurrence over the S-1
-// intermediate vertices: a launch lasts one lane's chain (~12 us), and at
-// one config-4 shard (B = 8192) the 8192 x 3 lanes fill only 384 of the
-// 1024 SIMDs.  Here the pair of lanes (lane ^ 1) splits the chain at the
-// middle vertex m = S/2: the even lane eliminates forward over
-// v = 1 .. m-1, the odd lane backward over v = S-1 .. m+1 (the same
-// recurrence on the reversed chain, whose couplings are the transposed
-// blocks C_(v-1)^T), so each lane walks half the vertices.  The two lanes
-// then exchange their Schur terms at m through DPP (quad_perm [1,0,3,2]),
-// both solve the middle block, and each back-substitutes its half outward,
-// fused with the coefficients and cost of its half's segments.  The chain
-// halves and twice as many waves cover the chip.
+// intermediate vertices: a launch lasts one lane's chain, and at one
+// config-4 shard (B = 8192) the 8192 x 3 lanes fill only 384 of the 1024
+// SIMDs.  Here a workgroup of two wavefronts covers 21 trajectories x 3
+// dimensions twice: wave 0 eliminates each chain forward over
+// v = 1 .. m-1, wave 1 backward over v = S-1 .. m+1 (the same recurrence on
+// the reversed chain, whose couplings are the transposed blocks C_(v-1)^T),
+// m = S/2.  The waves exchange their Schur terms at m through LDS (one
+// barrier), both solve the middle block in the same operation order
+// (bit-identical middle values), and each back-substitutes its half
+// outward, fused with the coefficients and cost of its half's segments;
+// wave 1 hands its cost shares to wave 0 (second barrier), which writes the
+// per-trajectory cost, status and the selection partial.
 //
-// Both lanes run ONE instruction stream: every difference between the two
-// directions is data (the lane's segment times, neighbour positions and
-// coupling orientation are chosen by selects between compile-time-indexed
-// registers), so there is no divergence.
+// The direction is a template parameter of each wave's code path, so every
+// index is compile-time and no lane selects between directions (a one-wave
+// variant with the two directions in neighbouring lanes needed ~540 selects
+// and 256 + AGPR registers per lane and was 14.3 vs 13.8 us at B = 8192).
 //
 // Mathematics as linear_lane_kernel / mtg_std_device.h (linear_impl:277-379,
 // 254-275, 113-130 with H_s(T) = T^(1-2r) S_T H(1) S_T and

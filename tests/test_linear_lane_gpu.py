@@ -73,8 +73,8 @@ def test_auto_selection_by_batch(ctx):
     assert plan.kernel == "standard"
     assert plan.kernel_for_batch(1024) == "standard"
     assert plan.kernel_for_batch(4095) == "standard"
-    assert plan.kernel_for_batch(4096) == "lane"
-    assert plan.kernel_for_batch(65536) == "lane"
+    assert plan.kernel_for_batch(4096) == "lane_pair"
+    assert plan.kernel_for_batch(65536) == "lane_pair"
     assert plan.set_kernel("standard").kernel_for_batch(65536) == "standard"
     # outside the lane kernels' instantiations: the wavefront kernel
     p2 = mtg.LinearPlan(ctx, N, 2, R, S, mask)
