@@ -265,7 +265,14 @@ class Polynomial {
       if (var == 1 || nd.depth >= 50) {
         ld lo = nd.lo, hi = nd.hi;
         if (var == 1) {
-          const bool pos_lo = horner(lo) > 0;
+          // The sign just right of lo: the first nonzero Bernstein
+          // coefficient (p(lo) itself is 0 at a root on the node's end).
+          bool pos_lo = false;
+          for (ld x : nd.bb)
+            if (x != 0) {
+              pos_lo = x > 0;
+              break;
+            }
           for (int it = 0; it < 200 && hi - lo > 0; ++it) {
             const ld mid = 0.5L * (lo + hi);
             if (mid <= lo || mid >= hi) break;

@@ -27,11 +27,13 @@
 //     (linear_impl:287-292, 370) are not reproduced;
 //   * setupFromPositons (header :79) is declared but never defined in the
 //     reference and is not provided;
-//   * computeMaximumOfMagnitude (linear_impl:449-487) runs on the device
-//     (mtg_max_magnitude) and does not produce the optional candidate list
-//     (candidates must be null); the per-segment candidate helpers
-//     computeSegmentMaximumMagnitudeCandidates(BySampling) (:395-447) are
-//     not provided.
+//   * computeMaximumOfMagnitude (linear_impl:449-487) runs on the device:
+//     mtg_max_magnitude, or with a candidate list mtg_magnitude_candidates
+//     (per segment 0, T, then the real roots ascending; a multiple root
+//     once, where RPOLY's cluster passes the |Im| test 0..m times).  The
+//     static per-segment helpers computeSegmentMaximumMagnitudeCandidates
+//     (BySampling) (:389-447) are host arithmetic on one Segment, as in
+//     the reference.
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_LINEAR_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_POLYNOMIAL_OPTIMIZATION_LINEAR_H_
 
@@ -274,16 +276,65 @@ class PolynomialOptimization {
     return st == MTG_TRAJ_OK;
   }
 
+  // Candidate times of the maximum magnitude of one segment over all its
+  // dimensions (linear_impl:389-409): Segment::
+  // computeMinMaxMagnitudeCandidateTimes on dimensions 0 .. D-1.
+  template <int Derivative>
+  static bool computeSegmentMaximumMagnitudeCandidates(const Segment& segment, double t_start,
+                                                       double t_stop,
+                                                       std::vector<double>* candidates) {
+    return computeSegmentMaximumMagnitudeCandidates(Derivative, segment, t_start, t_stop,
+                                                    candidates);
+  }
+  static bool computeSegmentMaximumMagnitudeCandidates(int derivative, const Segment& segment,
+                                                       double t_start, double t_stop,
+                                                       std::vector<double>* candidates) {
+    MTG_CHECK(candidates != nullptr, "candidates must not be null");
+    MTG_CHECK(N - derivative - 1 > 0, "N-Derivative-1 has to be greater 0");
+    std::vector<int> dimensions;
+    for (int i = 0; i < segment.D(); ++i) dimensions.push_back(i);
+    return segment.computeMinMaxMagnitudeCandidateTimes(derivative, t_start, t_stop, dimensions,
+                                                        candidates);
+  }
+
+  // The same candidates by sampling every dt (linear_impl:411-447): a change
+  // of the sign of d|p^(Derivative)|/dt between samples with
+  // |p^(Derivative+1)| < 1e-2 at the earlier sample appends that sample's
+  // time.  A debugging / test helper, as in the reference.
+  template <int Derivative>
+  static void computeSegmentMaximumMagnitudeCandidatesBySampling(
+      const Segment& segment, double t_start, double t_stop, double dt,
+      std::vector<double>* candidates) {
+    MTG_CHECK(candidates != nullptr, "candidates must not be null");
+    const VectorXd value_start = segment.evaluate(t_start - dt, Derivative);
+    VectorXd value_old = segment.evaluate(t_start, Derivative);
+    // the direction from t_start - dt to t_start: t_start itself may be an
+    // extremum (start and end vertices)
+    double direction = value_old.norm() - value_start.norm();
+    for (double t = t_start + dt; t < t_stop + dt; t += dt) {
+      const VectorXd value_new = segment.evaluate(t, Derivative);
+      const double direction_new = value_new.norm() - value_old.norm();
+      if (std::signbit(direction) != std::signbit(direction_new)) {
+        const VectorXd value_deriv = segment.evaluate(t - dt, Derivative + 1);
+        if (value_deriv.norm() < 1e-2) candidates->push_back(t - dt);
+      }
+      value_old = value_new;
+      direction = direction_new;
+    }
+  }
+
   // linear_impl:449-487: the maximum of |p^(Derivative)| over all segments,
-  // by the device extremum search (mtg_max_magnitude).
+  // by the device extremum search (mtg_max_magnitude); with `candidates`,
+  // the device candidate lists (mtg_magnitude_candidates) in the
+  // reference's order — per segment (0, T, roots...) with its index, then
+  // the last segment's end once more — and the first largest of them.
   template <int Derivative>
   Extremum computeMaximumOfMagnitude(std::vector<Extremum>* candidates) const {
     return computeMaximumOfMagnitude(Derivative, candidates);
   }
   Extremum computeMaximumOfMagnitude(int derivative, std::vector<Extremum>* candidates) const {
-    MTG_CHECK(candidates == nullptr,
-              "computeMaximumOfMagnitude: the candidate list is not produced by this build");
     MTG_CHECK(N - derivative - 1 > 0, "N-Derivative-1 has to be greater 0");
+    if (candidates != nullptr) return maximumWithCandidates(derivative, candidates);
     const int D = static_cast<int>(dimension_);
     const int S = static_cast<int>(n_segments_);
     std::vector<double> coeffs(static_cast<size_t>(S) * D * N);
@@ -310,6 +361,47 @@ class PolynomialOptimization {
     d_seg.download(&seg, 1);
     e.segment_idx = seg;
     return e;
+  }
+
+  Extremum maximumWithCandidates(int derivative, std::vector<Extremum>* candidates) const {
+    candidates->clear();
+    const int D = static_cast<int>(dimension_);
+    const int S = static_cast<int>(n_segments_);
+    const int C = 2 * (N - derivative) - 1;  // 2 + the degree of f: never overflows
+    std::vector<double> coeffs(static_cast<size_t>(S) * D * N);
+    std::vector<double> times(S);
+    for (int s = 0; s < S; ++s) {
+      times[s] = segments_[s].getTime();
+      for (int d = 0; d < D; ++d) {
+        const VectorXd c = segments_[s][d].getCoefficients(0);
+        for (int k = 0; k < N; ++k) coeffs[(static_cast<size_t>(s) * D + d) * N + k] = c[k];
+      }
+    }
+    internal::DeviceBuffer<double> d_c, d_t, d_ct(static_cast<size_t>(S) * C),
+        d_cv(static_cast<size_t>(S) * C);
+    internal::DeviceBuffer<int32_t> d_n(S);
+    d_c.upload(coeffs);
+    d_t.upload(times);
+    internal::checkStatus(mtg_magnitude_candidates(N, D, S, 1, d_c.get(), d_t.get(), derivative,
+                                                   C, d_ct.get(), d_cv.get(), d_n.get(),
+                                                   nullptr),
+                          "mtg_magnitude_candidates");
+    internal::synchronize();
+    const std::vector<double> ct = d_ct.download(), cv = d_cv.download();
+    const std::vector<int32_t> n = d_n.download();
+    Extremum extremum;
+    for (int s = 0; s < S; ++s)
+      for (int k = 0; k < n[s] && k < C; ++k) {
+        const Extremum c(ct[static_cast<size_t>(s) * C + k], cv[static_cast<size_t>(s) * C + k], s);
+        if (extremum < c) extremum = c;
+        candidates->push_back(c);
+      }
+    // the last segment's end once more (linear_impl:477-484)
+    const Segment& last = segments_.back();
+    const Extremum c(last.getTime(), last.evaluate(last.getTime(), derivative).norm(), S - 1);
+    if (extremum < c) extremum = c;
+    candidates->push_back(c);
+    return extremum;
   }
 
   void getTrajectory(Trajectory* trajectory) const {

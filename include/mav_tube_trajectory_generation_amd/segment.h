@@ -1,6 +1,8 @@
 // segment.h — Segment = segment time + D polynomials (reference:
 // include/mav_tube_trajectory_generation/segment.h:43-125,
-// src/segment.cpp:24-58, 186-248).
+// src/segment.cpp:24-248).  Host value type; the magnitude-candidate
+// helpers (segment.cpp:82-184) are per-segment host arithmetic as in the
+// reference (the batched form is mtg_magnitude_candidates).
 #ifndef MAV_TUBE_TRAJECTORY_GENERATION_AMD_SEGMENT_H_
 #define MAV_TUBE_TRAJECTORY_GENERATION_AMD_SEGMENT_H_
 
@@ -8,6 +10,7 @@
 #include <ostream>
 #include <vector>
 
+#include "mav_tube_trajectory_generation_amd/extremum.h"
 #include "mav_tube_trajectory_generation_amd/polynomial.h"
 
 namespace mav_trajectory_generation {
@@ -51,6 +54,94 @@ class Segment {
     VectorXd r(D_);
     for (int d = 0; d < D_; ++d) r[d] = polynomials_[d].evaluate(t, derivative_order);
     return r;
+  }
+
+  // Candidate times of the extrema of |p^(derivative)| over `dimensions` on
+  // [t_start, t_end] (segment.cpp:82-133): t_start, t_end and the real roots
+  // in the interval of sum_d conv(p_d^(derivative), p_d^(derivative+1))
+  // (several dimensions) or of p^(derivative+1) (one dimension), by
+  // Polynomial::computeMinMaxCandidates.  False: no dimensions, one out of
+  // range, or t_start > t_end.
+  bool computeMinMaxMagnitudeCandidateTimes(int derivative, double t_start, double t_end,
+                                            const std::vector<int>& dimensions,
+                                            std::vector<double>* candidate_times) const {
+    MTG_CHECK(candidate_times != nullptr, "candidate_times must not be null");
+    candidate_times->clear();
+    if (dimensions.empty()) {
+      internal::warn("No dimensions specified.");
+      return false;
+    }
+    if (dimensions.size() > 1) {
+      const int n_d = N_ - derivative, n_dd = n_d - 1;
+      if (derivative < 0 || n_dd < 1) {
+        internal::warn("N - derivative - 1 has to be at least 1.");
+        return false;
+      }
+      VectorXd f(Polynomial::getConvolutionLength(n_d, n_dd));
+      for (int dim : dimensions) {
+        if (dim < 0 || dim >= D_) {
+          internal::warn("Specified dimension out of bounds.");
+          return false;
+        }
+        // increasing coefficients: the derivatives' nonzero part is the head
+        const VectorXd d = polynomials_[dim].getCoefficients(derivative).head(n_d);
+        const VectorXd dd = polynomials_[dim].getCoefficients(derivative + 1).head(n_dd);
+        f += Polynomial::convolve(d, dd);
+      }
+      // f is already the derivative of the (half) squared magnitude: its
+      // roots are the candidates, hence derivative -1 (segment.cpp:116-122).
+      return Polynomial(f).computeMinMaxCandidates(t_start, t_end, -1, candidate_times);
+    }
+    if (dimensions[0] < 0 || dimensions[0] >= D_) {
+      internal::warn("Specified dimension out of bounds.");
+      return false;
+    }
+    return polynomials_[dimensions[0]].computeMinMaxCandidates(t_start, t_end, derivative,
+                                                              candidate_times);
+  }
+
+  // The candidate times with |p^(derivative)| over `dimensions` at each, as
+  // Extremum(time, magnitude, 0) (segment.cpp:136-161).
+  bool computeMinMaxMagnitudeCandidates(int derivative, double t_start, double t_end,
+                                        const std::vector<int>& dimensions,
+                                        std::vector<Extremum>* candidates) const {
+    MTG_CHECK(candidates != nullptr, "candidates must not be null");
+    std::vector<double> times;
+    computeMinMaxMagnitudeCandidateTimes(derivative, t_start, t_end, dimensions, &times);
+    candidates->resize(times.size());
+    for (size_t i = 0; i < times.size(); ++i) {
+      double m = 0.0;
+      for (int dim : dimensions) {
+        const double v = polynomials_[dim].evaluate(times[i], derivative);
+        m += v * v;
+      }
+      (*candidates)[i] = Extremum(times[i], std::sqrt(m), 0);
+    }
+    return true;
+  }
+
+  // Minimum and maximum among the candidates inside [t_start, t_end]
+  // (segment.cpp:163-184): strict comparisons in list order from
+  // (+max, lowest), so the first extremum wins; false if t_start > t_end.
+  bool selectMinMaxMagnitudeFromCandidates(int derivative, double t_start, double t_end,
+                                           const std::vector<int>& dimensions,
+                                           const std::vector<Extremum>& candidates,
+                                           Extremum* minimum, Extremum* maximum) const {
+    (void)derivative;
+    (void)dimensions;
+    MTG_CHECK(minimum != nullptr && maximum != nullptr, "outputs must not be null");
+    if (t_start > t_end) {
+      internal::warn("t_start is greater than t_end.");
+      return false;
+    }
+    minimum->value = std::numeric_limits<double>::max();
+    maximum->value = std::numeric_limits<double>::lowest();
+    for (const Extremum& c : candidates) {
+      if (c.time < t_start || c.time > t_end) continue;
+      if (*maximum < c) *maximum = c;  // std::max(*maximum, c)
+      if (c < *minimum) *minimum = c;  // std::min(*minimum, c)
+    }
+    return true;
   }
 
   // segment.cpp:186-201.

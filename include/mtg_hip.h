@@ -432,6 +432,30 @@ int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                       const double* times, int derivative, double* max_time,
                       double* max_value, int32_t* max_segment, void* stream);
 
+/* The candidate lists behind those extrema: for every segment s of every
+ * trajectory b, the candidates of Segment::computeMinMaxMagnitudeCandidates
+ * (src/segment.cpp:82-161, all D dimensions; PolynomialOptimization::
+ * computeSegmentMaximumMagnitudeCandidates, linear_impl:395-409, and the
+ * optional candidate list of computeMaximumOfMagnitude, linear_impl:455-487):
+ * t = 0, t = T_s, then the real roots in [0, T_s] of
+ * f = sum_d p_d^(derivative) p_d^(derivative+1) ascending (for D = 1 the
+ * roots of p^(derivative+1) alone, segment.cpp:123-129), each with
+ * |p^(derivative)(t)| (Euclidean norm over D).  Roots are isolated by
+ * Bernstein subdivision and refined as in mtg_max_magnitude; a multiple root
+ * is listed once (the reference's RPOLY lists a multiple root's cluster, of
+ * which its |Im| > DBL_EPSILON test keeps 0..m copies), and a root at
+ * exactly t = 0 or t = T_s only as the endpoint.  Outputs (device):
+ * cand_time / cand_value [B][S][max_candidates] (times relative to the
+ * segment start), n_candidates [B][S] = the number of candidates found (if
+ * it exceeds max_candidates only the first max_candidates are stored; 2 +
+ * the degree of f, i.e. 2 (N - derivative) - 1, always suffices).  A
+ * segment with T_s < 0 or NaN has none (the reference's t_start > t_end
+ * warning).  0 <= derivative <= 4, derivative <= N - 2, max_candidates >= 2. */
+int mtg_magnitude_candidates(int N, int D, int S, int64_t B, const double* coeffs,
+                             const double* times, int derivative, int max_candidates,
+                             double* cand_time, double* cand_value, int32_t* n_candidates,
+                             void* stream);
+
 /* Minimum and maximum of the magnitude: Trajectory::computeMinMaxMagnitude
  * (src/trajectory.cpp:184-220, candidates of Segment::
  * computeMinMaxMagnitudeCandidates, src/segment.cpp:82-161) over all D

@@ -209,6 +209,9 @@ SIGNATURES = {
                                                ctypes.c_int, _vp, _vp, _vp, _vp]),
     "mtg_max_magnitude": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                          _vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "mtg_magnitude_candidates": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int64, _vp, _vp, ctypes.c_int,
+                                                ctypes.c_int, _vp, _vp, _vp, _vp]),
     "mtg_soft_constraint_cost": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int64, _vp, _vp, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_int), _dp,

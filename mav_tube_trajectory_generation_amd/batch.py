@@ -634,6 +634,33 @@ def max_magnitude(coeffs, times, derivative, out=None):
     return out
 
 
+def magnitude_candidates(coeffs, times, derivative, max_candidates=None):
+    """Batched candidate lists of the magnitude extrema
+    (Segment::computeMinMaxMagnitudeCandidates, segment.cpp:82-161, per
+    segment over all D dimensions; mtg_magnitude_candidates).
+
+    coeffs [B, S, D, N], times [B, S] (float64, CUDA).  Returns a dict of
+    time / value [B, S, C] and count [B, S] int32: per segment t = 0, T and
+    the real roots of d/dt |p^(derivative)|^2 in [0, T] ascending, with
+    |p^(derivative)| at each; entries past count are unset.  C defaults to
+    2 (N - derivative) - 1, which always suffices.
+    """
+    import torch
+    B, S, D, N = coeffs.shape
+    _require(coeffs, (B, S, D, N), "coeffs")
+    _require(times, (B, S), "times")
+    dev = times.device
+    C = int(max_candidates or 2 * (N - derivative) - 1)
+    out = {"time": torch.empty((B, S, C), dtype=torch.float64, device=dev),
+           "value": torch.empty((B, S, C), dtype=torch.float64, device=dev),
+           "count": torch.empty((B, S), dtype=torch.int32, device=dev)}
+    check(lib().mtg_magnitude_candidates(N, D, S, B, _ptr(coeffs), _ptr(times), derivative, C,
+                                         _ptr(out["time"]), _ptr(out["value"]),
+                                         _ptr(out["count"]), _stream(dev)),
+          "mtg_magnitude_candidates")
+    return out
+
+
 def min_max_magnitude(coeffs, times, derivative):
     """Batched Trajectory::computeMinMaxMagnitude (trajectory.cpp:184-220;
     mtg_min_max_magnitude) over all D dimensions of coeffs [B, S, D, N].

@@ -207,6 +207,74 @@ hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
 }
 
 // ---------------------------------------------------------------------------
+// The candidate lists themselves (computeMaximumOfMagnitude's optional
+// `candidates`, linear_impl:455-487; Segment::computeMinMaxMagnitudeCandidates,
+// segment.cpp:82-161): one lane per (trajectory, segment) walks the whole
+// segment (one part) with the exhaustive search and writes t = 0, T and the
+// real roots of f in [0, T] ascending, with |p^(K)| at each.  A segment with
+// T < 0 or NaN has no candidates (the reference's t_start > t_end warning).
+template <int N, int K>
+__global__ __launch_bounds__(kExtBlock) void magnitude_candidates_kernel(
+    int D, int64_t n_seg, const double* __restrict__ coeffs, const double* __restrict__ times,
+    int cap, double* __restrict__ cand_time, double* __restrict__ cand_value,
+    int32_t* __restrict__ n_cand) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kExtBlock + threadIdx.x;
+  if (i >= n_seg) return;
+  const double T = times[i];
+  ExtEmit em{cand_time + i * cap, cand_value + i * cap, cap, 0, D == 1};
+  if (T >= 0.0) {
+    double bv = 0.0, bt = 0.0, mv = HUGE_VAL, mt = 0.0;
+    ext_segment_search<N, K, true, true>(coeffs + i * D * N, D, T, 0, 1, 0, bv, bt, mv, mt, 0.0,
+                                         &em);
+  }
+  n_cand[i] = em.n;
+}
+
+template <int N>
+static hipError_t launch_cand_n(int K, int D, int64_t n_seg, const double* coeffs,
+                                const double* times, int cap, double* ct, double* cv,
+                                int32_t* nc, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>((n_seg + kExtBlock - 1) / kExtBlock));
+#define CALL(k)                                                                           \
+  hipLaunchKernelGGL((magnitude_candidates_kernel<N, k>), grid, dim3(kExtBlock), 0, st, D, \
+                     n_seg, coeffs, times, cap, ct, cv, nc)
+  switch (K) {
+    case 0: CALL(0); break;
+    case 1: CALL(1); break;
+    case 2: CALL(2); break;
+    case 3:
+      if constexpr (N >= 5) { CALL(3); break; }
+      return hipErrorInvalidValue;
+    case 4:
+      if constexpr (N >= 6) { CALL(4); break; }
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+#undef CALL
+  return hipGetLastError();
+}
+
+hipError_t launch_magnitude_candidates(int N, int D, int64_t n_seg, int derivative,
+                                       const double* coeffs, const double* times, int cap,
+                                       double* cand_time, double* cand_value, int32_t* n_cand,
+                                       hipStream_t st) {
+  if (derivative < 0 || derivative > kMaxExtremaDerivative || N - derivative - 1 <= 0)
+    return hipErrorInvalidValue;
+  if (n_seg == 0) return hipSuccess;
+#define CALL(n) launch_cand_n<n>(derivative, D, n_seg, coeffs, times, cap, cand_time, \
+                                 cand_value, n_cand, st)
+  switch (N) {
+    case 4: return CALL(4);
+    case 6: return CALL(6);
+    case 8: return CALL(8);
+    case 10: return CALL(10);
+    case 12: return CALL(12);
+    default: return hipErrorInvalidValue;
+  }
+#undef CALL
+}
+
+// ---------------------------------------------------------------------------
 // evaluateMaximumMagnitudeAsSoftConstraint (nonlinear_impl:2735-2766) for
 // every constraint in one launch.  Workgroup = one trajectory; lane group c
 // (a whole number of waves, so the derivative switch is wave-uniform) runs

@@ -45,6 +45,20 @@ __device__ inline double ext_mag2(const double* c, int D, double t) {
   return sq;
 }
 
+// Candidate list output of the search (kEmit): every candidate (t, |p^(K)|)
+// in visiting order, t = 0, T, then the roots ascending; n counts all of
+// them (entries past cap are not stored).  single: the candidates of a
+// one-dimensional magnitude are the roots of p^(K+1) alone, as the
+// reference takes them (Polynomial::computeMinMaxCandidates on the
+// derivative, segment.cpp:123-129), not those of p^(K) p^(K+1).
+struct ExtEmit {
+  double* t;
+  double* v;
+  int cap;
+  int n;
+  bool single;
+};
+
 // One lane's share of segment s: the endpoint candidates (part 0: t = 0,
 // last part: t = T) and the real roots of f = sum_d p_d^(K) p_d^(K+1) in its
 // dyadic part [part / 2^log2parts, (part + 1) / 2^log2parts) of the segment.
@@ -55,11 +69,23 @@ __device__ inline double ext_mag2(const double* c, int D, double t) {
 // +inf).  lb: a value |p^(K)|^2 attains somewhere on the trajectory (0 if
 // none is known); without kMin, nodes whose upper bound lies below it are
 // pruned, which never drops the trajectory's maximum.
-template <int N, int K, bool kMin = false>
+template <int N, int K, bool kMin = false, bool kEmit = false>
 __device__ __attribute__((always_inline)) inline void ext_segment_search(const double* c, int D, double T, int part, int parts,
                                           int log2parts, double& best_v, double& best_t,
-                                          double& min_v, double& min_t, double lb = 0.0) {
+                                          double& min_v, double& min_t, double lb = 0.0,
+                                          ExtEmit* em = nullptr) {
+  static_assert(!kEmit || kMin, "the candidate list needs the exhaustive (kMin) search");
+  auto emit = [&](double v, double t) {
+    if constexpr (kEmit) {
+      if (em->n < em->cap) {
+        em->t[em->n] = t;
+        em->v[em->n] = sqrt(v);
+      }
+      ++em->n;
+    }
+  };
   auto take = [&](double v, double t) {
+    emit(v, t);
     if (v > best_v) {
       best_v = v;
       best_t = t;
@@ -78,6 +104,7 @@ __device__ __attribute__((always_inline)) inline void ext_segment_search(const d
   if (part == 0) {
     best_v = ext_mag2<N, K>(c, D, 0.0);
     best_t = 0.0;
+    emit(best_v, 0.0);
     if constexpr (kMin) {
       min_v = best_v;
       min_t = 0.0;
@@ -95,6 +122,12 @@ __device__ __attribute__((always_inline)) inline void ext_segment_search(const d
     double dv[ND], ddv[NDD];
 #pragma unroll
     for (int j = 0; j < ND; ++j) dv[j] = ext_falling(K, j + K) * cd[j + K];
+    if constexpr (kEmit) {
+      if (em->single) {  // f = p^(K+1)
+#pragma unroll
+        for (int j = 0; j < ND; ++j) dv[j] = j == 0 ? 1.0 : 0.0;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NDD; ++j) ddv[j] = ext_falling(K + 1, j + K + 1) * cd[j + K + 1];
 #pragma unroll

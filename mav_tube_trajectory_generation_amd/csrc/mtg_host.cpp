@@ -378,6 +378,21 @@ int mtg_sample_trajectories(int N, int D, int S, int64_t B, const double* coeffs
                                      static_cast<hipStream_t>(stream)));
 }
 
+int mtg_magnitude_candidates(int N, int D, int S, int64_t B, const double* coeffs,
+                             const double* times, int derivative, int max_candidates,
+                             double* cand_time, double* cand_value, int32_t* n_candidates,
+                             void* stream) {
+  if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || B < 0 || derivative < 0 ||
+      derivative > mtg::kMaxExtremaDerivative || N - derivative - 1 <= 0 || max_candidates < 2)
+    return MTG_ERR_INVALID_ARG;
+  if (B == 0) return MTG_OK;
+  if (!coeffs || !times || !cand_time || !cand_value || !n_candidates) return MTG_ERR_INVALID_ARG;
+  return from_hip(mtg::launch_magnitude_candidates(N, D, B * S, derivative, coeffs, times,
+                                                   max_candidates, cand_time, cand_value,
+                                                   n_candidates,
+                                                   static_cast<hipStream_t>(stream)));
+}
+
 int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                       const double* times, int derivative, double* max_time,
                       double* max_value, int32_t* max_segment, void* stream) {

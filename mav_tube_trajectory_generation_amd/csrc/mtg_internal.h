@@ -221,6 +221,12 @@ hipError_t launch_max_magnitude(int N, int D, int S, int64_t B, int derivative,
                                 double* max_value, int32_t* max_segment, int value_stride,
                                 int value_offset, const SoftCostArgs& soft, hipStream_t st,
                                 const MinOut* mino = nullptr);
+// Candidate lists of the magnitude extrema per segment (mtg_extrema.hip):
+// n_seg = B * S segments, cap entries each.
+hipError_t launch_magnitude_candidates(int N, int D, int64_t n_seg, int derivative,
+                                       const double* coeffs, const double* times, int cap,
+                                       double* cand_time, double* cand_value, int32_t* n_cand,
+                                       hipStream_t st);
 
 // Collision-driven objectives and their optimiser (mtg_coll_opt.hip); return
 // MTG_* codes.  All scratch comes from the caller's workspace.

@@ -1628,6 +1628,30 @@ int orc_max_magnitude(int N, int D, int S, const double* coeffs, const double* t
   return 0;
 }
 
+// The candidate lists of computeMaximumOfMagnitude (linear_impl:455-487),
+// per segment: Segment::computeMinMaxMagnitudeCandidates (segment.cpp:
+// 136-161) = t_start 0, t_end T_s, then the real roots (|Im| <= DBL_EPSILON)
+// of the magnitude derivative in [0, T_s] in the root finder's order.
+// cand_time / cand_value [S][cap]; n_cand[S] = the list length (entries past
+// cap dropped).  Returns 0.
+int orc_magnitude_candidates(int N, int D, int S, const double* coeffs, const double* times,
+                             int derivative, int cap, double* cand_time, double* cand_value,
+                             int* n_cand) {
+  if (N < 2 || D < 1 || S < 1 || !coeffs || !times || cap < 0) return -2;
+  if (N - derivative - 1 <= 0 || derivative < 0) return -3;
+  for (int s = 0; s < S; ++s) {
+    const double* seg = coeffs + static_cast<size_t>(s) * D * N;
+    std::vector<double> ts;
+    if (times[s] >= 0.0) magnitudeCandidateTimes(N, D, seg, derivative, 0.0, times[s], &ts);
+    n_cand[s] = static_cast<int>(ts.size());
+    for (int k = 0; k < static_cast<int>(ts.size()) && k < cap; ++k) {
+      cand_time[s * cap + k] = ts[k];
+      cand_value[s * cap + k] = magnitudeAt(N, D, seg, ts[k], derivative);
+    }
+  }
+  return 0;
+}
+
 // Real roots of a polynomial (increasing coefficients) by the oracle's root
 // finder; re/im hold up to n-1 entries.  Returns the number of roots.
 int orc_poly_roots(int n, const double* inc, double* re, double* im) {

@@ -93,6 +93,9 @@ int orc_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
 // on one trajectory (coeffs S x D x N, times S): the Extremum {time relative
 // to its segment, value, segment}.  Roots by companion-matrix eigenvalues in
 // place of Jenkins-Traub (see mtg_oracle.cpp).  -3 if N - derivative - 1 <= 0.
+int orc_magnitude_candidates(int N, int D, int S, const double* coeffs, const double* times,
+                             int derivative, int cap, double* cand_time, double* cand_value,
+                             int* n_cand);
 int orc_max_magnitude(int N, int D, int S, const double* coeffs, const double* times,
                       int derivative, double* time, double* value, int* segment,
                       int* n_candidates);

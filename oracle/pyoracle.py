@@ -393,6 +393,24 @@ def max_magnitude(N, coeffs, times, derivative):
     return dict(time=float(t[0]), value=float(v[0]), segment=seg.value, n_candidates=nc.value)
 
 
+def magnitude_candidates(N, coeffs, times, derivative):
+    """orc_magnitude_candidates: per segment of coeffs [S, D, N] the list
+    (t, |p^(derivative)(t)|) of Segment::computeMinMaxMagnitudeCandidates
+    (0, T, real roots in [0, T]).  Returns a list of S (times, values) arrays."""
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    S, D, _ = coeffs.shape
+    cap = 2 * N + 2
+    ct, cv = np.zeros((S, cap)), np.zeros((S, cap))
+    nc = np.zeros(S, dtype=np.int32)
+    L = lib()
+    L.orc_magnitude_candidates.argtypes = [ctypes.c_int] * 3 + [_dp, _dp, ctypes.c_int,
+                                                                ctypes.c_int, _dp, _dp, _ip]
+    _check(L.orc_magnitude_candidates(N, D, S, _d(coeffs), _d(times), derivative, cap, _d(ct),
+                                      _d(cv), nc.ctypes.data_as(_ip)), "magnitude_candidates")
+    return [(ct[s, :min(nc[s], cap)].copy(), cv[s, :min(nc[s], cap)].copy()) for s in range(S)]
+
+
 def poly_roots(inc):
     """orc_poly_roots: all complex roots (companion-matrix eigenvalues)."""
     inc = np.ascontiguousarray(inc, dtype=np.float64)

@@ -686,6 +686,134 @@ TEST(gpu, MaximumOfMagnitude) {
   }
 }
 
+// ExtremaOfMagnitude (test/test_polynomial_optimization.cpp:307-406) through
+// the same names: per segment the analytic candidates
+// (computeSegmentMaximumMagnitudeCandidates) contain every candidate the
+// sampling helper finds (checkExtrema, 0.01), the sampled candidates are
+// stationary points (|p^(k+1)| < 0.01), and computeMaximumOfMagnitude /
+// Trajectory::computeMinMaxMagnitude agree with getMaximumMagnitude's dense
+// sampling within 0.01.  Also: the optional candidate list of
+// computeMaximumOfMagnitude (device lists) against the host Segment lists.
+TEST(gpu, ExtremaOfMagnitude) {
+  constexpr int kDerivative = derivative_order::VELOCITY;
+  for (const Fixture& f : kFixtures) {
+    if (f.S > 10) continue;  // the 50/75-segment fixtures: same code, 10x the sampling time
+    const Vertex::Vector vs = fixtureVertices(f, 10);
+    const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+    PolynomialOptimization<10> opt(f.D);
+    opt.setupFromVertices(vs, times, f.r);
+    EXPECT_TRUE(opt.solveLinear());
+    Segment::Vector segments;
+    opt.getSegments(&segments);
+    Trajectory trajectory;
+    opt.getTrajectory(&trajectory);
+    std::vector<int> dimensions;
+    for (int i = 0; i < f.D; ++i) dimensions.push_back(i);
+    for (const Segment& s : segments) {
+      std::vector<double> res, res_sampling;
+      EXPECT_TRUE(PolynomialOptimization<10>::computeSegmentMaximumMagnitudeCandidates(
+          kDerivative, s, 0, s.getTime(), &res));
+      std::vector<double> res_t;
+      EXPECT_TRUE(PolynomialOptimization<10>::computeSegmentMaximumMagnitudeCandidates<
+                  kDerivative>(s, 0, s.getTime(), &res_t));
+      EXPECT_TRUE(res_t == res);
+      PolynomialOptimization<10>::computeSegmentMaximumMagnitudeCandidatesBySampling<kDerivative>(
+          s, 0, s.getTime(), 0.01, &res_sampling);
+      for (double c : res_sampling) EXPECT_LE(s.evaluate(c, kDerivative + 1).norm(), 0.01);
+      // checkExtrema(res_sampling, res, 0.01) (:225-245).  A sampled
+      // "extremum" where |v| itself is rounding noise (a rest vertex, e.g.
+      // deriv_jerk's last segment ends at |v| ~ 3e-12) is a flip of the
+      // noise's sign, not a stationary point: skipped.
+      for (double t : res_sampling) {
+        if (s.evaluate(t, kDerivative).norm() < 1e-9) continue;
+        bool found = false;
+        for (double r : res) found = found || std::fabs(t - r) < 0.01;
+        EXPECT_TRUE(found);
+      }
+    }
+    double v_max_ref = -1e9, a_max_ref = -1e9;  // getMaximumMagnitude (test_utils.h:43-54)
+    for (double ts = 0; ts < trajectory.getMaxTime(); ts += 0.01) {
+      v_max_ref = std::max(v_max_ref, trajectory.evaluate(ts, derivative_order::VELOCITY).norm());
+      a_max_ref =
+          std::max(a_max_ref, trajectory.evaluate(ts, derivative_order::ACCELERATION).norm());
+    }
+    const Extremum v_max_opt = opt.computeMaximumOfMagnitude<derivative_order::VELOCITY>(nullptr);
+    const Extremum a_max_opt =
+        opt.computeMaximumOfMagnitude<derivative_order::ACCELERATION>(nullptr);
+    Extremum v_min_traj, v_max_traj, a_min_traj, a_max_traj;
+    EXPECT_TRUE(trajectory.computeMinMaxMagnitude(derivative_order::VELOCITY, dimensions,
+                                                  &v_min_traj, &v_max_traj));
+    EXPECT_TRUE(trajectory.computeMinMaxMagnitude(derivative_order::ACCELERATION, dimensions,
+                                                  &a_min_traj, &a_max_traj));
+    EXPECT_LE(std::fabs(v_max_ref - v_max_opt.value), 0.01);
+    EXPECT_LE(std::fabs(a_max_ref - a_max_opt.value), 0.01);
+    EXPECT_LE(std::fabs(v_max_ref - v_max_traj.value), 0.01);
+    EXPECT_LE(std::fabs(a_max_ref - a_max_traj.value), 0.01);
+
+    // The candidate list: same maximum, segment order, every entry inside
+    // its segment and attaining its value, endpoints first, and each host
+    // Segment candidate time of a simple root matched by a device one.
+    std::vector<Extremum> cand;
+    const Extremum v_list = opt.computeMaximumOfMagnitude(derivative_order::VELOCITY, &cand);
+    EXPECT_TRUE(v_list.value == v_max_opt.value || std::fabs(v_list.value - v_max_opt.value) <=
+                                                       1e-12 * v_max_opt.value);
+    EXPECT_TRUE(!cand.empty() && cand.back().segment_idx == f.S - 1);
+    size_t i = 0;
+    for (int sidx = 0; sidx < f.S; ++sidx) {
+      const Segment& s = segments[sidx];
+      EXPECT_TRUE(i + 1 < cand.size() && cand[i].time == 0.0 && cand[i + 1].time == s.getTime());
+      std::vector<Extremum> host;
+      EXPECT_TRUE(s.computeMinMaxMagnitudeCandidates(derivative_order::VELOCITY, 0.0, s.getTime(),
+                                                     dimensions, &host));
+      size_t j = i;
+      while (j < cand.size() - 1 && cand[j].segment_idx == sidx) {
+        const double v = s.evaluate(cand[j].time, derivative_order::VELOCITY).norm();
+        EXPECT_LE(std::fabs(v - cand[j].value), 1e-9 * v + 1e-12);
+        EXPECT_TRUE(cand[j].time >= 0.0 && cand[j].time <= s.getTime());
+        ++j;
+      }
+      // f = sum_d v_d a_d in the monomial basis (segment.cpp:97-114); near
+      // a rest vertex f vanishes to high order and its values fall below
+      // the rounding of its coefficients (scale = sum |f_i| T^i): both
+      // searches then report roots of that noise, not necessarily the same
+      // ones.  Only simple roots, |f'| T > 1e-6 scale, are compared.
+      VectorXd fc(Polynomial::getConvolutionLength(9, 8));
+      for (int d = 0; d < f.D; ++d)
+        fc += Polynomial::convolve(s[d].getCoefficients(1).head(9), s[d].getCoefficients(2).head(8));
+      const Polynomial fp(fc);
+      double fscale = 0.0;
+      for (long q = 0; q < fc.size(); ++q) fscale += std::fabs(fc[q]) * std::pow(s.getTime(), q);
+      for (size_t h = 2; h < host.size(); ++h) {
+        const double t = host[h].time;
+        if (t < 1e-6 * s.getTime() || t > s.getTime() * (1 - 1e-6)) continue;
+        if (f.D > 1 && std::fabs(fp.evaluate(t, 1)) * s.getTime() <= 1e-6 * fscale) continue;
+        bool found = false;
+        for (size_t k = i + 2; k < j; ++k) found = found || std::fabs(cand[k].time - t) <= 1e-7 * s.getTime();
+        if (!found) {
+          std::fprintf(stderr, "  host root %.17g (T %.17g, D %d, S %d, seg %d, |v| %g |a| %g) device:",
+                       t, s.getTime(), f.D, f.S, sidx, s.evaluate(t, 1).norm(), s.evaluate(t, 2).norm());
+          for (size_t k = i; k < j; ++k) std::fprintf(stderr, " %.17g", cand[k].time);
+          std::fprintf(stderr, "\n");
+        }
+        EXPECT_TRUE(found);
+      }
+      // selectMinMaxMagnitudeFromCandidates over the host list: the maximum
+      // is the largest candidate of the segment
+      Extremum mn, mx;
+      EXPECT_TRUE(s.selectMinMaxMagnitudeFromCandidates(derivative_order::VELOCITY, 0.0,
+                                                        s.getTime(), dimensions, host, &mn, &mx));
+      double hmax = 0.0, hmin = 1e300;
+      for (const Extremum& e : host) {
+        hmax = std::max(hmax, e.value);
+        hmin = std::min(hmin, e.value);
+      }
+      EXPECT_TRUE(mx.value == hmax && mn.value == hmin);
+      i = j;
+    }
+    EXPECT_TRUE(i == cand.size() - 1);
+  }
+}
+
 // Soft magnitude constraints on the callback (addMaximumMagnitudeConstraint
 // + use_soft_constraints, nonlinear_impl:847-875, 907-913, 2735-2766).
 TEST(gpu, SoftConstraintTimeCost) {
@@ -854,6 +982,120 @@ TEST(host, PolynomialMinMax) {
   std::vector<double> cand;
   EXPECT_TRUE(lin.computeMinMaxCandidates(0.0, 1.0, 0, &cand));
   EXPECT_TRUE(cand.size() == 2);
+}
+
+// findRootsJenkinsTraub / Polynomial::getRoots (rpoly_ak1.cpp:70-117,
+// polynomial.cpp:28-30): polynomials built from known roots (real, complex
+// pairs, zeros at the origin) up to the 22nd degree of the magnitude
+// convolution; the contract's edge cases (trailing zeros dropped, constant
+// and zero polynomials have no roots).
+TEST(host, FindRoots) {
+  std::mt19937 gen(11);
+  std::uniform_real_distribution<double> u(-2.0, 2.0);
+  for (int trial = 0; trial < 60; ++trial) {
+    const int n_real = trial % 7, n_pair = (trial / 7) % 4, n_zero = trial % 3 == 0 ? 1 : 0;
+    std::vector<std::complex<double>> want;
+    for (int k = 0; k < n_real; ++k) want.emplace_back(u(gen) * (1 + k), 0.0);
+    for (int k = 0; k < n_pair; ++k) {
+      const std::complex<double> z(u(gen), 0.1 + std::fabs(u(gen)));
+      want.push_back(z);
+      want.push_back(std::conj(z));
+    }
+    for (int k = 0; k < n_zero; ++k) want.emplace_back(0.0, 0.0);
+    if (want.empty()) continue;
+    // coefficients (increasing) of 3.5 * prod (t - r)
+    std::vector<std::complex<double>> c(1, std::complex<double>(3.5, 0.0));
+    for (const auto& r : want) {
+      std::vector<std::complex<double>> nc(c.size() + 1);
+      for (size_t i = 0; i < c.size(); ++i) {
+        nc[i + 1] += c[i];
+        nc[i] -= r * c[i];
+      }
+      c = nc;
+    }
+    VectorXd inc(static_cast<long>(c.size()) + 2);  // two trailing zeros, dropped
+    for (size_t i = 0; i < c.size(); ++i) inc[static_cast<long>(i)] = c[i].real();
+    VectorXcd roots;
+    EXPECT_TRUE(findRootsJenkinsTraub(inc, &roots));
+    EXPECT_TRUE(roots.size() == static_cast<long>(want.size()));
+    for (const auto& r : want) {
+      double best = 1e300;
+      for (long i = 0; i < roots.size(); ++i) best = std::min(best, std::abs(roots[i] - r));
+      EXPECT_LE(best, 1e-8 * (1.0 + std::abs(r)));
+      if (r.imag() == 0.0) {  // a simple real root is reported exactly real
+        bool real = false;
+        for (long i = 0; i < roots.size(); ++i)
+          real = real || (std::abs(roots[i] - r) <= 1e-8 * (1.0 + std::abs(r)) &&
+                          roots[i].imag() == 0.0);
+        EXPECT_TRUE(real);
+      }
+    }
+  }
+  VectorXcd roots;
+  EXPECT_TRUE(findRootsJenkinsTraub(VectorXd{0.0, 0.0}, &roots) && roots.size() == 0);
+  EXPECT_TRUE(findRootsJenkinsTraub(VectorXd{4.0, 0.0, 0.0}, &roots) && roots.size() == 0);
+  EXPECT_TRUE(findRootsJenkinsTraub(VectorXd{0.0, 0.0, 2.0}, &roots) && roots.size() == 2 &&
+              roots[0] == std::complex<double>(0.0, 0.0));
+  // getRoots(derivative) finds the roots of that derivative: p = (t-1)(t-2)(t-3)
+  const Polynomial p(VectorXd{-6.0, 11.0, -6.0, 1.0});
+  EXPECT_TRUE(p.getRoots(0, &roots) && roots.size() == 3);
+  EXPECT_LE(std::fabs(roots[0].real() - 1.0) + std::fabs(roots[1].real() - 2.0) +
+                std::fabs(roots[2].real() - 3.0), 1e-12);
+  EXPECT_TRUE(p.getRoots(1, &roots) && roots.size() == 2);  // 3t^2 - 12t + 11
+  EXPECT_LE(std::fabs(roots[0].real() - (2.0 - 1.0 / std::sqrt(3.0))), 1e-12);
+  // selectMinMaxFromRoots with getRoots(derivative + 1) = computeMinMax
+  std::pair<double, double> mn, mx, mn2, mx2;
+  EXPECT_TRUE(p.selectMinMaxFromRoots(0.5, 3.2, 0, roots, &mn, &mx));
+  EXPECT_TRUE(p.computeMinMax(0.5, 3.2, 0, &mn2, &mx2));
+  EXPECT_LE(std::fabs(mn.first - mn2.first) + std::fabs(mx.first - mx2.first), 1e-12);
+  std::vector<double> cand;
+  EXPECT_TRUE(!Polynomial::selectMinMaxCandidatesFromRoots(2.0, 1.0, roots, &cand));
+}
+
+// Segment::computeMinMaxMagnitudeCandidate(Time)s (segment.cpp:82-161) on
+// random segments: the candidates attain the dense-sampled maximum of the
+// magnitude, the start / end times come first, one-dimension lists are the
+// derivative's candidates, and bad arguments return false.
+TEST(host, SegmentMagnitudeCandidates) {
+  std::mt19937 gen(5);
+  std::uniform_real_distribution<double> u(-1.0, 1.0);
+  for (int trial = 0; trial < 20; ++trial) {
+    const int D = 1 + trial % 3;
+    Segment s(10, D);
+    s.setTime(2.0);
+    for (int d = 0; d < D; ++d) {
+      VectorXd c(10);
+      for (int k = 0; k < 10; ++k) c[k] = u(gen) / (1 + k);
+      s[d] = Polynomial(c);
+    }
+    std::vector<int> dims;
+    for (int d = 0; d < D; ++d) dims.push_back(d);
+    for (int der = 0; der < 3; ++der) {
+      std::vector<Extremum> cand;
+      EXPECT_TRUE(s.computeMinMaxMagnitudeCandidates(der, 0.0, 2.0, dims, &cand));
+      EXPECT_TRUE(cand.size() >= 2 && cand[0].time == 0.0 && cand[1].time == 2.0);
+      Extremum mn, mx;
+      EXPECT_TRUE(s.selectMinMaxMagnitudeFromCandidates(der, 0.0, 2.0, dims, cand, &mn, &mx));
+      double smax = 0.0;
+      for (double t = 0.0; t <= 2.0; t += 1e-4) smax = std::max(smax, s.evaluate(t, der).norm());
+      EXPECT_LE(smax, mx.value * (1 + 1e-9));
+      EXPECT_LE(mx.value, smax + 1e-3 * std::max(1.0, smax));
+      if (D == 1) {
+        std::vector<double> pc, st;
+        EXPECT_TRUE(s[0].computeMinMaxCandidates(0.0, 2.0, der, &pc));
+        EXPECT_TRUE(s.computeMinMaxMagnitudeCandidateTimes(der, 0.0, 2.0, dims, &st));
+        EXPECT_TRUE(pc == st);
+      }
+    }
+  }
+  Segment s(10, 2);
+  s.setTime(1.0);
+  std::vector<double> t;
+  EXPECT_TRUE(!s.computeMinMaxMagnitudeCandidateTimes(1, 0.0, 1.0, {}, &t));
+  EXPECT_TRUE(!s.computeMinMaxMagnitudeCandidateTimes(1, 0.0, 1.0, {0, 2}, &t));
+  EXPECT_TRUE(!s.computeMinMaxMagnitudeCandidateTimes(1, 1.0, 0.0, {0, 1}, &t));
+  Extremum mn, mx;
+  EXPECT_TRUE(!s.selectMinMaxMagnitudeFromCandidates(1, 1.0, 0.0, {0, 1}, {}, &mn, &mx));
 }
 
 // Trajectory container operations (trajectory.cpp:136-251).
