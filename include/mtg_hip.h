@@ -59,7 +59,10 @@ enum {
   MTG_TRAJ_OK = 0,
   MTG_TRAJ_BAD_TIME = 1,     /* a segment time <= 0 (linear_impl:296) */
   MTG_TRAJ_NOT_SPD = 2,      /* free-derivative system not positive definite */
-  MTG_TRAJ_NOT_CONVERGED = 3 /* interior-point solve hit its iteration cap */
+  MTG_TRAJ_NOT_CONVERGED = 3, /* interior-point solve hit its iteration cap */
+  MTG_TRAJ_NEAR_OPTIMAL = 4   /* interior-point solve stopped where its KKT
+                                 system broke down, every residual within
+                                 1e3 x tol: usable, not converged to tol */
 };
 
 typedef struct mtg_ctx mtg_ctx;

@@ -116,7 +116,8 @@ void tube_solve_kernel(
     if (status)
       status[b] = (fl & 1) ? MTG_TRAJ_BAD_TIME
                            : ((fl & 2) || st == 2) ? MTG_TRAJ_NOT_SPD
-                           : (st == 0 ? MTG_TRAJ_OK : MTG_TRAJ_NOT_CONVERGED);
+                           : st == 0 ? MTG_TRAJ_OK
+                           : st == 3 ? MTG_TRAJ_NEAR_OPTIMAL : MTG_TRAJ_NOT_CONVERGED;
   }
 }
 

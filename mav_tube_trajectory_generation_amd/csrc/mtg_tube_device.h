@@ -852,11 +852,13 @@ struct Tube {
 
   // Full IPM (oracle TubeProblem::solveIPM).  Returns iterations; *status
   // 0 converged, 1 iteration cap, 2 numerical breakdown away from the
-  // optimum; *bad bit 2 set for a non-positive pivot of the start system.
-  // Safeguard (same in the oracle): when the KKT factorisation or the step
-  // breaks down, stop at the current iterate and accept it if every
-  // residual is within 1e3 * tol (status 0); with the dual residual within
-  // 1e5 * tol instead, report it not converged (status 1).
+  // optimum, 3 near-optimal; *bad bit 2 set for a non-positive pivot of the
+  // start system.  Safeguard (same in the oracle): when the KKT
+  // factorisation or the step breaks down, stop at the current iterate and
+  // report it near-optimal if every residual is within 1e3 * tol (status 3);
+  // with the dual residual within 1e5 * tol instead, not converged
+  // (status 1).
+  static constexpr double kComplFloor = 0.01;
   __device__ int ipm(double tol, int max_iter, int* status, int* bad) {
     int* fail = bad + 1;
     if (tid == 0) *fail = 0;
@@ -932,10 +934,11 @@ struct Tube {
         break;
       }
       const bool near = rdn <= 1e3 * tol * (1.0 + qn) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
+      const double infeas = fmax(rdn / (1.0 + qn), rpn);
       // Stalled dual residual (lam / s ~ 1e12 on active constraints): not
       // converged, value usable (same tiers in the oracle).
       const bool stalled = rdn <= 1e5 * tol * (1.0 + qn) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
-      const int brk = near ? 0 : (stalled ? 1 : 2);
+      const int brk = near ? 3 : (stalled ? 1 : 2);
       MTG_TACC(200, tl);
       assemble_g();
       MTG_TACC(201, tl);
@@ -957,7 +960,17 @@ struct Tube {
         mua += (sm[L->s + k] + a_aff * sm[L->ds + k]) * (sm[L->lam + k] + a_aff * sm[L->dl + k]);
       mua = block_sum(mua) / nc;
       const double ratio = mua / mu;
-      const double sigma = ratio * ratio * ratio;
+      // Mehrotra's sigma, with the complementarity target kept at or above
+      // kComplFloor x the relative infeasibility (the oracle's rule): mu
+      // running ahead of the dual residual sends lam / s on the active
+      // constraints past 1e12, where the condensed KKT matrix loses its
+      // null-space part to rounding, the dual residual stalls and the
+      // factorisation breaks down.
+      double sigma = ratio * ratio * ratio;
+      {
+        const double floor_mu = fmin(mu, kComplFloor * infeas);
+        if (sigma * mu < floor_mu) sigma = floor_mu / mu;
+      }
       __syncthreads();
       // Corrector: rc = s lam + ds_aff dl_aff - sigma mu.
       MTG_TACC(204, tl);

@@ -855,7 +855,9 @@ struct TubeProblem {
 
   // Primal-dual interior point (Mehrotra predictor-corrector) for
   //   min 0.5 x^T P x + q^T x  s.t.  g_k(x) <= 0  (convex QCQP),
-  // replacing MSK_optimizetrm (qcqp_impl:700-712).
+  // replacing MSK_optimizetrm (qcqp_impl:700-712).  Status 0 converged,
+  // 1 iteration cap / stalled, 2 breakdown, 3 near-optimal at a breakdown.
+  static constexpr double kComplFloor = 0.01;
   int solveIPM(double tol, int max_iter, std::vector<double>* xout, int* iters) {
     Mat P;
     std::vector<double> q;
@@ -913,14 +915,15 @@ struct TubeProblem {
         break;
       }
       // Safeguard: on a breakdown of the KKT factorisation or step, stop at
-      // the current iterate and accept it if within 1e3 * tol (status 0), or
+      // the current iterate and accept it if within 1e3 * tol (status 3,
+      // near-optimal), or
       // report it as not converged (status 1, value usable) when it is
       // primal feasible and complementary to 1e3 * tol with the dual
       // residual within 1e5 * tol: with lam_k / s_k ~ 1e12 on the active
       // constraints the dual residual stalls at the KKT solve's accuracy.
       const bool near = rdn <= 1e3 * tol * (1.0 + qnorm) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
       const bool stalled = rdn <= 1e5 * tol * (1.0 + qnorm) && rpn <= 1e3 * tol && mu <= 1e3 * tol;
-      const int brk = near ? 0 : (stalled ? 1 : 2);
+      const int brk = near ? 3 : (stalled ? 1 : 2);
       // K = P + sum lam_k Q_k + sum (lam_k/s_k) a_k a_k^T.
       Mat Kmat = P;
       for (int k = 0; k < m; ++k) {
@@ -973,7 +976,18 @@ struct TubeProblem {
       for (int k = 0; k < m; ++k)
         mu_aff += (s[k] + a_aff * ds[k]) * (lam[k] + a_aff * dl[k]);
       mu_aff /= std::max(m, 1);
-      const double sigma = std::pow(mu_aff / mu, 3);
+      // Mehrotra's sigma, with the complementarity target kept at or above
+      // kComplFloor x the (relative) infeasibility: letting mu run ahead of
+      // the dual residual sends lam_k / s_k on the active constraints past
+      // 1e12, where the condensed KKT matrix loses its null-space part to
+      // rounding and the dual residual stalls (and the factorisation breaks
+      // down: 87 of 400 problems stopped that way before).
+      double sigma = std::pow(mu_aff / mu, 3);
+      {
+        const double infeas = std::max(rdn / (1.0 + qnorm), rpn);
+        const double floor_mu = std::min(mu, kComplFloor * infeas);
+        if (sigma * mu < floor_mu) sigma = floor_mu / mu;
+      }
       for (int k = 0; k < m; ++k) rc[k] = s[k] * lam[k] + ds[k] * dl[k] - sigma * mu;
       direction(rc, &dx, &dl, &ds);
       const double alpha = std::min(1.0, 0.99 * max_step(dl, ds));

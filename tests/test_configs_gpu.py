@@ -120,16 +120,17 @@ def test_config3_tube_at_size(ctx, dev, oracle):
     cost = out["cost"].cpu().numpy()
     resid = res.cpu().numpy()
     conv = st == 0
+    near = st == 4  # MTG_TRAJ_NEAR_OPTIMAL: stopped at a breakdown within 1e3 tol
+    usable = conv | near
     hist = dict(zip(*np.unique(st, return_counts=True)))
     print("config 3 GPU status histogram", hist)
-    assert set(np.unique(st)) <= {0, 2, 3}
-    # Status 0 includes the IPM's "near" tier (mtg_tube_device.h ipm():
-    # factorisation breakdown with every residual within 1e3 tol), so a
-    # converged point is feasible to 1e3 * tol = 1e-7.
-    assert resid[conv].max() <= 1e3 * 1e-10
-    print("config 3 max residual (converged)", resid[conv].max(),
-          "share above 1e-8", np.mean(resid[conv].max(axis=1) > 1e-8))
-    assert np.all(np.isfinite(cost[conv]))
+    assert set(np.unique(st)) <= {0, 2, 3, 4}
+    # converged: primal feasible to tol (g_k = -s_k + rp_k, rp <= tol)
+    assert resid[conv].max() <= 1e-10
+    if near.any():
+        assert resid[near].max() <= 1e3 * 1e-10
+    print("config 3 max residual (converged)", resid[conv].max())
+    assert np.all(np.isfinite(cost[usable]))
 
     rad1 = np.full((S, 2), 0.15)
 
@@ -144,7 +145,12 @@ def test_config3_tube_at_size(ctx, dev, oracle):
         refs = dict(ex.map(ref, range(B)))
     ost = np.array([refs[b]["status"] for b in range(B)])
     print("config 3 oracle status histogram", dict(zip(*np.unique(ost, return_counts=True))))
-    assert (~conv).sum() <= max(int(1.5 * (ost != 0).sum()), 8), ((~conv).sum(), (ost != 0).sum())
+    # The GPU fails (no usable point) no more often than the oracle, and at
+    # most 0.25 % of the problems (the complementarity floor of the IPM,
+    # mtg_tube_device.h ipm(); 0 of 2,400 oracle breakdowns).
+    o_usable = (ost == 0) | (ost == 3)
+    assert (~usable).sum() <= (~o_usable).sum(), ((~usable).sum(), (~o_usable).sum())
+    assert (~usable).sum() <= 0.0025 * B and (~o_usable).sum() <= 0.0025 * B
     both = np.nonzero(conv & (ost == 0))[0]
     for b in both[::max(1, len(both) // 32)][:33]:
         r = refs[b]

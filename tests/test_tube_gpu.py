@@ -160,7 +160,9 @@ def test_polynomial_orders_vs_oracle(ctx, dev, oracle, n, r, S):
     agree = 0
     for b, (v, t) in enumerate(items):
         ref = oracle.tube_solve(n, r, v, t, np.full((S, 2), 0.15), tol=1e-10, max_iter=100)
-        assert o["status"][b] == ref["status"], b
+        # oracle 0 converged / 1 cap / 3 near-optimal = MTG_TRAJ_OK /
+        # NOT_CONVERGED / NEAR_OPTIMAL
+        assert o["status"][b] == {0: 0, 1: 3, 3: 4}[ref["status"]], b
         if ref["status"] != 0:
             continue
         agree += 1

@@ -105,13 +105,17 @@ def test_ipm_matches_scipy(oracle, case):
     scale = max(1.0, np.abs(ref.x).max())
     assert np.max(np.abs(sol["x"] - ref.x)) <= 1e-3 * scale
     # KKT at the oracle's x: grad f = -sum lambda_k grad g_k over the active
-    # set with lambda >= 0 (non-negative least squares residual ~ 0).
+    # set with lambda >= 0 (non-negative least squares residual ~ 0).  The
+    # IPM stops at mu <= tol = 1e-10 (its complementarity target is kept at
+    # >= 1e-2 x the infeasibility, so mu does not run to 1e-20): the ~100
+    # inactive constraints (slack ~0.05) keep lambda ~ mu / s ~ 1e-9 each,
+    # which the active-set NNLS leaves out, hence 1e-7.
     from scipy.optimize import nnls
     x = sol["x"]
     act = g > -1e-6
     Jg = (np.einsum("kij,j->ki", Qk, x) + lk)[act]
     _, resid = nnls(Jg.T, -(P @ x + q))
-    assert resid <= 1e-8 * max(1.0, np.linalg.norm(P @ x + q))
+    assert resid <= 1e-7 * max(1.0, np.linalg.norm(P @ x + q))
 
 
 def test_tube_time_objective_oracle(oracle):
