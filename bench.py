@@ -206,6 +206,21 @@ def load_pmc_traffic(workload, config_key):
     return None
 
 
+def load_sq_executed(config_key):
+    """Executed FP64 FLOP per trajectory (SQ instruction counts x active
+    lanes, tools/sq_summary.py) from the committed profiles/sq_executed.json,
+    for the workload/batch/kernel key, if measured."""
+    path = os.path.join(REPO, "profiles", "sq_executed.json")
+    try:
+        with open(path) as f:
+            entry = json.load(f).get(config_key)
+        if entry:
+            return entry["executed_f64_flop_per_trajectory"], entry["source"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None, None
+
+
 def tube_flops_per_iter(N, S):
     """FLOP per interior-point iteration of one tube QCQP:
     m (2 v^2 + 2 v) constraint evaluation + m v^2 Hessian accumulation +
@@ -569,10 +584,21 @@ def main():
                 "traffic": traffic, "alg_bytes_per_launch": alg_bytes}
     roof["kernel_ms"] = kernel_ms
     roof["kernel_timing"] = timing
+    # Executed FP64 work beside the dense-equivalent count: the kernel's SQ
+    # FP64 instruction counts x active lanes (a committed rocprofv3 pass at
+    # this workload, batch and kernel) over this run's kernel time.
+    kname = (plan.kernel_for_batch(B) if wl == "linear" else
+             wl + ("_soft" if getattr(args, "soft", False) else ""))
+    ex_flop, ex_src = load_sq_executed(f"{config_key}:{kname}")
+    if ex_flop is not None:
+        ex_tf = ex_flop * B / (kernel_ms * 1e-3) / 1e12
+        roof["executed"] = {"achieved": ex_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": ex_tf / FP64_PEAK_TFLOPS,
+                            "flop_per_trajectory": ex_flop, "source": ex_src}
     if select and wl == "linear":
-        roof["kernel_timing"] += ("; per-step device time includes the selection (solve with the "
-                                  "shard's argmin fused into its launch, RCCL all-gather, global "
-                                  "argmin kernel)")
+        roof["kernel_timing"] += ("; per-step device time includes the selection (solve with "
+                                  "per-workgroup partials, shard reduction launch, RCCL "
+                                  "all-gather, global argmin kernel)")
 
     if rank == 0:
         cpu = None

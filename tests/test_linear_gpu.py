@@ -89,6 +89,50 @@ def _exact_cases():
         return json.load(f)["cases"]
 
 
+def _golden_cases():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "linear_golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _golden_cases(), ids=lambda c: c["name"])
+def test_committed_golden_vectors(ctx, dev, oracle, case, kernel):
+    """The committed golden vectors (tests/golden/linear_golden.json, made by
+    make_golden.py: the reference's TwoVerticesSetup Matlab solution and
+    reference-fixture problems) read directly, not through the oracle, so a
+    drift in the oracle cannot move the GPU's target.  Batched 2x (and, where
+    the pattern allows, through the lane kernels at a batch of 70)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    N, r = case["N"], case["r"]
+    # oracle.Vertices is only the dense (mask, vals) container
+    v = oracle.Vertices(np.array(case["mask"], np.uint8), np.array(case["vals"]))
+    times = np.array(case["times"])
+    want_c, want_J = np.array(case["coeffs"]), case["cost"]
+    mask, df = compact_fixed(v, N)
+    _, out = _solve_gpu(ctx, dev, N, r, mask, np.stack([df, df]), np.stack([times, times]), kernel)
+    for b in range(2):
+        assert out["status"][b] == 0
+        assert rel_err_coeffs(out["coeffs"][b], want_c) <= REL_TOL, case["name"]
+        assert rel_err(out["cost"][b], want_J) <= REL_TOL, case["name"]
+    S, D = len(times), v.D
+    if kernel == "auto" and N == 10 and r == 4 and D == 3 and 2 <= S <= 12:
+        plan = mtg.LinearPlan(ctx, N, D, r, S, mask)
+        try:
+            plan.set_kernel("lane_pair")
+        except mtg.MTGError:
+            return  # not the standard pattern
+        for k in ("lane", "lane_pair"):
+            plan.set_kernel(k)
+            o = plan.solve(torch.from_numpy(np.repeat(df[None], 70, 0)).to(dev),
+                           torch.from_numpy(np.repeat(times[None], 70, 0)).to(dev))
+            c = o["coeffs"].cpu().numpy()
+            J = o["cost"].cpu().numpy()
+            for b in (0, 33, 69):
+                assert rel_err_coeffs(c[b], want_c) <= REL_TOL, (k, case["name"])
+                assert rel_err(J[b], want_J) <= REL_TOL, (k, case["name"])
+
+
 @pytest.mark.parametrize("case", _exact_cases(), ids=lambda c: f"N{c['N']}_r{c['r']}")
 def test_orders_vs_exact(ctx, dev, oracle, case, kernel):
     """Every supported N (4..12) and derivative order against the exact

@@ -1,8 +1,13 @@
 """Median per-dispatch SQ counters of one kernel from a tools/pmc_sq.sh run.
 
-    python tools/sq_summary.py <tag> <kernel-substring> [trajectories-per-launch]
+    python tools/sq_summary.py <tag> <kernel-substring> [trajectories-per-launch] [out.json]
 Prints JSON: counters, per-wave instruction counts and derived ratios
-(VALU lane utilisation = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)).
+(VALU lane utilisation = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)),
+and the EXECUTED FP64 work per trajectory: (2 FMA + MUL + ADD + TRANS) wave
+instructions x 64 lanes x the lane utilisation / trajectories.  bench.py
+reads that figure from the committed profiles/r03_sq_*.json to state real
+pipe use beside the dense-equivalent roofline.  With out.json the summary is
+also written there.
 """
 import csv
 import json
@@ -42,7 +47,19 @@ def main():
                                           "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64"))
     if vals.get("SQ_INSTS_VALU"):
         out["f64_share_of_valu"] = f64 / vals["SQ_INSTS_VALU"]
+    if units and vals.get("SQ_ACTIVE_INST_VALU"):
+        flop_instr = (2.0 * vals.get("SQ_INSTS_VALU_FMA_F64", 0.0) +
+                      vals.get("SQ_INSTS_VALU_MUL_F64", 0.0) +
+                      vals.get("SQ_INSTS_VALU_ADD_F64", 0.0) +
+                      vals.get("SQ_INSTS_VALU_TRANS_F64", 0.0))
+        out["executed_f64_flop_per_trajectory"] = (
+            flop_instr * 64.0 * out["valu_lane_utilisation"] / units)
+    out["kernel"] = kernel
+    out["trajectories_per_launch"] = units
     print(json.dumps(out, indent=1))
+    if len(sys.argv) > 4:
+        with open(sys.argv[4], "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
