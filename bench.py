@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
     p.add_argument("--segments", type=int, default=10)
     p.add_argument("--workload", choices=["linear", "time", "tube", "time-qcqp", "sample",
-                                          "extrema"], default="linear")
+                                          "extrema", "collision"], default="linear")
     p.add_argument("--cpu-seconds", type=float, default=20.0,
                    help="total CPU-baseline budget (all reps, both modes)")
     p.add_argument("--cpu-reps", type=int, default=5)
@@ -108,6 +108,42 @@ def _median_rate(run, reps, seconds):
     run(min(0.3, seconds))
     rates = sorted(u / s for u, s in (run(seconds) for _ in range(reps)))
     return rates[len(rates) // 2], rates
+
+
+def cpu_baseline_collision(N, r, coll, seconds, reps):
+    """Oracle port of the device optimiser (orc_coll_optimize: the same
+    projected L-BFGS on objectiveFunctionFreeConstraintsAndCollision) over 8
+    of the bench's starts, 1 thread and all cores (orc_bench_coll)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    mask, df = coll["mask"], coll["df"]
+    S = mask.shape[0] - 1
+    K = mask.shape[1]
+    D = df.shape[0]
+    vals = np.zeros((S + 1, K, D))
+    vals[0, :, :] = df[:, :K].T
+    vals[S, :, :] = df[:, K:].T
+    v = pyoracle.Vertices(mask, vals)
+    X0 = coll["X0"][:8]
+
+    def run(threads, sec):
+        return pyoracle.bench_coll(N, r, v, coll["times"], coll["occ"], coll["params"], X0,
+                                   coll["max_evals"], threads=threads, seconds=sec)
+    threads = _cpu_threads()
+    per_rep = seconds / (2 * reps)
+    one, one_all = _median_rate(lambda s_: run(1, s_), reps, per_rep)
+    allc, allc_all = _median_rate(lambda s_: run(threads, s_), reps, per_rep)
+    return {
+        "value": allc, "cores": threads, "kind": "port",
+        "single_core": {"value": one, "cores": 1, "reps": [round(x, 3) for x in one_all]},
+        "all_core_reps": [round(x, 3) for x in allc_all],
+        "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+        "method": (f"median of {reps} repetitions of ~{per_rep:.1f} s after a warm-up, "
+                   "std::chrono::steady_clock"),
+        "sample": (f"{coll['max_evals']}-evaluation collision optimisations (orc_coll_optimize) "
+                   f"cycling over 8 of the bench's starts of main.cpp's problem, oracle C++ port "
+                   f"(-O3 -march=x86-64-v3); value = all {threads} threads"),
+    }
 
 
 def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None):
@@ -250,6 +286,8 @@ def config_name(wl, B, world, S):
         return "C3: 4096 x 10-segment tube QCQP"
     if wl == "time" and S == 10 and B == 4096 and world == 1:
         return "C5: 4096 x 50-evaluation time allocation"
+    if wl == "collision":
+        return f"demo: {B} x main.cpp's 4-segment collision objective per GPU"
     return f"{wl}: {B} x {S}-segment per GPU"
 
 
@@ -294,7 +332,7 @@ def main():
     N, D, r, S = 10, 3, 4, args.segments
     wl = args.workload
     B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "time-qcqp": 1024,
-                       "sample": 1024, "extrema": 1024}[wl]
+                       "sample": 1024, "extrema": 1024, "collision": 4096}[wl]
     from mav_tube_trajectory_generation_amd.shard import select_best_device, shard_range
     global_batch = B * world
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
@@ -310,6 +348,8 @@ def main():
     flop_note = None
     useful_per_step = None  # units that count towards `value` (converged solves)
     metric_base = "trajectories/sec (10-seg, N=10, 3D minimum-snap) at 1/2/4/8 MI355X"
+    coll = None  # collision workload inputs (also the CPU baseline's)
+    extra_cfg = {}
 
     if wl == "linear":
         out = plan.solve(fixed_d, times_d, free=False)
@@ -403,6 +443,62 @@ def main():
         unit = "trajectories/s"
         units_per_step = B
         bound = "hbm"
+    elif wl == "collision":
+        # The reference demo's objective (main.cpp:77, 104-105:
+        # kOptimizeFreeConstraintsAndCollision with LD_LBFGS, max_iterations
+        # 25, main.cpp's weights): mtg_coll_optimize's projected L-BFGS on B
+        # starts around the demo's tube-QCQP solution (main.cpp:69-73, solved
+        # here on the device), over a synthetic forest map standing in for the
+        # demo's private supereight map (mav_tube_trajectory_generation_amd/
+        # demo.py).  One unit = one 25-evaluation optimisation.
+        from mav_tube_trajectory_generation_amd import demo
+        pos_m = demo.MAIN_POSITIONS
+        Sd = pos_m.shape[0] - 1
+        t_m = demo.estimate_segment_times(pos_m, 2.0, 2.0)  # main.cpp:51-53
+        cmask, cdf = demo.tube_pattern(pos_m)
+        cplan = mtg.LinearPlan(ctx, N, D, r, Sd, cmask)
+        T1 = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        tf1 = np.zeros((1, 3, N))
+        tf1[0] = cdf
+        q = mtg.tube_solve(ctx, N, r, T1(pos_m[None]), T1(tf1), T1(t_m[None]), T1(t_m[None]),
+                           T1(demo.MAIN_RADII[None]))
+        x0 = q["x"][0].cpu().numpy()
+        X0 = np.array([x0] + demo.perturbed_starts(x0, B - 1, 0.005, seed=23))
+        occ_np = demo.forest_map()
+        cparams = demo.coll_params()
+        prm = mtg.make_coll_params(**cparams)
+        c_df, c_x0, c_t = T1(np.repeat(cdf[None], B, 0)), T1(X0), T1(np.repeat(t_m[None], B, 0))
+        c_occ = T1(occ_np)
+        c_max_evals = int(demo.MAIN_PARAMS["max_iterations"])
+        c_ws = torch.empty(cplan.coll_workspace_bytes(B, prm, 0, True), dtype=torch.uint8,
+                           device=dev)
+        # the map's near field (mtg_coll_field), once per map, outside the
+        # timed steps: the walk then reads one voxel record per sample
+        c_field = mtg.coll_field(c_occ, prm)
+        coll = {"mask": cmask, "df": cdf, "times": t_m, "occ": occ_np, "params": cparams,
+                "X0": X0, "max_evals": c_max_evals}
+
+        def step():
+            return cplan.coll_optimize(c_df, c_x0, c_t, c_occ, prm, max_evals=c_max_evals,
+                                       workspace=c_ws, near_field=c_field)
+
+        probe = step()
+        torch.cuda.synchronize(dev)
+        ev = probe["evals"].cpu().numpy()
+        res_hist = {int(k): int(v) for k, v in zip(*np.unique(probe["result"].cpu().numpy(),
+                                                               return_counts=True))}
+        nvar = X0.shape[1]
+        # inputs (x0, d_f, times) + outputs (x, cost, evals, result, status,
+        # terms); the map (1.3 MB, L2-resident) read per launch
+        bytes_per_traj = (nvar + D * 2 * (N // 2) + Sd) * 8 + (nvar + 1 + 4) * 8 + 12
+        bytes_per_traj += occ_np.nbytes / B
+        metric = ("collision optimisations/sec (main.cpp's kOptimizeFreeConstraintsAndCollision "
+                  "objective, 25 evaluations, 4-seg, N=10, 3D, synthetic forest map)")
+        unit = "optimisations/s"
+        units_per_step = B
+        bound = "hbm"
+        extra_cfg = {"segments": Sd, "max_evals": c_max_evals, "mean_evals": float(ev.mean()),
+                     "results": res_hist, "map_voxels": list(occ_np.shape)}
     else:  # tube, time-qcqp
         radii = torch.full((B, S, 2), 0.15, dtype=torch.float64, device=dev)
         pos_d = torch.from_numpy(pos).to(dev)
@@ -603,14 +699,18 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(wl, N, D, r, S, args.cpu_seconds, args.cpu_reps,
-                               sample_args=(0.01, 4) if wl == "sample" else None)
+            if wl == "collision":
+                cpu = cpu_baseline_collision(N, r, coll, args.cpu_seconds, args.cpu_reps)
+            else:
+                cpu = cpu_baseline(wl, N, D, r, S, args.cpu_seconds, args.cpu_reps,
+                                   sample_args=(0.01, 4) if wl == "sample" else None)
             cpu["unit"] = unit
         cfg = {"workload": config_name(wl, B, world, S), "global_batch": global_batch,
                "kernel": plan.kernel_for_batch(B) if wl == "linear" else None,
                "batch_per_gpu": B, "segments": S, "N": N, "D": D, "r": r,
                "parallelism": f"shard{world}",
                "selection": bool(select and wl == "linear")}
+        cfg.update(extra_cfg)
         if useful_per_step is not None:
             cfg["converged_per_step"] = useful_per_step
         if selection_ms is not None:
@@ -629,7 +729,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (createRandomVertices seeds 105+i, estimateSegmentTimes v=3 a=5)",
+            "data": ("synthetic (main.cpp's vertices, starts perturbed around the device tube "
+                     "QCQP solution, synthetic forest occupancy map)" if wl == "collision" else
+                     "synthetic (createRandomVertices seeds 105+i, estimateSegmentTimes v=3 a=5)"),
             "config": cfg,
             "roofline": roof,
             "cpu_baseline": cpu,

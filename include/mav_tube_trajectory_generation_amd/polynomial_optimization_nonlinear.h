@@ -461,6 +461,7 @@ class PolynomialOptimizationNonLinear {
     occ_dims_[2] = nz;
     occupancy_.upload(occupancy);
     grid_set_ = true;
+    field_side_ = -1;  // the near field is rebuilt for the new map
   }
 
   // The collision objective at x (objectiveFunctionFreeConstraintsAndCollision,
@@ -490,7 +491,8 @@ class PolynomialOptimizationNonLinear {
     d_ref.upload(&ref, 1);
     internal::checkStatus(
         mtg_coll_cost(poly_opt_.getPlan(), 1, mode, d_df.get(), d_x.get(), d_t.get(),
-                      occupancy_.get(), occ_dims_[0], occ_dims_[1], occ_dims_[2], &cp,
+                      occupancy_.get(), occ_dims_[0], occ_dims_[1], occ_dims_[2],
+                      nearField(cp.coll), &cp,
                       d_ref.get(), d_cost.get(), gradient ? d_g.get() : nullptr, d_terms.get(),
                       d_coll.get(), d_st.get(), ws.get(), static_cast<size_t>(nb), nullptr),
         "mtg_coll_cost");
@@ -696,7 +698,8 @@ class PolynomialOptimizationNonLinear {
     internal::checkStatus(
         mtg_coll_optimize(poly_opt_.getPlan(), 1, mode, d_df.get(), d_x.get(), d_t.get(),
                           d_lo.get(), d_hi.get(), d_step.get(), occupancy_.get(), occ_dims_[0],
-                          occ_dims_[1], occ_dims_[2], &cp, budget, d_cost.get(), d_ev.get(),
+                          occ_dims_[1], occ_dims_[2], nearField(cp.coll), &cp, budget,
+                          d_cost.get(), d_ev.get(),
                           d_res.get(), d_st.get(), d_terms.get(), ws.get(),
                           static_cast<size_t>(nb), nullptr),
         "mtg_coll_optimize");
@@ -970,6 +973,22 @@ class PolynomialOptimizationNonLinear {
   internal::DeviceBuffer<float> occupancy_;
   int occ_dims_[3] = {0, 0, 0};
   bool grid_set_ = false;
+  // Near field of the map (mtg_coll_field) for the current box side, built
+  // on first use and kept until the map or the box side changes.
+  internal::DeviceBuffer<uint16_t> field_;
+  int field_side_ = -1;
+
+  const uint16_t* nearField(const mtg_collision_params& cp) {
+    if (field_side_ == cp.box_side) return field_.get();
+    const int64_t n = mtg_coll_field_bytes(occ_dims_[0], occ_dims_[1], occ_dims_[2]);
+    if (n <= 0) return nullptr;
+    field_.resize(static_cast<size_t>(n) / sizeof(uint16_t));
+    if (mtg_coll_field(occupancy_.get(), occ_dims_[0], occ_dims_[1], occ_dims_[2], &cp,
+                       field_.get(), nullptr) != MTG_OK)
+      return nullptr;  // box side beyond the field's range: the walk scans
+    field_side_ = cp.box_side;
+    return field_.get();
+  }
   // Collision raise state (polynomial_optimization_nonlinear.h:672-673, and
   // the optimization_info_ totals of the last evaluation, :1216-1219).
   double total_cost_iter0_ = 0.0;

@@ -605,17 +605,37 @@ typedef struct mtg_coll_params {
   int lbfgs_memory;               /* history pairs (10) */
 } mtg_coll_params;
 
+/* Near field of an occupancy map for the collision walk.  For every voxel v
+ * of the nx x ny x nz grid, 8 uint16 (7 used): the squared voxel distances
+ * from v and from its 6 axis neighbours to the nearest occupied voxel of the
+ * box_side^3 box the walk searches around v (0xFFFF: none) — the minima of
+ * getCostAndGradientPotentialOctree's search (nonlinear_impl:1782-2018), so
+ * a walk that reads them instead of scanning the box gives identical
+ * results (the scan remains for samples whose voxel lies outside the grid).
+ * It depends only on the occupancy and params->box_side: compute it once
+ * per map (mtg_coll_field_bytes(nx, ny, nz) bytes, device) and pass it as
+ * `near_field` to mtg_coll_cost / mtg_coll_optimize, whose walk then runs on
+ * one thread per walk with one load per evaluated sample instead of a
+ * workgroup-wide box scan and reduction per sample.  box_side <= 31. */
+int64_t mtg_coll_field_bytes(int nx, int ny, int nz);
+int mtg_coll_field(const float* occupancy, int nx, int ny, int nz,
+                   const mtg_collision_params* params, uint16_t* field, void* stream);
+
 int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
                                  const mtg_coll_params* params, int optimize);
+/* near_field: mtg_coll_field of the same occupancy and box_side, or NULL
+ * (every sample's box is scanned). */
 int mtg_coll_cost(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
                   const double* x, const double* times, const float* occupancy, int nx,
-                  int ny, int nz, const mtg_coll_params* params, const double* raise_ref,
+                  int ny, int nz, const uint16_t* near_field, const mtg_coll_params* params,
+                  const double* raise_ref,
                   double* cost, double* grad, double* terms, int32_t* collision,
                   int32_t* status, void* workspace, size_t workspace_bytes, void* stream);
 int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
                       double* x_io, const double* times, const double* lower,
                       const double* upper, const double* initial_step, const float* occupancy,
-                      int nx, int ny, int nz, const mtg_coll_params* params, int max_evals,
+                      int nx, int ny, int nz, const uint16_t* near_field,
+                      const mtg_coll_params* params, int max_evals,
                       double* cost, int32_t* evals, int32_t* result, int32_t* status,
                       double* terms, void* workspace, size_t workspace_bytes, void* stream);
 

@@ -8,13 +8,15 @@ package is the batched front end used by tests and bench.py.
 """
 from ._abi import (COLL_DEFAULTS, LIB_PATH, MTGError, lib, make_coll_params,  # noqa: F401
                    make_collision_params, make_time_params)
-from .batch import (Context, LinearPlan, generate_random_problems, magnitude_candidates,  # noqa: F401
+from .batch import (Context, LinearPlan, coll_field, generate_random_problems,  # noqa: F401
+                    magnitude_candidates,
                     max_magnitude,
                     min_max_magnitude, sample_trajectories, segment_matrices, soft_constraint_cost,
                     tube_num_constraints, tube_residuals, tube_solve, tube_time_cost,
                     tube_time_optimize, tube_time_workspace_bytes)
 
-__all__ = ["Context", "LinearPlan", "MTGError", "generate_random_problems", "magnitude_candidates",
+__all__ = ["Context", "LinearPlan", "MTGError", "coll_field", "generate_random_problems",
+           "magnitude_candidates",
            "max_magnitude",
            "min_max_magnitude", "make_coll_params", "make_collision_params", "make_time_params",
            "COLL_DEFAULTS",

@@ -150,13 +150,17 @@ SIGNATURES = {
     "mtg_coll_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64, ctypes.c_int,
                                                   ctypes.POINTER(CollObjectiveParams),
                                                   ctypes.c_int]),
+    "mtg_coll_field_bytes": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "mtg_coll_field": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(CollisionParams), _vp, _vp]),
     "mtg_coll_cost": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp, _vp,
-                                     ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
                                      ctypes.POINTER(CollObjectiveParams), _vp, _vp, _vp, _vp,
                                      _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "mtg_coll_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                         ctypes.POINTER(CollObjectiveParams), ctypes.c_int, _vp,
+                                         _vp, ctypes.POINTER(CollObjectiveParams), ctypes.c_int,
+                                         _vp,
                                          _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "mtg_min_max_magnitude": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp, _vp,

@@ -358,14 +358,17 @@ class LinearPlan:
         return B
 
     def coll_cost(self, fixed_vals, x, times, occupancy, params, mode=0, raise_ref=None,
-                  grad=True, workspace=None):
+                  grad=True, workspace=None, near_field=None):
         """objectiveFunctionFreeConstraintsAndCollision (mode 0, x = d_p
         [B, D*n_free]) or ...AndCollisionAndTime (mode 1, x = [T; d_p]
         [B, S + D*n_free]) on the device (mtg_coll_cost).  params from
         make_coll_params; raise_ref [B] the collision raise reference (None:
-        0).  Returns dict(cost, grad, terms [B, 4], collision, status)."""
+        0); near_field from coll_field(occupancy, params) (None: every
+        sample's box is scanned).  Returns dict(cost, grad, terms [B, 4],
+        collision, status)."""
         import torch
         B = self._coll_inputs(fixed_vals, x, times, occupancy, mode)
+        _check_field(near_field, occupancy)
         dev = x.device
         nz, ny, nx = occupancy.shape
         cost = torch.empty(B, dtype=torch.float64, device=dev)
@@ -377,18 +380,22 @@ class LinearPlan:
         ws = _workspace(workspace, nb, dev)
         check(lib().mtg_coll_cost(self._h, B, mode, _ptr(fixed_vals), _ptr(x),
                                   _ptr(times) if mode == 0 else None, _ptr(occupancy), nx, ny,
-                                  nz, ctypes.byref(params), _ptr(raise_ref), _ptr(cost), _ptr(g),
+                                  nz, _ptr(near_field), ctypes.byref(params), _ptr(raise_ref),
+                                  _ptr(cost), _ptr(g),
                                   _ptr(terms), _ptr(coll), _ptr(st), _ptr(ws), nb,
                                   _stream(dev)), "mtg_coll_cost")
         return dict(cost=cost, grad=g, terms=terms, collision=coll, status=st)
 
     def coll_optimize(self, fixed_vals, x0, times, occupancy, params, mode=0, max_evals=25,
-                      lower=None, upper=None, initial_step=None, workspace=None):
+                      lower=None, upper=None, initial_step=None, workspace=None,
+                      near_field=None):
         """Device L-BFGS over the collision objective (mtg_coll_optimize;
         optimizeFreeConstraintsAndCollision / ...AndTime with NLopt
-        replaced).  Returns dict(x, cost, evals, result, status, terms)."""
+        replaced); near_field as coll_cost.  Returns dict(x, cost, evals,
+        result, status, terms)."""
         import torch
         B = self._coll_inputs(fixed_vals, x0, times, occupancy, mode)
+        _check_field(near_field, occupancy)
         dev = x0.device
         nv = self._n_vars(mode)
         for a, name in ((lower, "lower"), (upper, "upper"), (initial_step, "initial_step")):
@@ -406,7 +413,8 @@ class LinearPlan:
         check(lib().mtg_coll_optimize(self._h, B, mode, _ptr(fixed_vals), _ptr(x),
                                       _ptr(times) if mode == 0 else None, _ptr(lower),
                                       _ptr(upper), _ptr(initial_step), _ptr(occupancy), nx, ny,
-                                      nz, ctypes.byref(params), max_evals, _ptr(cost), _ptr(ev),
+                                      nz, _ptr(near_field), ctypes.byref(params), max_evals,
+                                      _ptr(cost), _ptr(ev),
                                       _ptr(res), _ptr(st), _ptr(terms), _ptr(ws), nb,
                                       _stream(dev)), "mtg_coll_optimize")
         return dict(x=x, cost=cost, evals=ev, result=res, status=st, terms=terms)
@@ -632,6 +640,31 @@ def max_magnitude(coeffs, times, derivative, out=None):
                                   _ptr(out["time"]), _ptr(out["value"]), _ptr(out["segment"]),
                                   _stream(dev)), "mtg_max_magnitude")
     return out
+
+
+def _check_field(field, occupancy):
+    if field is None:
+        return
+    import torch
+    nz, ny, nx = occupancy.shape
+    if not (isinstance(field, torch.Tensor) and field.is_cuda and field.dtype == torch.int16 and
+            field.is_contiguous() and field.numel() == nz * ny * nx * 8):
+        raise MTGError("near_field must be coll_field()'s int16 CUDA tensor [nz, ny, nx, 8]")
+
+
+def coll_field(occupancy, params):
+    """Near field of an occupancy map for the collision walk (mtg_coll_field):
+    per voxel the seven box minima the walk would scan for (uint16 bits in an
+    int16 tensor [nz, ny, nx, 8]).  params: make_coll_params(...) or
+    make_collision_params(...) (only box_side is read).  Compute once per map
+    and pass as near_field to LinearPlan.coll_cost / coll_optimize."""
+    import torch
+    nz, ny, nx = occupancy.shape
+    cp = getattr(params, "coll", params)
+    field = torch.empty((nz, ny, nx, 8), dtype=torch.int16, device=occupancy.device)
+    check(lib().mtg_coll_field(_ptr(occupancy), nx, ny, nz, ctypes.byref(cp), _ptr(field),
+                               _stream(occupancy.device)), "mtg_coll_field")
+    return field
 
 
 def magnitude_candidates(coeffs, times, derivative, max_candidates=None):

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kWave) void coll_prep_kernel(PlanDev pl, CollDims c
 template <int N>
 __global__ __launch_bounds__(kCollBlock) void coll_walk_kernel(
     PlanDev pl, CollDims cd, const float* __restrict__ occ, int nx, int ny, int nz,
-    mtg_collision_params cp, double inc, CollWs w) {
+    const uint16_t* __restrict__ field, mtg_collision_params cp, double inc, CollWs w) {
   constexpr int D = 3;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int S = pl.S;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kCollBlock) void coll_walk_kernel(
       w.coll[prob] = 0;
     }
     if (q == 0)
-      for (int i = tid; i < cd.nfr; i += kCollBlock) w.gc[b * cd.nfr + i] = NAN;
+      for (int i = tid; i < cd.nfr; i += static_cast<int>(blockDim.x)) w.gc[b * cd.nfr + i] = NAN;
     return;
   }
   double* c_s = sm;               // S x D x N
@@ -253,21 +253,21 @@ __global__ __launch_bounds__(kCollBlock) void coll_walk_kernel(
   double* g_s = T_s + S;          // S x D x N
   double* scratch = g_s + S * D * N;
   const bool grad = q == 0;
-  for (int i = tid; i < S * D * N; i += kCollBlock) {
+  for (int i = tid; i < S * D * N; i += static_cast<int>(blockDim.x)) {
     c_s[i] = w.coeffs[b * S * D * N + i];
     if (grad) g_s[i] = 0.0;
   }
-  for (int i = tid; i < S; i += kCollBlock) T_s[i] = walk_time(cd, w.T + b * S, q, i, inc);
+  for (int i = tid; i < S; i += static_cast<int>(blockDim.x)) T_s[i] = walk_time(cd, w.T + b * S, q, i, inc);
   __syncthreads();
   double J;
   bool hit;
-  collision_walk<N>(S, c_s, T_s, occ, nx, ny, nz, cp, grad, g_s, scratch, &J, &hit);
+  collision_walk<N>(S, c_s, T_s, occ, nx, ny, nz, cp, grad, g_s, scratch, &J, &hit, field);
   if (tid == 0) {
     w.Jc[prob] = J;
     w.coll[prob] = hit ? 1 : 0;
   }
   if (grad)  // T_s is T itself for q = 0
-    for (int i = tid; i < cd.nfr; i += kCollBlock)
+    for (int i = tid; i < cd.nfr; i += static_cast<int>(blockDim.x))
       w.gc[b * cd.nfr + i] =
           coll_grad_free<N>(S, D, pl.np, pl.tab + N * N, pl.free_map, T_s, g_s, i);
 }
@@ -733,7 +733,8 @@ hipError_t prepare(K kernel, size_t bytes) {
 template <int N>
 hipError_t evaluate_n(const PlanDev& pl, const CollDims& cd, int64_t B, const double* df,
                       const double* xsrc, const double* times, const float* occ, int nx, int ny,
-                      int nz, const mtg_coll_params& p, const CollWs& w, hipStream_t st) {
+                      int nz, const uint16_t* field, const mtg_coll_params& p, const CollWs& w,
+                      hipStream_t st) {
   const size_t lds_prep = free_lds(N, pl.S, pl.D, pl.np, false).bytes;
   hipError_t e = prepare(coll_prep_kernel<N>, lds_prep);
   if (e != hipSuccess) return e;
@@ -741,8 +742,10 @@ hipError_t evaluate_n(const PlanDev& pl, const CollDims& cd, int64_t B, const do
                      times, xsrc, p.increment_time, w);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const size_t lds_walk = collision_lds_bytes(N, pl.S);
-  hipLaunchKernelGGL(coll_walk_kernel<N>, dim3(grid1(B * cd.P)), dim3(kCollBlock), lds_walk, st,
-                     pl, cd, occ, nx, ny, nz, p.coll, p.increment_time, w);
+  // With the near field one thread walks alone: one wave per walk.
+  hipLaunchKernelGGL(coll_walk_kernel<N>, dim3(grid1(B * cd.P)),
+                     dim3(field ? kWave : kCollBlock), lds_walk, st, pl, cd, occ, nx, ny, nz,
+                     field, p.coll, p.increment_time, w);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (cd.Q > 0) {
     hipLaunchKernelGGL(coll_soft_points_kernel<N>, dim3(grid1(B * cd.Q)), dim3(kWave), 0, st, pl,
@@ -791,7 +794,7 @@ int64_t coll_problems(const PlanDev& pl, int64_t B, int mode, const mtg_coll_par
 
 int coll_cost(const PlanDev& pl, int64_t B, int mode, const double* df, const double* x,
               const double* times, const float* occ, int nx, int ny, int nz,
-              const mtg_coll_params& p, const double* raise_ref, double* cost, double* grad,
+              const uint16_t* field, const mtg_coll_params& p, const double* raise_ref, double* cost, double* grad,
               double* terms, int32_t* collision, int32_t* status, void* workspace,
               size_t workspace_bytes, hipStream_t st) {
   const CollDims cd = coll_dims(pl, mode, p);
@@ -799,7 +802,7 @@ int coll_cost(const PlanDev& pl, int64_t B, int mode, const double* df, const do
   CollWs w;
   carve(workspace, cd, pl.N, B, p.n_soft, false, &w);
   hipError_t e;
-  MTG_COLL_DISPATCH(evaluate_n, pl, cd, B, df, x, times, occ, nx, ny, nz, p, w, st)
+  MTG_COLL_DISPATCH(evaluate_n, pl, cd, B, df, x, times, occ, nx, ny, nz, field, p, w, st)
   if (e != hipSuccess) return MTG_ERR_HIP;
   const CombineOut o{raise_ref, cost, grad, terms, collision, status};
   hipLaunchKernelGGL(coll_combine_kernel<false>, dim3(grid1(B)), dim3(kWave), 0, st, cd, p, 0,
@@ -810,7 +813,7 @@ int coll_cost(const PlanDev& pl, int64_t B, int mode, const double* df, const do
 int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, double* x_io,
                   const double* times, const double* lower, const double* upper,
                   const double* initial_step, const float* occ, int nx, int ny, int nz,
-                  const mtg_coll_params& p, int max_evals, double* cost, int32_t* evals,
+                  const uint16_t* field, const mtg_coll_params& p, int max_evals, double* cost, int32_t* evals,
                   int32_t* result, int32_t* status, double* terms, void* workspace,
                   size_t workspace_bytes, hipStream_t st) {
   const CollDims cd = coll_dims(pl, mode, p);
@@ -824,7 +827,7 @@ int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, doub
   const CombineOut none{};
   for (int round = 0; round < max_evals; ++round) {
     hipError_t e;
-    MTG_COLL_DISPATCH(evaluate_n, pl, cd, B, df, w.xt, times, occ, nx, ny, nz, p, w, st)
+    MTG_COLL_DISPATCH(evaluate_n, pl, cd, B, df, w.xt, times, occ, nx, ny, nz, field, p, w, st)
     if (e != hipSuccess) return MTG_ERR_HIP;
     hipLaunchKernelGGL(coll_combine_kernel<true>, dim3(grid1(B)), dim3(kWave), 0, st, cd, p,
                        max_evals, bd, w, none);

@@ -29,6 +29,8 @@
 
 #include <cmath>
 
+#include <stdint.h>
+
 #include "mtg_device.h"
 #include "mtg_internal.h"
 
@@ -51,164 +53,252 @@ __device__ inline double coll_potential(double d, const mtg_collision_params& p,
   return 0.0;
 }
 
-__device__ inline double coll_wg_min(double x, double* red) {
-  for (int off = 32; off > 0; off >>= 1) x = fmin(x, __shfl_xor(x, off, kWave));
+// The seven box minima reduced over the workgroup at once (one barrier
+// pair); red holds 7 x (kCollBlock / kWave) doubles.
+__device__ inline void coll_wg_min7(double (&m)[7], double* red) {
+  constexpr int W = kCollBlock / kWave;
+#pragma unroll
+  for (int q = 0; q < 7; ++q)
+    for (int off = 32; off > 0; off >>= 1) m[q] = fmin(m[q], __shfl_xor(m[q], off, kWave));
   const int w = threadIdx.x / kWave;
   __syncthreads();
-  if ((threadIdx.x & (kWave - 1)) == 0) red[w] = x;
+  if ((threadIdx.x & (kWave - 1)) == 0)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) red[q * W + w] = m[q];
   __syncthreads();
-  double m = red[0];
-  for (int i = 1; i < kCollBlock / kWave; ++i) m = fmin(m, red[i]);
-  return m;
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    double x = red[q * W];
+    for (int i = 1; i < W; ++i) x = fmin(x, red[q * W + i]);
+    m[q] = x;
+  }
 }
 
-// LDS scratch of one walk: smp (10 doubles) + red (kCollBlock / kWave).
-constexpr int kCollScratch = 10 + kCollBlock / kWave;
+// LDS scratch of one walk: smp (10 doubles) + red (7 x kCollBlock / kWave).
+constexpr int kCollScratch = 10 + 7 * (kCollBlock / kWave);
 
-// The walk over segments with coefficients c_s (S x 3 x N) and segment times
-// T_s (LDS).  g_s (S x 3 x N, LDS, zeroed by the caller) receives dJ_c/dc
-// when `grad`.  Called by all kCollBlock threads; on return every thread
-// holds J_c (0 on a collision) and the collision flag.
-template <int N>
-__device__ void collision_walk(int S, const double* c_s, const double* T_s, const float* occ,
-                               int nx, int ny, int nz, const mtg_collision_params& p, bool grad,
-                               double* g_s, double* scratch, double* J_out, bool* hit_out) {
-  constexpr int D = 3;
-  double* smp = scratch;      // pos[3], vel[3], time_sum, t, seg, flag
-  double* red = scratch + 10;  // reduction scratch
-  const int tid = threadIdx.x;
-  const double res = p.map_resolution, dt = p.coll_check_time_increment;
-  // Thread 0's walk state (nonlinear_impl:1670-1768).
+// The walk's box around voxel v: offsets a in [coll_box_lo(side),
+// coll_box_lo(side) + side + 1] on every axis.
+__host__ __device__ inline int coll_box_lo(int side) { return -(side / 2) - 1; }
+
+// m[0..6] of voxel (vx, vy, vz) from the near field; false outside the grid.
+__device__ inline bool coll_field_lookup(const uint16_t* __restrict__ field, int nx, int ny,
+                                         int nz, int vx, int vy, int vz, double (&m)[7]) {
+  if (vx < 0 || vy < 0 || vz < 0 || vx >= nx || vy >= ny || vz >= nz) return false;
+  const uint4 raw = *reinterpret_cast<const uint4*>(
+      field + ((static_cast<int64_t>(vz) * ny + vy) * nx + vx) * kFieldSlots);
+  const unsigned w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    const unsigned u = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+    m[q] = u == kFieldNone ? HUGE_VAL : static_cast<double>(u);
+  }
+  return true;
+}
+
+// The walk's box search for voxel (vx, vy, vz), voxels i = first, first +
+// stride, ... of the box (one thread: first = 0, stride = 1); minima folded
+// into m.
+__device__ inline void coll_box_scan(const float* __restrict__ occ, int nx, int ny, int nz,
+                                     int vx, int vy, int vz, int side, int first, int stride,
+                                     double (&m)[7]) {
+  const int lo = coll_box_lo(side), ext = side + 2;
+  const int lo_x = vx + lo, lo_y = vy + lo, lo_z = vz + lo;
+  const int nbox = ext * ext * ext;
+  for (int i = first; i < nbox; i += stride) {
+    const int x = lo_x + i % ext, y = lo_y + (i / ext) % ext, z = lo_z + i / (ext * ext);
+    if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) continue;
+    if (!(occ[(static_cast<int64_t>(z) * ny + y) * nx + x] >= 0.0f)) continue;
+    const double ax = x - vx, ay = y - vy, az = z - vz;
+    m[0] = fmin(m[0], ax * ax + ay * ay + az * az);
+    m[1] = fmin(m[1], (ax + 1) * (ax + 1) + ay * ay + az * az);  // v - e_x
+    m[2] = fmin(m[2], (ax - 1) * (ax - 1) + ay * ay + az * az);  // v + e_x
+    m[3] = fmin(m[3], ax * ax + (ay + 1) * (ay + 1) + az * az);
+    m[4] = fmin(m[4], ax * ax + (ay - 1) * (ay - 1) + az * az);
+    m[5] = fmin(m[5], ax * ax + ay * ay + (az + 1) * (az + 1));
+    m[6] = fmin(m[6], ax * ax + ay * ay + (az - 1) * (az - 1));
+  }
+}
+
+// Thread 0's walk state (nonlinear_impl:1670-1768).
+struct CollWalk {
   int seg = 0;
   double t = 0.0, time_sum = -1.0, dist_sum = 0.0, J = 0.0;
   double prev[3] = {0.0, 0.0, 0.0};
-  bool in_seg = false, coll = false;
-  for (;;) {
-    if (tid == 0) {
-      bool emit = false;
-      while (!emit && seg < S) {
-        if (!in_seg) {
-          t = 0.0;
-          in_seg = true;
-        } else {
-          t += dt;
-        }
-        if (!(t < T_s[seg])) {  // segment done: time_sum += -dt + (T_i - t)
-          time_sum += -dt + (T_s[seg] - t);
-          ++seg;
-          in_seg = false;
-          continue;
-        }
-        double pos[3], vel[3];
-        for (int d = 0; d < D; ++d) {
-          const double* cd = c_s + (seg * D + d) * N;
-          double x = cd[N - 1], v = (N - 1) * cd[N - 1];
-          for (int n = N - 2; n >= 0; --n) x = fma(x, t, cd[n]);
-          for (int n = N - 2; n >= 1; --n) v = fma(v, t, n * cd[n]);
-          pos[d] = x;
-          vel[d] = v;
-        }
-        if (time_sum < 0.0) {  // the first sample only seeds the integrals
-          time_sum = 0.0;
-          for (int d = 0; d < D; ++d) prev[d] = pos[d];
-          continue;
-        }
-        time_sum += dt;
-        double dd = 0.0;
-        for (int d = 0; d < D; ++d) dd += (pos[d] - prev[d]) * (pos[d] - prev[d]);
-        dist_sum += sqrt(dd);
-        for (int d = 0; d < D; ++d) prev[d] = pos[d];
-        if (dist_sum < res) continue;
-        for (int d = 0; d < D; ++d) {
-          smp[d] = pos[d];
-          smp[3 + d] = vel[d];
-        }
-        smp[6] = time_sum;
-        smp[7] = t;
-        smp[8] = seg;
-        emit = true;
+  bool in_seg = false;
+
+  // Advances to the next evaluated sample: smp = pos[3], vel[3], time_sum,
+  // t, seg.  False when the walk is over.
+  template <int N>
+  __device__ bool next(int S, const double* c_s, const double* T_s,
+                       const mtg_collision_params& p, double* smp) {
+    constexpr int D = 3;
+    const double res = p.map_resolution, dt = p.coll_check_time_increment;
+    while (seg < S) {
+      if (!in_seg) {
+        t = 0.0;
+        in_seg = true;
+      } else {
+        t += dt;
       }
-      smp[9] = emit ? 1.0 : 0.0;
+      if (!(t < T_s[seg])) {  // segment done: time_sum += -dt + (T_i - t)
+        time_sum += -dt + (T_s[seg] - t);
+        ++seg;
+        in_seg = false;
+        continue;
+      }
+      double pos[3], vel[3];
+      for (int d = 0; d < D; ++d) {
+        const double* cd = c_s + (seg * D + d) * N;
+        double x = cd[N - 1], v = (N - 1) * cd[N - 1];
+        for (int n = N - 2; n >= 0; --n) x = fma(x, t, cd[n]);
+        for (int n = N - 2; n >= 1; --n) v = fma(v, t, n * cd[n]);
+        pos[d] = x;
+        vel[d] = v;
+      }
+      if (time_sum < 0.0) {  // the first sample only seeds the integrals
+        time_sum = 0.0;
+        for (int d = 0; d < D; ++d) prev[d] = pos[d];
+        continue;
+      }
+      time_sum += dt;
+      double dd = 0.0;
+      for (int d = 0; d < D; ++d) dd += (pos[d] - prev[d]) * (pos[d] - prev[d]);
+      dist_sum += sqrt(dd);
+      for (int d = 0; d < D; ++d) prev[d] = pos[d];
+      if (dist_sum < res) continue;
+      for (int d = 0; d < D; ++d) {
+        smp[d] = pos[d];
+        smp[3 + d] = vel[d];
+      }
+      smp[6] = time_sum;
+      smp[7] = t;
+      smp[8] = seg;
+      return true;
+    }
+    return false;
+  }
+
+  // Consumes the evaluated sample smp with its box minima m (valid: inside
+  // the map bounds): J_c and (grad) dJ_c/dc.  True on a collision.
+  template <int N>
+  __device__ bool take(const double* smp, bool valid, const double (&m)[7],
+                       const mtg_collision_params& p, bool grad, double* g_s) {
+    constexpr int D = 3;
+    const double res = p.map_resolution;
+    // getDistanceOctree (:2031-2043): min |voxel - v| times res (an empty
+    // set gives max double); invalid states keep distance 0 (:1832-1839).
+    auto dist = [&](double d2) {
+      return d2 == HUGE_VAL ? 1.7976931348623157e308 * res : sqrt(d2) * res;
+    };
+    bool coll;
+    const double c = coll_potential(valid ? dist(m[0]) : 0.0, p, &coll);
+    if (coll) return true;
+    const double ts = smp[6], tt = smp[7];
+    const int s = static_cast<int>(smp[8]);
+    const double* vel = smp + 3;
+    const double vn = sqrt(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
+    J += c * vn * ts;
+    if (grad && vn > 1e-6) {  // :1729-1750 (else the gradient term is dropped)
+      double gp[3];
+      for (int k = 0; k < D; ++k) {
+        bool cl, cr;
+        const double left = coll_potential(dist(m[1 + 2 * k]), p, &cl);
+        const double right = coll_potential(dist(m[2 + 2 * k]), p, &cr);
+        gp[k] = (right - left) / (2.0 * res);
+      }
+      // eq. (14): d/dc_n of vn ts c(pos) with pos = sum c_n t^n,
+      // vel = sum n c_n t^(n-1).
+      for (int k = 0; k < D; ++k) {
+        double* g = g_s + (s * D + k) * N;
+        const double a = vn * ts * gp[k], bcoef = ts * c * vel[k] / vn;
+        double tn = 1.0, tn1 = 0.0;  // t^n, n t^(n-1)
+        for (int n = 0; n < N; ++n) {
+          g[n] += a * tn + bcoef * tn1;
+          tn1 = (n + 1) * tn;
+          tn *= tt;
+        }
+      }
+    }
+    dist_sum = 0.0;
+    time_sum = 0.0;
+    return false;
+  }
+};
+
+// is_valid_state (:1803-1811): within one voxel of the map bounds.
+__device__ inline bool coll_valid_state(const double* pos, const mtg_collision_params& p) {
+  const double res = p.map_resolution;
+  return !(pos[0] < p.min_bound[0] + res || pos[0] > p.max_bound[0] - res ||
+           pos[1] < p.min_bound[1] + res || pos[1] > p.max_bound[1] - res ||
+           pos[2] < p.min_bound[2] + res || pos[2] > p.max_bound[2] - res);
+}
+
+// The walk over segments with coefficients c_s (S x 3 x N) and segment times
+// T_s (LDS).  g_s (S x 3 x N, LDS, zeroed by the caller) receives dJ_c/dc
+// when `grad`.  Called by every thread of the workgroup (blockDim.x, a
+// multiple of 64 up to kCollBlock); on return every thread holds J_c (0 on a
+// collision) and the collision flag.  With a near field (mtg_coll_field)
+// thread 0 walks alone and looks every sample's minima up (a serial box
+// scan for a voxel outside the grid); without, the workgroup scans each
+// sample's box in parallel.
+template <int N>
+__device__ void collision_walk(int S, const double* c_s, const double* T_s, const float* occ,
+                               int nx, int ny, int nz, const mtg_collision_params& p, bool grad,
+                               double* g_s, double* scratch, double* J_out, bool* hit_out,
+                               const uint16_t* field = nullptr) {
+  double* smp = scratch;       // pos[3], vel[3], time_sum, t, seg, flag
+  double* red = scratch + 10;  // reduction scratch
+  const int tid = threadIdx.x;
+  const double res = p.map_resolution;
+  CollWalk wk;
+  if (field) {
+    if (tid == 0) {
+      bool hit = false;
+      while (wk.next<N>(S, c_s, T_s, p, smp)) {
+        const bool valid = coll_valid_state(smp, p);
+        // Voxel of the sample: (position / res).cast<int>() truncates
+        // toward zero.
+        const int vx = static_cast<int>(smp[0] / res), vy = static_cast<int>(smp[1] / res),
+                  vz = static_cast<int>(smp[2] / res);
+        double m[7];
+        for (int q = 0; q < 7; ++q) m[q] = HUGE_VAL;
+        if (valid && !coll_field_lookup(field, nx, ny, nz, vx, vy, vz, m))
+          coll_box_scan(occ, nx, ny, nz, vx, vy, vz, p.box_side, 0, 1, m);
+        if (wk.take<N>(smp, valid, m, p, grad, g_s)) {
+          hit = true;
+          break;
+        }
+      }
+      smp[9] = hit ? -1.0 : 0.0;
+      smp[6] = hit ? 0.0 : wk.J;
     }
     __syncthreads();
+    *J_out = smp[6];
+    *hit_out = smp[9] < 0.0;
+    __syncthreads();
+    return;
+  }
+  for (;;) {
+    if (tid == 0) smp[9] = wk.next<N>(S, c_s, T_s, p, smp) ? 1.0 : 0.0;
+    __syncthreads();
     if (smp[9] == 0.0) break;
-    const double px = smp[0], py = smp[1], pz = smp[2];
-    // is_valid_state (:1803-1811): within one voxel of the map bounds.
-    const bool valid = !(px < p.min_bound[0] + res || px > p.max_bound[0] - res ||
-                         py < p.min_bound[1] + res || py > p.max_bound[1] - res ||
-                         pz < p.min_bound[2] + res || pz > p.max_bound[2] - res);
-    // Voxel of the sample: (position / res).cast<int>() truncates toward zero.
-    const int vx = static_cast<int>(px / res), vy = static_cast<int>(py / res),
-              vz = static_cast<int>(pz / res);
-    // Nearest occupied voxel from the centre and its 6 neighbours over the
-    // voxels overlapping the box [v - side/2, v - side/2 + side].
-    const int side = p.box_side, lo_x = vx - side / 2 - 1, lo_y = vy - side / 2 - 1,
-              lo_z = vz - side / 2 - 1, ext = side + 2;
+    const bool valid = coll_valid_state(smp, p);
+    const int vx = static_cast<int>(smp[0] / res), vy = static_cast<int>(smp[1] / res),
+              vz = static_cast<int>(smp[2] / res);
     double m[7];
     for (int q = 0; q < 7; ++q) m[q] = HUGE_VAL;
     if (valid) {
-      const int nbox = ext * ext * ext;
-      for (int i = tid; i < nbox; i += kCollBlock) {
-        const int x = lo_x + i % ext, y = lo_y + (i / ext) % ext, z = lo_z + i / (ext * ext);
-        if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) continue;
-        if (!(occ[(static_cast<int64_t>(z) * ny + y) * nx + x] >= 0.0f)) continue;
-        const double ax = x - vx, ay = y - vy, az = z - vz;
-        m[0] = fmin(m[0], ax * ax + ay * ay + az * az);
-        m[1] = fmin(m[1], (ax + 1) * (ax + 1) + ay * ay + az * az);  // v - e_x
-        m[2] = fmin(m[2], (ax - 1) * (ax - 1) + ay * ay + az * az);  // v + e_x
-        m[3] = fmin(m[3], ax * ax + (ay + 1) * (ay + 1) + az * az);
-        m[4] = fmin(m[4], ax * ax + (ay - 1) * (ay - 1) + az * az);
-        m[5] = fmin(m[5], ax * ax + ay * ay + (az + 1) * (az + 1));
-        m[6] = fmin(m[6], ax * ax + ay * ay + (az - 1) * (az - 1));
-      }
-      for (int q = 0; q < 7; ++q) m[q] = coll_wg_min(m[q], red);
+      coll_box_scan(occ, nx, ny, nz, vx, vy, vz, p.box_side, tid, kCollBlock, m);
+      coll_wg_min7(m, red);
     }
-    if (tid == 0) {
-      // getDistanceOctree (:2031-2043): min |voxel - v| times res (an empty
-      // set gives max double); invalid states keep distance 0 (:1832-1839).
-      auto dist = [&](double d2) {
-        return d2 == HUGE_VAL ? 1.7976931348623157e308 * res : sqrt(d2) * res;
-      };
-      const double c = coll_potential(valid ? dist(m[0]) : 0.0, p, &coll);
-      if (!coll) {
-        const double ts = smp[6], tt = smp[7];
-        const int s = static_cast<int>(smp[8]);
-        const double* vel = smp + 3;
-        const double vn = sqrt(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
-        J += c * vn * ts;
-        if (grad && vn > 1e-6) {  // :1729-1750 (else the gradient term is dropped)
-          double gp[3];
-          for (int k = 0; k < D; ++k) {
-            bool cl, cr;
-            const double left = coll_potential(dist(m[1 + 2 * k]), p, &cl);
-            const double right = coll_potential(dist(m[2 + 2 * k]), p, &cr);
-            gp[k] = (right - left) / (2.0 * res);
-          }
-          // eq. (14): d/dc_n of vn ts c(pos) with pos = sum c_n t^n,
-          // vel = sum n c_n t^(n-1).
-          for (int k = 0; k < D; ++k) {
-            double* g = g_s + (s * D + k) * N;
-            const double a = vn * ts * gp[k], bcoef = ts * c * vel[k] / vn;
-            double tn = 1.0, tn1 = 0.0;  // t^n, n t^(n-1)
-            for (int n = 0; n < N; ++n) {
-              g[n] += a * tn + bcoef * tn1;
-              tn1 = (n + 1) * tn;
-              tn *= tt;
-            }
-          }
-        }
-        dist_sum = 0.0;
-        time_sum = 0.0;
-      } else {
-        smp[9] = -1.0;  // collision: stop
-      }
-    }
+    if (tid == 0 && wk.take<N>(smp, valid, m, p, grad, g_s)) smp[9] = -1.0;  // collision: stop
     __syncthreads();
     if (smp[9] < 0.0) break;
   }
   __syncthreads();
   const bool hit = smp[9] < 0.0;
-  if (tid == 0) smp[6] = hit ? 0.0 : J;
+  if (tid == 0) smp[6] = hit ? 0.0 : wk.J;
   __syncthreads();
   *J_out = smp[6];
   *hit_out = hit;

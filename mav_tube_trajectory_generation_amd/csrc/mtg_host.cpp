@@ -501,9 +501,26 @@ int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
       mtg::coll_workspace_bytes(plan->dev, B, mode, *params, optimize != 0));
 }
 
+int64_t mtg_coll_field_bytes(int nx, int ny, int nz) {
+  if (nx < 0 || ny < 0 || nz < 0) return MTG_ERR_INVALID_ARG;
+  return static_cast<int64_t>(nx) * ny * nz * mtg::kFieldSlots * sizeof(uint16_t);
+}
+
+int mtg_coll_field(const float* occupancy, int nx, int ny, int nz,
+                   const mtg_collision_params* params, uint16_t* field, void* stream) {
+  if (!params || !valid_collision_params(*params, nx, ny, nz) ||
+      !mtg::coll_field_supported(params->box_side))
+    return MTG_ERR_INVALID_ARG;
+  if (static_cast<int64_t>(nx) * ny * nz == 0) return MTG_OK;
+  if (!occupancy || !field) return MTG_ERR_INVALID_ARG;
+  return from_hip(mtg::launch_coll_field(occupancy, nx, ny, nz, params->box_side, field,
+                                         static_cast<hipStream_t>(stream)));
+}
+
 int mtg_coll_cost(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
                   const double* x, const double* times, const float* occupancy, int nx,
-                  int ny, int nz, const mtg_coll_params* params, const double* raise_ref,
+                  int ny, int nz, const uint16_t* near_field, const mtg_coll_params* params,
+                  const double* raise_ref,
                   double* cost, double* grad, double* terms, int32_t* collision,
                   int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || !valid_coll_params(plan, mode, params) ||
@@ -514,15 +531,16 @@ int mtg_coll_cost(const mtg_plan* plan, int64_t B, int mode, const double* fixed
   if (!fixed_vals || !x || (mode == 0 && !times) || !workspace ||
       (!occupancy && static_cast<int64_t>(nx) * ny * nz > 0))
     return MTG_ERR_INVALID_ARG;
-  return mtg::coll_cost(plan->dev, B, mode, fixed_vals, x, times, occupancy, nx, ny, nz, *params,
-                        raise_ref, cost, grad, terms, collision, status, workspace,
+  return mtg::coll_cost(plan->dev, B, mode, fixed_vals, x, times, occupancy, nx, ny, nz,
+                        near_field, *params, raise_ref, cost, grad, terms, collision, status, workspace,
                         workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
 int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
                       double* x_io, const double* times, const double* lower,
                       const double* upper, const double* initial_step, const float* occupancy,
-                      int nx, int ny, int nz, const mtg_coll_params* params, int max_evals,
+                      int nx, int ny, int nz, const uint16_t* near_field,
+                      const mtg_coll_params* params, int max_evals,
                       double* cost, int32_t* evals, int32_t* result, int32_t* status,
                       double* terms, void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || max_evals < 1 || !valid_coll_params(plan, mode, params) ||
@@ -534,7 +552,8 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
       (!occupancy && static_cast<int64_t>(nx) * ny * nz > 0))
     return MTG_ERR_INVALID_ARG;
   return mtg::coll_optimize(plan->dev, B, mode, fixed_vals, x_io, times, lower, upper,
-                            initial_step, occupancy, nx, ny, nz, *params, max_evals, cost, evals,
+                            initial_step, occupancy, nx, ny, nz, near_field, *params, max_evals,
+                            cost, evals,
                             result, status, terms, workspace, workspace_bytes,
                             static_cast<hipStream_t>(stream));
 }

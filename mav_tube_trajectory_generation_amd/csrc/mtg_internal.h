@@ -187,6 +187,17 @@ struct SoftCostArgs {
 };
 // Collision cost over a dense occupancy grid (mtg_collision.hip).
 size_t collision_lds_bytes(int N, int S);
+// Near field of an occupancy map for the collision walk (mtg_coll_field,
+// mtg_collision.hip): per voxel v, in kFieldSlots uint16 slots, the squared
+// voxel distances from v and from its 6 axis neighbours (v - e_x, v + e_x,
+// v - e_y, v + e_y, v - e_z, v + e_z) to the nearest occupied voxel of the
+// box the walk scans around v, or kFieldNone when the box holds none:
+// exactly the walk's minima m[0..6].
+constexpr int kFieldSlots = 8;
+constexpr unsigned kFieldNone = 0xFFFFu;
+bool coll_field_supported(int side);
+hipError_t launch_coll_field(const float* occ, int nx, int ny, int nz, int side,
+                             uint16_t* field, hipStream_t st);
 hipError_t launch_collision_cost(const PlanDev& pl, int64_t B, const double* coeffs,
                                  const double* times, const float* occ, int nx, int ny, int nz,
                                  const mtg_collision_params& p, double* cost, int32_t* coll,
@@ -235,13 +246,13 @@ size_t coll_workspace_bytes(const PlanDev& pl, int64_t B, int mode, const mtg_co
 int64_t coll_problems(const PlanDev& pl, int64_t B, int mode, const mtg_coll_params& p);
 int coll_cost(const PlanDev& pl, int64_t B, int mode, const double* df, const double* x,
               const double* times, const float* occ, int nx, int ny, int nz,
-              const mtg_coll_params& p, const double* raise_ref, double* cost, double* grad,
+              const uint16_t* field, const mtg_coll_params& p, const double* raise_ref, double* cost, double* grad,
               double* terms, int32_t* collision, int32_t* status, void* workspace,
               size_t workspace_bytes, hipStream_t st);
 int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, double* x_io,
                   const double* times, const double* lower, const double* upper,
                   const double* initial_step, const float* occ, int nx, int ny, int nz,
-                  const mtg_coll_params& p, int max_evals, double* cost, int32_t* evals,
+                  const uint16_t* field, const mtg_coll_params& p, int max_evals, double* cost, int32_t* evals,
                   int32_t* result, int32_t* status, double* terms, void* workspace,
                   size_t workspace_bytes, hipStream_t st);
 

@@ -2965,4 +2965,49 @@ int orc_coll_optimize(int N, int D, int r, int S, int K, const uint8_t* mask, co
   return 0;
 }
 
+// CPU baseline of bench.py's collision workload: orc_coll_optimize (mode 0,
+// unbounded, default initial step) cycling over the B starts X0 [B][nv] of
+// one problem, `threads` std::threads, until min_seconds have passed.
+int orc_bench_coll(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                   const double* times, const float* occupancy, int nx, int ny, int nz,
+                   const double* params, const int* iparams, const int* soft_derivatives,
+                   const double* soft_limits, int B, int nv, const double* X0, int max_evals,
+                   int threads, double min_seconds, int64_t* units, double* seconds) {
+  if (B < 1 || nv < 1 || threads < 1 || !X0) return -1;
+  std::atomic<int> failed(0);
+  std::atomic<int64_t> total(0);
+  volatile double sink = 0.0;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto worker = [&](int tid) {
+    int64_t n = 0;
+    double acc = 0.0;
+    std::vector<double> x(nv);
+    for (int64_t it = tid;; it += threads) {
+      const int b = static_cast<int>(it % B);
+      std::copy(X0 + static_cast<size_t>(b) * nv, X0 + static_cast<size_t>(b + 1) * nv,
+                x.begin());
+      double c = 0.0, terms[4];
+      int ev = 0, res = 0;
+      if (orc_coll_optimize(N, D, r, S, K, mask, vals, times, 0, occupancy, nx, ny, nz, params,
+                            iparams, soft_derivatives, soft_limits, nullptr, nullptr, nullptr,
+                            max_evals, x.data(), &c, &ev, &res, terms))
+        failed = 1;
+      acc += c;
+      ++n;
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0)
+                            .count();
+      if (el >= min_seconds || failed) break;
+    }
+    total += n;
+    sink = sink + acc;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(worker, t);
+  worker(0);
+  for (auto& th : pool) th.join();
+  *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  *units = total;
+  return failed ? -2 : 0;
+}
+
 }  // extern "C"

@@ -295,6 +295,14 @@ int orc_coll_optimize(int N, int D, int r, int S, int K, const uint8_t* mask, co
                       int max_evals, double* x_io, double* cost, int* evals, int* result,
                       double* terms);
 
+// CPU baseline of bench.py's collision workload (orc_coll_optimize mode 0
+// over B starts X0 [B][nv], `threads` threads, >= min_seconds).
+int orc_bench_coll(int N, int D, int r, int S, int K, const uint8_t* mask, const double* vals,
+                   const double* times, const float* occupancy, int nx, int ny, int nz,
+                   const double* params, const int* iparams, const int* soft_derivatives,
+                   const double* soft_limits, int B, int nv, const double* X0, int max_evals,
+                   int threads, double min_seconds, int64_t* units, double* seconds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -607,6 +607,32 @@ def coll_cost(N, r, vertices, times, mode, x, occupancy, params, raise_ref=0.0):
     return float(cost[0]), grad, terms, coll.value
 
 
+def bench_coll(N, r, vertices, times, occupancy, params, X0, max_evals, threads=1,
+               seconds=2.0):
+    """orc_bench_coll: CPU rate of orc_coll_optimize (mode 0) cycling over the
+    starts X0 [B, nv].  Returns (optimisations, seconds)."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    occ = np.ascontiguousarray(occupancy, dtype=np.float32)
+    nz, ny, nx = occ.shape
+    prm, ip, der, lim = _coll_arrays(params)
+    X0 = np.ascontiguousarray(X0, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    units = ctypes.c_int64()
+    sec = np.zeros(1)
+    L = lib()
+    L.orc_bench_coll.argtypes = [ctypes.c_int] * 5 + [_u8p, _dp, _dp] + [
+        ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _ip, _ip,
+        _dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+        ctypes.POINTER(ctypes.c_int64), _dp]
+    _check(L.orc_bench_coll(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                            _d(vertices.vals), _d(times),
+                            occ.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), nx, ny, nz,
+                            _d(prm), ip.ctypes.data_as(_ip), der.ctypes.data_as(_ip), _d(lim),
+                            X0.shape[0], X0.shape[1], _d(X0), max_evals, threads, seconds,
+                            ctypes.byref(units), _d(sec)), "bench_coll")
+    return units.value, float(sec[0])
+
+
 def coll_optimize(N, r, vertices, times, mode, x0, occupancy, params, max_evals, lower=None,
                   upper=None, initial_step=None):
     """orc_coll_optimize: the mtg_coll_optimize algorithm (projected L-BFGS)

@@ -169,3 +169,68 @@ def test_coll_rejects_bad_arguments(ctx, dev):
         plan.coll_cost(*args, mtg.make_coll_params(**coll_params(map_resolution=0.0)))
     with pytest.raises(MTGError):  # soft limit must be positive
         plan.coll_cost(*args, mtg.make_coll_params(**coll_params(soft=[(1, 0.0)])))
+
+
+def _field_numpy(occ, side):
+    """The walk's box minima per voxel (collision_walk's m[0..6]) by brute
+    force: squared voxel distances from v and v -+ e_x, e_y, e_z to the
+    occupied voxels of the box [v + lo, v + lo + side + 1], lo = -(side/2)-1."""
+    nz, ny, nx = occ.shape
+    lo, ext = -(side // 2) - 1, side + 2
+    occd = np.argwhere(occ >= 0)  # (z, y, x)
+    out = np.full((nz, ny, nx, 7), 0xFFFF, np.int64)
+    sh = [(0, 0, 0), (-1, 0, 0), (1, 0, 0), (0, -1, 0), (0, 1, 0), (0, 0, -1), (0, 0, 1)]
+    for z in range(nz):
+        for y in range(ny):
+            for x in range(nx):
+                a = occd - np.array([z, y, x])  # (az, ay, ax)
+                inb = np.all((a >= lo) & (a < lo + ext), axis=1)
+                if not inb.any():
+                    continue
+                a = a[inb]
+                for q, (dx, dy, dz) in enumerate(sh):
+                    out[z, y, x, q] = np.min((a[:, 2] - dx) ** 2 + (a[:, 1] - dy) ** 2 +
+                                             (a[:, 0] - dz) ** 2)
+    return out
+
+
+@pytest.mark.parametrize("side", [3, 8])
+def test_coll_field_matches_brute_force(dev, side):
+    """mtg_coll_field against a brute-force numpy restatement of the walk's
+    box search on a small random map with edges (voxels outside the grid are
+    free)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    rng = np.random.default_rng(side)
+    occ = np.where(rng.random((7, 11, 13)) < 0.04, 1.0, -1.0).astype(np.float32)
+    prm = mtg.make_collision_params(0.1, (0.0, 0.0, 0.0), (1.3, 1.1, 0.7), box_side=side)
+    f = mtg.coll_field(_T(occ, dev), prm).cpu().numpy().view(np.uint16).astype(np.int64)
+    want = _field_numpy(occ, side)
+    assert np.array_equal(f[..., :7], want)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_coll_near_field_bit_identical(ctx, dev, mode):
+    """The walk with the near field (one thread, one load per sample) gives
+    the same bits as the workgroup box scan: cost, gradient, terms, collision
+    flags, and the optimiser's path."""
+    import mav_tube_trajectory_generation_amd as mtg
+    plan, vt, t, x0, df = _setup(ctx, dev)
+    occ = _T(forest_map(), dev)
+    prm = mtg.make_coll_params(**coll_params(**VARIANTS["soft"]))
+    starts = [x0] + perturbed_starts(x0, 11, 0.02)
+    if mode == 1:
+        starts = [np.concatenate([t, x]) for x in starts]
+    X = np.array(starts)
+    B = X.shape[0]
+    field = mtg.coll_field(occ, prm)
+    args = (_T(np.repeat(df[None], B, 0), dev), _T(X, dev), _T(np.repeat(t[None], B, 0), dev),
+            occ, prm)
+    a = plan.coll_cost(*args, mode=mode)
+    b = plan.coll_cost(*args, mode=mode, near_field=field)
+    for k in ("cost", "grad", "terms", "collision", "status"):
+        assert np.array_equal(a[k].cpu().numpy(), b[k].cpu().numpy()), k
+    assert 0 < int(a["collision"].sum()) < B  # both outcomes exercised
+    oa = plan.coll_optimize(*args, mode=mode, max_evals=10)
+    ob = plan.coll_optimize(*args, mode=mode, max_evals=10, near_field=field)
+    for k in ("x", "cost", "evals", "result", "status", "terms"):
+        assert np.array_equal(oa[k].cpu().numpy(), ob[k].cpu().numpy()), k

@@ -20,6 +20,8 @@ LD_LBFGS is unpinned.  What is pinned here:
   * the soft-constraint gradient as the central difference of the soft cost.
 """
 import numpy as np
+
+import mav_tube_trajectory_generation_amd.demo as demo
 import pytest
 
 import numpy_ref
@@ -312,3 +314,16 @@ def test_main_problem_fixture(oracle):
                                        coll_params())
     assert c == 0 and J > 0.0
     assert D == 3
+
+
+def test_demo_module_matches_fixture(oracle):
+    """The package's demo data (bench.py's collision workload) equals the
+    oracle's view of main.cpp: segment times (estimateSegmentTimes), the tube
+    pattern's mask and fixed values."""
+    from coll_fixture import main_problem
+    from helpers import compact_fixed
+    v, vt, t, _ = main_problem()
+    assert np.array_equal(demo.estimate_segment_times(demo.MAIN_POSITIONS, 2.0, 2.0), t)
+    mask, df = compact_fixed(vt, demo.N)
+    dmask, ddf = demo.tube_pattern(demo.MAIN_POSITIONS)
+    assert np.array_equal(mask, dmask) and np.array_equal(df, ddf)

@@ -19,6 +19,8 @@ case "${1:-benches}" in
     B --workload time-qcqp --steps 5 --warmup 1 > gpurun_out/bench_time_qcqp.json 2> gpurun_out/bench_time_qcqp.err
     B --workload extrema > gpurun_out/bench_extrema.json 2> gpurun_out/bench_extrema.err
     B --workload sample > gpurun_out/bench_sample.json 2> gpurun_out/bench_sample.err
+    B --workload collision --steps 5 --warmup 1 > gpurun_out/bench_collision.json 2> gpurun_out/bench_collision.err
+    B --batch 8192 --kernel lane --no-cpu-baseline > gpurun_out/bench_linear_8192_lane.json 2> gpurun_out/bench_linear_8192_lane.err
     ;;
   profiles)
     bash tools/profile.sh linear
