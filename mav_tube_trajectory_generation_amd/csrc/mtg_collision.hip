@@ -140,7 +140,7 @@ hipError_t launch_coll_field(const float* occ, int nx, int ny, int nz, int side,
 }
 
 size_t collision_lds_bytes(int N, int S) {
-  return sizeof(double) * (2 * S * 3 * N + S + kCollScratch);
+  return sizeof(double) * (2 * S * 3 * N + S + coll_scratch_doubles(N));
 }
 
 hipError_t launch_collision_cost(const PlanDev& pl, int64_t B, const double* coeffs,

@@ -74,9 +74,6 @@ __device__ inline void coll_wg_min7(double (&m)[7], double* red) {
   }
 }
 
-// LDS scratch of one walk: smp (10 doubles) + red (7 x kCollBlock / kWave).
-constexpr int kCollScratch = 10 + 7 * (kCollBlock / kWave);
-
 // The walk's box around voxel v: offsets a in [coll_box_lo(side),
 // coll_box_lo(side) + side + 1] on every axis.
 __host__ __device__ inline int coll_box_lo(int side) { return -(side / 2) - 1; }
@@ -120,112 +117,6 @@ __device__ inline void coll_box_scan(const float* __restrict__ occ, int nx, int 
   }
 }
 
-// Thread 0's walk state (nonlinear_impl:1670-1768).
-struct CollWalk {
-  int seg = 0;
-  double t = 0.0, time_sum = -1.0, dist_sum = 0.0, J = 0.0;
-  double prev[3] = {0.0, 0.0, 0.0};
-  bool in_seg = false;
-
-  // Advances to the next evaluated sample: smp = pos[3], vel[3], time_sum,
-  // t, seg.  False when the walk is over.
-  template <int N>
-  __device__ bool next(int S, const double* c_s, const double* T_s,
-                       const mtg_collision_params& p, double* smp) {
-    constexpr int D = 3;
-    const double res = p.map_resolution, dt = p.coll_check_time_increment;
-    while (seg < S) {
-      if (!in_seg) {
-        t = 0.0;
-        in_seg = true;
-      } else {
-        t += dt;
-      }
-      if (!(t < T_s[seg])) {  // segment done: time_sum += -dt + (T_i - t)
-        time_sum += -dt + (T_s[seg] - t);
-        ++seg;
-        in_seg = false;
-        continue;
-      }
-      double pos[3], vel[3];
-      for (int d = 0; d < D; ++d) {
-        const double* cd = c_s + (seg * D + d) * N;
-        double x = cd[N - 1], v = (N - 1) * cd[N - 1];
-        for (int n = N - 2; n >= 0; --n) x = fma(x, t, cd[n]);
-        for (int n = N - 2; n >= 1; --n) v = fma(v, t, n * cd[n]);
-        pos[d] = x;
-        vel[d] = v;
-      }
-      if (time_sum < 0.0) {  // the first sample only seeds the integrals
-        time_sum = 0.0;
-        for (int d = 0; d < D; ++d) prev[d] = pos[d];
-        continue;
-      }
-      time_sum += dt;
-      double dd = 0.0;
-      for (int d = 0; d < D; ++d) dd += (pos[d] - prev[d]) * (pos[d] - prev[d]);
-      dist_sum += sqrt(dd);
-      for (int d = 0; d < D; ++d) prev[d] = pos[d];
-      if (dist_sum < res) continue;
-      for (int d = 0; d < D; ++d) {
-        smp[d] = pos[d];
-        smp[3 + d] = vel[d];
-      }
-      smp[6] = time_sum;
-      smp[7] = t;
-      smp[8] = seg;
-      return true;
-    }
-    return false;
-  }
-
-  // Consumes the evaluated sample smp with its box minima m (valid: inside
-  // the map bounds): J_c and (grad) dJ_c/dc.  True on a collision.
-  template <int N>
-  __device__ bool take(const double* smp, bool valid, const double (&m)[7],
-                       const mtg_collision_params& p, bool grad, double* g_s) {
-    constexpr int D = 3;
-    const double res = p.map_resolution;
-    // getDistanceOctree (:2031-2043): min |voxel - v| times res (an empty
-    // set gives max double); invalid states keep distance 0 (:1832-1839).
-    auto dist = [&](double d2) {
-      return d2 == HUGE_VAL ? 1.7976931348623157e308 * res : sqrt(d2) * res;
-    };
-    bool coll;
-    const double c = coll_potential(valid ? dist(m[0]) : 0.0, p, &coll);
-    if (coll) return true;
-    const double ts = smp[6], tt = smp[7];
-    const int s = static_cast<int>(smp[8]);
-    const double* vel = smp + 3;
-    const double vn = sqrt(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
-    J += c * vn * ts;
-    if (grad && vn > 1e-6) {  // :1729-1750 (else the gradient term is dropped)
-      double gp[3];
-      for (int k = 0; k < D; ++k) {
-        bool cl, cr;
-        const double left = coll_potential(dist(m[1 + 2 * k]), p, &cl);
-        const double right = coll_potential(dist(m[2 + 2 * k]), p, &cr);
-        gp[k] = (right - left) / (2.0 * res);
-      }
-      // eq. (14): d/dc_n of vn ts c(pos) with pos = sum c_n t^n,
-      // vel = sum n c_n t^(n-1).
-      for (int k = 0; k < D; ++k) {
-        double* g = g_s + (s * D + k) * N;
-        const double a = vn * ts * gp[k], bcoef = ts * c * vel[k] / vn;
-        double tn = 1.0, tn1 = 0.0;  // t^n, n t^(n-1)
-        for (int n = 0; n < N; ++n) {
-          g[n] += a * tn + bcoef * tn1;
-          tn1 = (n + 1) * tn;
-          tn *= tt;
-        }
-      }
-    }
-    dist_sum = 0.0;
-    time_sum = 0.0;
-    return false;
-  }
-};
-
 // is_valid_state (:1803-1811): within one voxel of the map bounds.
 __device__ inline bool coll_valid_state(const double* pos, const mtg_collision_params& p) {
   const double res = p.map_resolution;
@@ -234,74 +125,243 @@ __device__ inline bool coll_valid_state(const double* pos, const mtg_collision_p
            pos[2] < p.min_bound[2] + res || pos[2] > p.max_bound[2] - res);
 }
 
+// Scratch doubles of one walk (LDS, after c_s / T_s / g_s): control words,
+// the chunk's evaluated voxels (for the workgroup box scans), the min
+// reduction, and the chunk's gradient rows (t^0..t^(N-1), a[3], b[3] per
+// sample).
+__host__ __device__ constexpr int coll_scratch_doubles(int N) {
+  return 8 + 2 * kWave + 7 * (kCollBlock / kWave) + kWave * (N + 6);
+}
+
+// Lane l's x (l wave-uniform).
+__device__ inline double coll_readlane(double x, int l) {
+  const unsigned long long v = static_cast<unsigned long long>(__double_as_longlong(x));
+  const unsigned lo = static_cast<unsigned>(
+      __builtin_amdgcn_readlane(static_cast<int>(static_cast<unsigned>(v)), l));
+  const unsigned hi = static_cast<unsigned>(
+      __builtin_amdgcn_readlane(static_cast<int>(static_cast<unsigned>(v >> 32)), l));
+  return __longlong_as_double(
+      static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+
+// LDS written by some lanes of a wave and read by others after it.
+__device__ inline void coll_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // The walk over segments with coefficients c_s (S x 3 x N) and segment times
 // T_s (LDS).  g_s (S x 3 x N, LDS, zeroed by the caller) receives dJ_c/dc
-// when `grad`.  Called by every thread of the workgroup (blockDim.x, a
-// multiple of 64 up to kCollBlock); on return every thread holds J_c (0 on a
-// collision) and the collision flag.  With a near field (mtg_coll_field)
-// thread 0 walks alone and looks every sample's minima up (a serial box
-// scan for a voxel outside the grid); without, the workgroup scans each
-// sample's box in parallel.
+// when `grad`.  Called by every thread of the workgroup (blockDim.x = kWave
+// with a near field, kCollBlock without); on return every thread holds J_c
+// (0 on a collision) and the collision flag.
+//
+// Wave 0 takes the sample sequence in chunks of up to 64 samples of one
+// segment, lane j holding sample j:
+//   1. the times t0, t0 + dt, ... (the reference's repeated addition, a
+//      64-step uniform chain), positions and velocities by Horner per lane,
+//      the path length from the previous sample by a lane shuffle;
+//   2. a uniform scan in sample order applies the reference's running sums
+//      (the first sample, or one after time_sum went negative at a segment
+//      end, only seeds; a sample is evaluated once dist_sum >= res; both sums
+//      reset after it), marking the evaluated samples and their time_sum;
+//   3. every evaluated sample's seven box minima at once: a near-field lookup
+//      per lane (a serial scan for a voxel outside the grid), or without the
+//      field one workgroup box scan per evaluated sample;
+//   4. the potential per lane; the first colliding evaluated sample ends the
+//      walk; J_c += c |v| time_sum over the evaluated samples before it, in
+//      order, and with `grad` the eq. (14) terms, lane (k, n) of the
+//      coefficient gradient adding sample after sample from the LDS rows.
+// Every floating-point sum runs in the reference's order, so a chunked walk
+// equals the sample-by-sample one bit for bit.
 template <int N>
 __device__ void collision_walk(int S, const double* c_s, const double* T_s, const float* occ,
                                int nx, int ny, int nz, const mtg_collision_params& p, bool grad,
                                double* g_s, double* scratch, double* J_out, bool* hit_out,
                                const uint16_t* field = nullptr) {
-  double* smp = scratch;       // pos[3], vel[3], time_sum, t, seg, flag
-  double* red = scratch + 10;  // reduction scratch
-  const int tid = threadIdx.x;
-  const double res = p.map_resolution;
-  CollWalk wk;
-  if (field) {
-    if (tid == 0) {
-      bool hit = false;
-      while (wk.next<N>(S, c_s, T_s, p, smp)) {
-        const bool valid = coll_valid_state(smp, p);
-        // Voxel of the sample: (position / res).cast<int>() truncates
-        // toward zero.
-        const int vx = static_cast<int>(smp[0] / res), vy = static_cast<int>(smp[1] / res),
-                  vz = static_cast<int>(smp[2] / res);
-        double m[7];
-        for (int q = 0; q < 7; ++q) m[q] = HUGE_VAL;
-        if (valid && !coll_field_lookup(field, nx, ny, nz, vx, vy, vz, m))
-          coll_box_scan(occ, nx, ny, nz, vx, vy, vz, p.box_side, 0, 1, m);
-        if (wk.take<N>(smp, valid, m, p, grad, g_s)) {
-          hit = true;
-          break;
+  constexpr int D = 3, RW = N + 6;
+  static_assert(D * N <= kWave, "one lane per gradient coefficient");
+  double* ctl = scratch;                           // [0] chunk, [1] boxes, [2] J, [3] hit
+  int* evl = reinterpret_cast<int*>(scratch + 8);  // kWave x {vx, vy, vz, lane}
+  double* red = scratch + 8 + 2 * kWave;
+  double* rows = red + 7 * (kCollBlock / kWave);   // kWave x RW
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const bool w0 = tid < kWave;
+  const double res = p.map_resolution, dt = p.coll_check_time_increment;
+  auto dist = [&](double d2) {  // getDistanceOctree (:2031-2043); empty set: max double
+    return d2 == HUGE_VAL ? 1.7976931348623157e308 * res : sqrt(d2) * res;
+  };
+  // Wave 0's walk state, uniform over its lanes (nonlinear_impl:1670-1768).
+  int seg = 0;
+  double t0 = 0.0, time_sum = -1.0, dist_sum = 0.0, J = 0.0;
+  double prev[3] = {0.0, 0.0, 0.0};
+  bool hit = false;
+  for (;;) {
+    int n_in = 0;
+    double T = 0.0, t_end = 0.0, tj = 0.0, ts_me = 0.0;
+    double pos[3] = {0.0, 0.0, 0.0}, vel[3] = {0.0, 0.0, 0.0};
+    unsigned long long ev = 0;
+    if (w0) {
+      while (!hit && seg < S) {  // the next segment with samples left
+        T = T_s[seg];
+        double cur = t0;
+        int k = 0;
+        for (; k < kWave && cur < T; ++k) {
+          if (lane == k) tj = cur;
+          cur += dt;
+        }
+        n_in = k;
+        t_end = cur;
+        if (n_in > 0) break;
+        time_sum += -dt + (T - cur);  // segment done: its first failing t
+        ++seg;
+        t0 = 0.0;
+      }
+      if (lane < n_in) {
+        for (int d = 0; d < D; ++d) {
+          const double* cd = c_s + (seg * D + d) * N;
+          double x = cd[N - 1], v = (N - 1) * cd[N - 1];
+          for (int n = N - 2; n >= 0; --n) x = fma(x, tj, cd[n]);
+          for (int n = N - 2; n >= 1; --n) v = fma(v, tj, n * cd[n]);
+          pos[d] = x;
+          vel[d] = v;
         }
       }
-      smp[9] = hit ? -1.0 : 0.0;
-      smp[6] = hit ? 0.0 : wk.J;
+      double dd = 0.0;
+      for (int d = 0; d < D; ++d) {
+        double q = __shfl(pos[d], (lane + kWave - 1) & (kWave - 1), kWave);
+        if (lane == 0) q = prev[d];
+        dd += (pos[d] - q) * (pos[d] - q);
+      }
+      const double sl = sqrt(dd);
+      for (int j = 0; j < n_in; ++j) {
+        const double s = coll_readlane(sl, j);
+        if (time_sum < 0.0) {  // seeds the integrals only
+          time_sum = 0.0;
+          continue;
+        }
+        time_sum += dt;
+        dist_sum += s;
+        if (dist_sum < res) continue;
+        ev |= 1ull << j;
+        ts_me = lane == j ? time_sum : ts_me;
+        dist_sum = 0.0;
+        time_sum = 0.0;
+      }
+      if (!field) {  // the evaluated voxels inside the bounds, in order
+        const bool e = (ev >> lane) & 1ull;
+        const bool valid = e && coll_valid_state(pos, p);
+        const unsigned long long vm = __ballot(valid);
+        if (valid) {
+          int* en = evl + 4 * __popcll(vm & ((1ull << lane) - 1ull));
+          en[0] = static_cast<int>(pos[0] / res);
+          en[1] = static_cast<int>(pos[1] / res);
+          en[2] = static_cast<int>(pos[2] / res);
+          en[3] = lane;
+        }
+        if (lane == 0) ctl[1] = __popcll(vm);
+      }
+      if (lane == 0) ctl[0] = n_in > 0 ? 1.0 : 0.0;
     }
     __syncthreads();
-    *J_out = smp[6];
-    *hit_out = smp[9] < 0.0;
-    __syncthreads();
-    return;
-  }
-  for (;;) {
-    if (tid == 0) smp[9] = wk.next<N>(S, c_s, T_s, p, smp) ? 1.0 : 0.0;
-    __syncthreads();
-    if (smp[9] == 0.0) break;
-    const bool valid = coll_valid_state(smp, p);
-    const int vx = static_cast<int>(smp[0] / res), vy = static_cast<int>(smp[1] / res),
-              vz = static_cast<int>(smp[2] / res);
+    if (ctl[0] == 0.0) break;
     double m[7];
     for (int q = 0; q < 7; ++q) m[q] = HUGE_VAL;
-    if (valid) {
-      coll_box_scan(occ, nx, ny, nz, vx, vy, vz, p.box_side, tid, kCollBlock, m);
-      coll_wg_min7(m, red);
+    if (!field) {
+      const int n_box = static_cast<int>(ctl[1]);
+      for (int e = 0; e < n_box; ++e) {
+        const int* en = evl + 4 * e;
+        double mm[7];
+        for (int q = 0; q < 7; ++q) mm[q] = HUGE_VAL;
+        coll_box_scan(occ, nx, ny, nz, en[0], en[1], en[2], p.box_side, tid, kCollBlock, mm);
+        coll_wg_min7(mm, red);
+        if (tid == en[3])
+          for (int q = 0; q < 7; ++q) m[q] = mm[q];
+      }
     }
-    if (tid == 0 && wk.take<N>(smp, valid, m, p, grad, g_s)) smp[9] = -1.0;  // collision: stop
+    if (w0) {
+      const bool e = (ev >> lane) & 1ull;
+      bool valid = false, coll = false;
+      double c = 0.0;
+      if (e) {
+        valid = coll_valid_state(pos, p);
+        // Voxel of the sample: (position / res).cast<int>() truncates toward zero.
+        const int vx = static_cast<int>(pos[0] / res), vy = static_cast<int>(pos[1] / res),
+                  vz = static_cast<int>(pos[2] / res);
+        if (field && valid && !coll_field_lookup(field, nx, ny, nz, vx, vy, vz, m))
+          coll_box_scan(occ, nx, ny, nz, vx, vy, vz, p.box_side, 0, 1, m);
+        // invalid states keep distance 0 (:1832-1839), i.e. collide
+        c = coll_potential(valid ? dist(m[0]) : 0.0, p, &coll);
+      }
+      const unsigned long long cm = __ballot(e && coll);
+      const unsigned long long live = cm ? ev & ((cm & (0ull - cm)) - 1ull) : ev;
+      const double vn = sqrt(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
+      const double cv = c * vn;
+      for (unsigned long long mm = live; mm; mm &= mm - 1ull) {
+        const int j = __builtin_ctzll(mm);
+        J += coll_readlane(cv, j) * coll_readlane(ts_me, j);
+      }
+      if (grad) {  // :1729-1750 (vn <= 1e-6 drops the gradient term)
+        const bool gl = ((live >> lane) & 1ull) && vn > 1e-6;
+        const unsigned long long gm = __ballot(gl);
+        if (gm) {
+          coll_wave_sync();  // the previous chunk's rows are read
+          if (gl) {
+            double* row = rows + lane * RW;
+            double tn = 1.0;
+            for (int n = 0; n < N; ++n) {
+              row[n] = tn;
+              tn *= tj;
+            }
+            for (int k = 0; k < D; ++k) {
+              bool cl, cr;
+              const double left = coll_potential(dist(m[1 + 2 * k]), p, &cl);
+              const double right = coll_potential(dist(m[2 + 2 * k]), p, &cr);
+              const double gp = (right - left) / (2.0 * res);
+              row[N + k] = vn * ts_me * gp;
+              row[N + 3 + k] = ts_me * c * vel[k] / vn;
+            }
+          }
+          coll_wave_sync();
+          if (lane < D * N) {  // eq. (14), lane (k, n), sample after sample
+            const int k = lane / N, n = lane - k * N;
+            double* gp = g_s + (seg * D + k) * N + n;
+            double g = *gp;
+            for (unsigned long long mm = gm; mm; mm &= mm - 1ull) {
+              const double* row = rows + __builtin_ctzll(mm) * RW;
+              const double a = row[N + k], bcoef = row[N + 3 + k];
+              const double tn = row[n], tn1 = n > 0 ? n * row[n - 1] : 0.0;
+              g += a * tn + bcoef * tn1;
+            }
+            *gp = g;
+          }
+        }
+      }
+      if (cm) {
+        hit = true;
+      } else {
+        for (int d = 0; d < D; ++d) prev[d] = coll_readlane(pos[d], n_in - 1);
+        // A segment ends at its first t >= T (a full chunk continues; one
+        // whose times stopped growing is ended rather than walked forever).
+        if (n_in < kWave || !(t_end > t0)) {
+          time_sum += -dt + (T - t_end);
+          ++seg;
+          t0 = 0.0;
+        } else {
+          t0 = t_end;
+        }
+      }
+    }
     __syncthreads();
-    if (smp[9] < 0.0) break;
+  }
+  if (tid == 0) {
+    ctl[2] = hit ? 0.0 : J;
+    ctl[3] = hit ? 1.0 : 0.0;
   }
   __syncthreads();
-  const bool hit = smp[9] < 0.0;
-  if (tid == 0) smp[6] = hit ? 0.0 : wk.J;
-  __syncthreads();
-  *J_out = smp[6];
-  *hit_out = hit;
+  *J_out = ctl[2];
+  *hit_out = ctl[3] != 0.0;
   __syncthreads();
 }
 

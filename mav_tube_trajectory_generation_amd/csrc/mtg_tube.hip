@@ -14,7 +14,8 @@ __device__ inline Tube<N> make_tube(const TubeLayout* L, double* smem, int S, in
                                     const double* tab) {
   const int tid = static_cast<int>(threadIdx.x);
   return Tube<N>{S,   r,         S - 1, tube_ncon(N, S), L, smem, tid & (kWave - 1), tab,
-                 tid, static_cast<int>(blockDim.x), tid / kWave};
+                 tid, static_cast<int>(blockDim.x),
+                 __builtin_amdgcn_readfirstlane(tid / kWave)};
 }
 
 // Constraint residuals g_k(x) (compute_sphere/tube/tube_end_constraints,

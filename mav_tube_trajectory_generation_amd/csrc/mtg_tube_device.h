@@ -49,6 +49,9 @@ struct TubeLayout {
   int s, lam, ds, dl;     // ncon each
   int Li;                 // nv*BS(BS+1)/2 L_a^-1 packed by rows, diagonal = 1/pivot
   int W;                  // BS*BS  W_a of the current block, row-major
+  int Wb;                 // BS*BS  V_a of the backward sweep's current block: ds/dl
+                          // (dead during the factorisation) when they are large
+                          // enough, else its own slot
   int Gc;                 // S*N*6  per control point: sum lam Hess + lam/s w w^T (sym)
   int red;                // 4: cross-wave reductions
   int ndouble;
@@ -88,6 +91,12 @@ __host__ __device__ inline TubeLayout make_tube_layout(int N, int S) {
   l.W = o;    o += BS * BS;
   l.Gc = o;   o += S * N * 6;
   l.red = o;  o += 4;
+  if (2 * nc >= BS * BS) {
+    l.Wb = l.ds;  // ds, dl adjacent
+  } else {
+    l.Wb = o;
+    o += BS * BS;
+  }
   l.ndouble = o;
   return l;
 }
@@ -510,16 +519,25 @@ struct Tube {
   }
 
   // --------------------------------------------------------- factorisation
-  // Block LDL^T of the block-tridiagonal KKT matrix.  For vertex block a:
-  //   S_a = K_a - W_{a-1}^T D_{a-1}^-1 W_{a-1} = L_a D_a L_a^T,
-  //   W_a = L_a^-1 C_a,   C_a = I_3 (x) Po_a (coupling to block a+1).
+  // Twisted block LDL^T of the block-tridiagonal KKT matrix.  With two waves,
+  // wave 0 eliminates blocks 0 .. m-1 forward while wave 1 eliminates
+  // nv-1 .. m+1 backward, then wave 0 the middle block m = nv / 2 with both
+  // Schur terms (one wave: m = nv - 1, a plain forward sweep):
+  //   forward   S_a = K_a - W_{a-1}^T D_{a-1}^-1 W_{a-1},  W_a = L_a^-1 C_a,
+  //   backward  S_a = K_a - V_{a+1}^T D_{a+1}^-1 V_{a+1},  V_a = L_a^-1 C_{a-1}^T,
+  //   middle    S_m = K_m - W_{m-1}^T D^-1 W_{m-1} - V_{m+1}^T D^-1 V_{m+1},
+  // C_a = I_3 (x) Po_a coupling block a to a+1, S_a = L_a D_a L_a^T.
   // The constraint and Schur terms of S_a are accumulated with the rows
   // sharing the sums (control points q = g + 4k, W rows t = g + 4k), then
-  // the elimination runs on [S_a | I | C_a] held column-per-lane in
-  // registers; the pivot column is broadcast with v_readlane, so it needs no
-  // LDS traffic and no barrier inside.  Afterwards the identity lanes hold
-  // L_a^-1 (unit lower) and the C_a lanes W_a; the pivots are D_a.  S_a is
-  // SPD (no pivoting); a non-positive pivot sets *fail.
+  // the elimination runs on [S_a | I | C] held column-per-lane in registers;
+  // the pivot column is broadcast with v_readlane, so it needs no LDS traffic
+  // and no barrier inside.  Afterwards the identity lanes hold L_a^-1 (unit
+  // lower) and the coupling lanes W_a / V_a; the pivots are D_a.  S_a is SPD
+  // (no pivoting); a non-positive pivot sets *fail.  W is kept for the block
+  // being eliminated only, V likewise in Wb (normally the ds / dl buffers,
+  // dead from the step update to the next direction).
+  __device__ int mid() const { return nthr > kWave ? nv / 2 : nv - 1; }
+
   __device__ void factor(int* fail, bool with_constraints) {
     const double* Gcp = sm + L->Gc;
     int bad = 0;
@@ -531,7 +549,16 @@ struct Tube {
     // Per-lane target of the unused stores (rhs is dead during factor():
     // written by direction() / the start system afterwards).
     const int dummy = L->rhs + lane;
-    for (int a = 0; a < nv; ++a) {
+    const int m = mid(), nb = nv - 1 - m;
+    const bool bw = wv == 1;  // wave-uniform
+    for (int st = 0; st <= m; ++st) {
+      // This wave's block: wave 0 a = st (the middle at st = m), wave 1
+      // a = nv - 1 - st while st < nb.
+      const bool act = bw ? st < nb : true;
+      const int a = bw ? nv - 1 - st : st;
+      const bool midb = !bw && st == m;
+      const bool sf = !bw && a > 0;                         // W_{a-1} term
+      const bool sb = bw ? st > 0 : (midb && m < nv - 1);   // V_{a+1} term
       const int u = a + 1;  // vertex
       double col[BS], acc[BS];
       // Opaque per iteration: keeps the compiler from hoisting the 0/1
@@ -539,22 +566,25 @@ struct Tube {
       int cc = cc0;
       asm volatile("" : "+v"(cc));
       const int d2 = cc / M, m2 = cc % M;
-      const int role = (role0 == 2 && a == nv - 1) ? 3 : role0;
+      const int role = (role0 == 2 && midb) ? 3 : role0;
       // Roles enter as exact 0/1 factors (VGPR values: no lane masks kept
       // live); loads are unconditional with clamped indices.
       const double r0 = is_zero(role), r1 = is_zero(role - 1), r2 = is_zero(role - 2);
       double dpiv = 1.0;
-      if (wv == 0) {  // ---- wave 0: assemble and eliminate block a
+      if (act) {  // ---- assemble and eliminate block a
       {
-        const double* Po = sm + L->Po + (a < nv - 1 ? a : 0) * M * M;
+        // Coupling columns: C_a = I_3 (x) Po_a (forward), C_{a-1}^T (backward).
+        const int pb = bw ? (a > 0 ? a - 1 : 0) : (a < nv - 1 ? a : 0);
+        const double* Po = sm + L->Po + pb * M * M;
+        const int pt = bw ? 1 : M, ps = bw ? M : 1;
         double ind[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) ind[d] = is_zero(d - d2);
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const double v = pd(a, m, m2) * r0 + Po[m * M + m2] * r2;
+        for (int mm = 0; mm < M; ++mm) {
+          const double v = pd(a, mm, m2) * r0 + Po[mm * pt + m2 * ps] * r2;
 #pragma unroll
-          for (int d = 0; d < 3; ++d) col[d * M + m] = v * ind[d];
+          for (int d = 0; d < 3; ++d) col[d * M + mm] = v * ind[d];
         }
 #pragma unroll
         for (int i = 0; i < BS; ++i) col[i] += r1 * is_zero(i - cc);
@@ -578,24 +608,22 @@ struct Tube {
           const int cpi = seg * N + (lo ? q + M : q - M);
           double bt[M];
 #pragma unroll
-          for (int m = 0; m < M; ++m) bt[m] = (m & 1) ? sg * bro[m] : bro[m];
+          for (int mm = 0; mm < M; ++mm) bt[mm] = (mm & 1) ? sg * bro[mm] : bro[mm];
           const double bm = ((m2 & 1) ? sg * bro[m2] : bro[m2]) * wq;
 #pragma unroll
           for (int d = 0; d < 3; ++d) {
             const double gd = Gcp[cpi * 6 + gsym(d, d2)] * bm;
 #pragma unroll
-            for (int m = 0; m < M; ++m) acc[d * M + m] = fma(gd, bt[m], acc[d * M + m]);
+            for (int mm = 0; mm < M; ++mm) acc[d * M + mm] = fma(gd, bt[mm], acc[d * M + mm]);
           }
         }
       }
       MTG_TACC(221, tf);
-      if (a > 0) {
-        // acc -= sum_t W[t][:] dinv[t] W[t][c]  over this row's t (W = W_{a-1},
-        // dinv on the diagonal of the packed L_{a-1}^-1).
-        // Row t + kNG is loaded while row t is applied (sched barriers keep
-        // the loads ahead: otherwise they are issued one pair at a time).
-        const double* Wp = sm + L->W;
-        const double* Lp = sm + L->Li + (a - 1) * kTri;
+      // acc -= sum_t X[t][:] dinv[t] X[t][c] over this row's t, X = W_{a-1}
+      // or V_{a+1} with dinv on the diagonal of the neighbour's packed L^-1.
+      // Row t + kNG is loaded while row t is applied (sched barriers keep
+      // the loads ahead: otherwise they are issued one pair at a time).
+      auto schur = [&](const double* Wp, const double* Lp) {
         constexpr int KT = (BS + kNG - 1) / kNG;
         double wr[BS], wn[BS], wc, dt, wcn = 0.0, dtn = 0.0;
         auto row = [&](int k, double* w, double* c, double* d) {
@@ -620,7 +648,9 @@ struct Tube {
           wc = wcn;
           dt = dtn;
         }
-      }
+      };
+      if (sf) schur(sm + L->W, sm + L->Li + (a - 1) * kTri);
+      if (sb) schur(sm + L->Wb, sm + L->Li + (a + 1) * kTri);
 #pragma unroll
       for (int i = 0; i < BS; ++i) col[i] = fma(rows_sum(acc[i]), r0, col[i]);
       // Forward elimination (below the pivot) on all columns at once; the
@@ -642,21 +672,22 @@ struct Tube {
       }
       bad |= __ballot(lane < BS && !(dpiv > 0.0)) != 0;
       MTG_TACC(223, tf);
-      }  // ---- wave 0
+      }  // ---- act
       // S_a lanes store 1 / pivot on the diagonal of the packed L_a^-1, the
-      // identity lanes its strictly lower columns, the C_a lanes W_a
-      // (replacing W_{a-1}, which every lane has read by the barrier).
-      // Offsets are selected per lane with integer masks (no branches),
-      // unused stores go to a per-lane dummy slot.
+      // identity lanes its strictly lower columns, the coupling lanes W_a or
+      // V_a (replacing the previous block's, which every lane of the wave has
+      // read by the barrier).  Offsets are selected per lane with integer
+      // masks (no branches), unused stores go to a per-lane dummy slot.
       __syncthreads();
-      if (wv == 0) {
+      if (act) {
         const int li = L->Li + a * kTri;
+        const int wo = bw ? L->Wb : L->W;
         const int s0 = -izero(role), s1 = -izero(role - 1), s2 = -izero(role - 2);
         sm[((li + tri(cc, cc)) & s0) | (dummy & ~s0)] = rcp64(dpiv > 0.0 ? dpiv : 1.0);
 #pragma unroll
         for (int i = 0; i < BS; ++i) {
           const int a1 = s1 & ((cc - i) >> 31);  // identity lane, i > cc
-          const int o = ((li + tri(i, cc)) & a1) | ((L->W + i * BS + cc) & s2) |
+          const int o = ((li + tri(i, cc)) & a1) | ((wo + i * BS + cc) & s2) |
                         (dummy & ~(a1 | s2));
           sm[o] = col[i];
         }
@@ -664,18 +695,20 @@ struct Tube {
       __syncthreads();
       MTG_TACC(224, tf);
     }
-    if (bad && tid == 0) *fail = 1;
+    if (bad && lane == 0) *fail = 1;
   }
 
-  // Solve K out = rhs with the block factors (rhs overwritten by y).
+  // Solve K out = rhs with the twisted factors (rhs overwritten by y).
   // Row i of a block belongs to lanes (g, i) of every row g, which share its
   // dot products; the vectors of the recurrence stay in registers (lane k
-  // holds entry k) and move between lanes with __shfl, so the only barriers
-  // are between the two sweeps and at the end.  W_a = L_a^-1 C_a is not
+  // holds entry k) and move between lanes with __shfl.  W and V are not
   // stored; the coupling is applied as C_a = I_3 (x) Po_a next to the
-  // packed L^-1:
-  //   forward   y_a = L_a^-1 (b_a - C_{a-1}^T L_{a-1}^-T D_{a-1}^-1 y_{a-1})
-  //   backward  x_a = L_a^-T D_a^-1 (y_a - L_a^-1 C_a x_{a+1}).
+  // packed L^-1.  Outer blocks (wave 0 forward from block 0, wave 1 backward
+  // from block nv-1), with p the previous block of the wave:
+  //   y_a = L_a^-1 (b_a - X_a L_p^-T D_p^-1 y_p),  X_a = C_{a-1}^T / C_a,
+  // the middle block with both neighbours' terms and x_m = L_m^-T D_m^-1 y_m,
+  // then outward from the middle, with n the block towards it:
+  //   x_a = L_a^-T D_a^-1 (y_a - L_a^-1 Y_a x_n),    Y_a = C_a / C_{a-1}^T.
   // Triangular sums run over the full row with the out-of-triangle terms
   // weighted by exact 0 (the unit diagonal by exact 1).
   __device__ void solve(int rhs_off, int out_off) {
@@ -702,21 +735,29 @@ struct Tube {
       const int kx = k > i ? k : i;
       return fma(Lb[tri(kx, i)], static_cast<double>(k > i && k0 < BS), is_zero(k0 - i));
     };
-    double u = 0.0;  // D_{a-1}^-1 y_{a-1}, entry i
-    for (int a = 0; a < (wv == 0 ? nv : 0); ++a) {  // wave 0 only
+    // (X L_p^-T uu)_i with uu = D_p^-1 y_p (lane k holds entry k), X given
+    // by its Po block: X[(d, mi), (d, mm)] = Po[mm * pt + mi * ps].
+    auto term = [&](double uu, const double* Lp, const double* Po, int pt, int ps) {
+      double v = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) v = fma(lcol(Lp, kk), __shfl(uu, kidx(kk)), v);
+      v = rows_sum(v);
+      double s = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < M; ++mm) s = fma(Po[mm * pt + mi * ps], __shfl(v, di * M + mm), s);
+      return s;
+    };
+    const int m = mid(), nb = nv - 1 - m;
+    const bool bw = wv == 1;  // wave-uniform
+    const int nf = bw ? nb : m;  // this wave's outer blocks
+    double u = 0.0;              // D_p^-1 y_p, entry i
+    for (int k = 0; k < nf; ++k) {
+      const int a = bw ? nv - 1 - k : k;
       const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
-      if (a > 0) {
-        // v = L_{a-1}^-T u (row i), then t -= (C^T v)_i.
-        const double* Lp = Li - kTri;
-        double v = 0.0;
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) v = fma(lcol(Lp, kk), __shfl(u, kidx(kk)), v);
-        v = rows_sum(v);
-        const double* Po = sm + L->Po + (a - 1) * M * M;
-#pragma unroll
-        for (int m = 0; m < M; ++m) t = fma(-Po[m * M + mi], __shfl(v, di * M + m), t);
-      }
+      if (k > 0)  // forward: C_{a-1}^T (Po_{a-1} transposed); backward: C_a
+        t -= bw ? term(u, Li + kTri, sm + L->Po + a * M * M, 1, M)
+                : term(u, Li - kTri, sm + L->Po + (a - 1) * M * M, M, 1);
       double z = 0.0;
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) z = fma(lrow(Li, kk), __shfl(t, kidx(kk)), z);
@@ -725,21 +766,43 @@ struct Tube {
       if (wr) y[a * BS + i] = z;
     }
     __syncthreads();
-    double xn = 0.0;  // x_{a+1}, entry i
-    for (int a = (wv == 0 ? nv - 1 : -1); a >= 0; --a) {  // wave 0 only
+    double xn = 0.0;  // x of the block towards the middle, entry i
+    if (!bw) {        // the middle block
+      const double* Li = sm + L->Li + m * kTri;
+      double t = y[m * BS + i];
+      if (m > 0) t -= term(u, Li - kTri, sm + L->Po + (m - 1) * M * M, M, 1);
+      if (m < nv - 1) {
+        const double ub = y[(m + 1) * BS + i] * Li[kTri + tri(i, i)];
+        t -= term(ub, Li + kTri, sm + L->Po + m * M * M, 1, M);
+      }
+      double z = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) z = fma(lrow(Li, kk), __shfl(t, kidx(kk)), z);
+      z = rows_sum(z) * Li[tri(i, i)];
+      double x = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) x = fma(lcol(Li, kk), __shfl(z, kidx(kk)), x);
+      x = rows_sum(x);
+      xn = x;
+      if (wr) xo[m * BS + i] = x;
+    }
+    __syncthreads();
+    if (bw) xn = xo[m * BS + i];
+    for (int k = nf - 1; k >= 0; --k) {
+      const int a = bw ? nv - 1 - k : k;
       const double* Li = sm + L->Li + a * kTri;
       double t = y[a * BS + i];
-      if (a < nv - 1) {
-        // c = C_a x_{a+1} (row i); t -= (L_a^-1 c)_i.
-        const double* Po = sm + L->Po + a * M * M;
-        double c = 0.0;
+      // c = C_a x_{a+1} (forward blocks) or C_{a-1}^T x_{a-1} (backward);
+      // t -= (L_a^-1 c)_i.
+      const double* Po = sm + L->Po + (bw ? a - 1 : a) * M * M;
+      const int pt = bw ? M : 1, ps = bw ? 1 : M;
+      double c = 0.0;
 #pragma unroll
-        for (int m = 0; m < M; ++m) c = fma(Po[mi * M + m], __shfl(xn, di * M + m), c);
-        double s = 0.0;
+      for (int mm = 0; mm < M; ++mm) c = fma(Po[mm * pt + mi * ps], __shfl(xn, di * M + mm), c);
+      double s = 0.0;
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) s = fma(lrow(Li, kk), __shfl(c, kidx(kk)), s);
-        t -= rows_sum(s);
-      }
+      for (int kk = 0; kk < KS; ++kk) s = fma(lrow(Li, kk), __shfl(c, kidx(kk)), s);
+      t -= rows_sum(s);
       t *= Li[tri(i, i)];
       double x = 0.0;
 #pragma unroll
