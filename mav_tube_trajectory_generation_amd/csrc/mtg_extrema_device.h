@@ -9,6 +9,9 @@
 #include <cmath>
 
 #include "mtg_internal.h"
+#ifdef MTG_STAMPS
+#include "mtg_device.h"  // g_mtg_stamps
+#endif
 
 namespace mtg {
 
@@ -73,7 +76,8 @@ template <int N, int K, bool kMin = false, bool kEmit = false>
 __device__ __attribute__((always_inline)) inline void ext_segment_search(const double* c, int D, double T, int part, int parts,
                                           int log2parts, double& best_v, double& best_t,
                                           double& min_v, double& min_t, double lb = 0.0,
-                                          ExtEmit* em = nullptr) {
+                                          ExtEmit* em = nullptr, int* nodes = nullptr,
+                                          int* iters = nullptr) {
   static_assert(!kEmit || kMin, "the candidate list needs the exhaustive (kMin) search");
   auto emit = [&](double v, double t) {
     if constexpr (kEmit) {
@@ -190,6 +194,7 @@ __device__ __attribute__((always_inline)) inline void ext_segment_search(const d
     const int max_level = kExtMaxLevel - log2parts;
     int level = 0, idx = 0;
     for (;;) {
+      if (nodes) ++*nodes;
       const double w = ldexp(1.0, -level);
       const double a = idx * w;
       const double e = a + w;
@@ -260,6 +265,7 @@ __device__ __attribute__((always_inline)) inline void ext_segment_search(const d
         double lo = a, hi = e, x = 0.5 * (a + e);
         const bool pos_lo = first > 0.0;
         for (int it = 0; it < kExtRefineIters; ++it) {
+          if (iters) ++*iters;
           double fx = q[M], d1 = 0.0, d2 = 0.0, ab = fabs(q[M]);
 #pragma unroll
           for (int j = M - 1; j >= 0; --j) {
@@ -326,13 +332,29 @@ __device__ __attribute__((always_inline)) inline double ext_trajectory_max_wave(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) lb = fmax(lb, __shfl_xor(lb, off, 64));
   double best = 0.0;
+#ifdef MTG_STAMPS
+  // Diagnostic build: per-lane node and Laguerre-iteration counts of
+  // workgroup 0 (stamp slots 320 + lane, 384 + lane).
+  int n_nodes = 0, n_iters = 0;
+  int* pn = &n_nodes;
+  int* pi = &n_iters;
+#else
+  int* pn = nullptr;
+  int* pi = nullptr;
+#endif
   for (int item = lane; item < S * parts; item += 64) {
     const int s = item >> log2parts, part = item & (parts - 1);
     double v = -1.0, t = 0.0, mv = 0.0, mt = 0.0;
     ext_segment_search<N, K>(coeffs + s * D * N, D, times[s], part, parts, log2parts, v, t, mv,
-                             mt, lb);
+                             mt, lb, nullptr, pn, pi);
     best = fmax(best, v);
   }
+#ifdef MTG_STAMPS
+  if (blockIdx.x == 0) {
+    atomicAdd(&g_mtg_stamps[320 + lane], static_cast<unsigned long long>(n_nodes));
+    atomicAdd(&g_mtg_stamps[384 + lane], static_cast<unsigned long long>(n_iters));
+  }
+#endif
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) best = fmax(best, __shfl_xor(best, off, 64));
   return sqrt(best);

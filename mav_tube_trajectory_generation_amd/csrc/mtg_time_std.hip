@@ -33,6 +33,8 @@ __device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& s
                                 const double* T, const mtg_time_params& p, double* cbuf,
                                 bool* bad, bool* not_spd, double* viol) {
   *viol = 0.0;
+  unsigned long long tt = 0;
+  MTG_TACC(511, tt);
   __syncthreads();
   const bool b = sv.powers_from(T);
   __syncthreads();
@@ -50,6 +52,7 @@ __device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& s
   double tot = 0.0;
   for (int i = 0; i < sv.S; ++i) tot += T[i];  // nonlinear_impl:2768-2774
   J += tot * tot * p.time_penalty;
+  MTG_TACC(450, tt);  // diagnostic: solve + coefficients
   if constexpr (kSoft) {
     __syncthreads();
     double soft = 0.0;
@@ -69,6 +72,7 @@ __device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& s
         const double relative_violation = (m - lim) / lim;
         soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
       }
+      MTG_TACC(451 + c, tt);  // diagnostic: search c
     }
     J += soft;
   }
@@ -191,6 +195,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
   double f = 0.0, fv = 0.0, Jlo = 0.0, vlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   bool bad = false, not_spd = false;
+  MTG_STAMP(460);
   while (phase != kDone) {
     double viol;
     const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd, &viol);
@@ -253,6 +258,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
     }
   }
   __syncthreads();
+  MTG_STAMP(461);
   for (int i = lane; i < S; i += kWave) times_io[b * S + i] = Tcur[i];
   if (lane == 0) {
     if (cost) cost[b] = bad ? NAN : f;
@@ -351,3 +357,11 @@ hipError_t launch_time_optimize_std(const PlanDev& pl, int64_t B, const double* 
 }
 
 }  // namespace mtg
+
+#ifdef MTG_STAMPS
+// This translation unit's stamps (the soft searches' per-lane counters).
+extern "C" int mtg_debug_stamps_time(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mtg_stamps),
+                             sizeof(unsigned long long) * n) == hipSuccess ? 0 : -3;
+}
+#endif
