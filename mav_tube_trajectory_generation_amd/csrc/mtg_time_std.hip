@@ -55,24 +55,31 @@ __device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& s
   MTG_TACC(450, tt);  // diagnostic: solve + coefficients
   if constexpr (kSoft) {
     __syncthreads();
+    // Every constraint's maximum in one pass (ext_soft_maxima_wave).
+    int Ks[kMaxSoftConstraints];
+    int kmin = 4;
+#pragma unroll
+    for (int cc = 0; cc < kMaxSoftConstraints; ++cc) {
+      Ks[cc] = p.soft_derivative[cc];
+      if (cc < p.n_soft && Ks[cc] < kmin) kmin = Ks[cc];
+    }
+    double* scratch = cbuf + sv.S * D * N;
+    double* maxima = scratch + kMaxSoftConstraints * (N + 1);
+    ext_soft_maxima_wave_k<N>(kmin, cbuf, T, sv.S, D, sv.lane, p.n_soft, Ks, scratch, maxima);
     double soft = 0.0;
     for (int c = 0; c < p.n_soft; ++c) {
-      int K = 0;
       double lim = 1.0;
 #pragma unroll
       for (int cc = 0; cc < kMaxSoftConstraints; ++cc)  // compile-time indices
-        if (cc == c) {
-          K = p.soft_derivative[cc];
-          lim = p.soft_limit[cc];
-        }
-      const double m = ext_trajectory_max_wave_k<N>(K, cbuf, T, sv.S, D, sv.lane);
+        if (cc == c) lim = p.soft_limit[cc];
+      const double m = maxima[c];
       if (p.hard_constraints) {
         *viol = fmax(*viol, m - lim - p.hard_tolerance);
       } else {
         const double relative_violation = (m - lim) / lim;
         soft += fmin(p.soft_maximum_cost, exp(relative_violation * p.soft_weight));
       }
-      MTG_TACC(451 + c, tt);  // diagnostic: search c
+      MTG_TACC(451 + c, tt);  // diagnostic
     }
     J += soft;
   }
@@ -102,7 +109,11 @@ __device__ inline void std_set_fd_point(double* T, const double* Tb, int S, int 
 
 size_t time_std_lds_bytes(int N, int S, int D, bool soft) {
   const size_t base = sizeof(double) * static_cast<size_t>(stdp::layout(N, S, D).n);
-  return soft ? (base + 15) / 16 * 16 + sizeof(double) * S * D * N : base;
+  // soft: the coefficients (S x D x N), then the soft searches' scratch and
+  // maxima (ext_soft_maxima_wave).
+  return soft ? (base + 15) / 16 * 16 +
+                    sizeof(double) * (S * D * N + kMaxSoftConstraints * (N + 2))
+              : base;
 }
 
 template <int N, int R, int D, bool kSoft>

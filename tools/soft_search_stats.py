@@ -42,18 +42,24 @@ def main():
         after = read()
         nodes = (after - before)[320:384]
         iters = (after - before)[384:448]
-        act = nodes[:40]
+        act = nodes[:60]
         tot_nodes += nodes
         print(f"traj {b}: solves {int(out['solves'][0])}  nodes/lane mean {act.mean():.0f} "
               f"max {act.max()} (lane {act.argmax()})  min {act.min()}  "
-              f"laguerre/lane mean {iters[:40].mean():.0f} max {iters[:40].max()}")
+              f"laguerre/lane mean {iters[:60].mean():.0f} max {iters[:60].max()}")
         d = after - before
         tot = after[461] - after[460]
         print(f"   cycles: kernel loop {tot}  solve+coeffs {d[450]}  search K=1 {d[451]}  "
               f"search K=2 {d[452]}  per solve: {d[450] / int(out['solves'][0]):.0f} / "
               f"{d[451] / int(out['solves'][0]):.0f} / {d[452] / int(out['solves'][0]):.0f}")
+        ns = 2 * int(out['solves'][0])
+        print(f"   search phases per call (lane 0): bound {d[470] / ns:.0f}  setup "
+              f"{d[471] / ns:.0f}  tree walk {d[472] / ns:.0f}  reductions {d[473] / ns:.0f}")
+        print(f"   node {d[474] / (ns / 2):.0f}  lane-0 refine {d[475] / (ns / 2):.0f}  "
+              f"refine+value {d[476] / (ns / 2):.0f} (per evaluation)")
         print("   nodes per lane:", " ".join(str(x) for x in act))
-        print("   iters per lane:", " ".join(str(x) for x in iters[:40]))
+        print("   iters per lane:", " ".join(str(x) for x in iters[:60]))
+        print("   max iters in one call per lane:", " ".join(str(x) for x in after[256:316]))
 
 
 if __name__ == "__main__":
