@@ -100,6 +100,50 @@ __device__ inline void ldlt_solve(const double (&S)[MF][MF], const double (&r)[M
   }
 }
 
+// x = S^-1 r for a symmetric 4 x 4 block by 2 x 2 blocks, S = [P Q; Q^T W]:
+// P^-1 and (W - Q^T P^-1 Q)^-1 from their adjugates and one reciprocal of
+// each determinant.  The dependent chain is two reciprocals deep (18 FP64
+// operations) instead of LDL^T's four (about 28), which is what a sweep step
+// waits on at one wave per SIMD.  pmin as ldlt_solve: the leading minors
+// p00, det P, w00, det W' are all positive exactly when S is.
+__device__ inline void block2_solve(const double (&S)[4][4], const double (&r)[4],
+                                    double (&x)[4], double& pmin) {
+  const double p00 = S[0][0], p10 = S[1][0], p11 = S[1][1];
+  const double detP = fma(p00, p11, -(p10 * p10));
+  const double ip = rcp64_1(detP);
+  const double Pi00 = p11 * ip, Pi11 = p00 * ip, Pi10 = -p10 * ip;
+  // Qt[a][b] = S[2+a][b] (= Q^T); Y = P^-1 Q, column a = P^-1 Qt[a][:]^T.
+  const double Y00 = fma(Pi10, S[2][1], Pi00 * S[2][0]);
+  const double Y10 = fma(Pi11, S[2][1], Pi10 * S[2][0]);
+  const double Y01 = fma(Pi10, S[3][1], Pi00 * S[3][0]);
+  const double Y11 = fma(Pi11, S[3][1], Pi10 * S[3][0]);
+  // W' = W - Q^T Y (symmetric).
+  const double w00 = fma(-S[2][1], Y10, fma(-S[2][0], Y00, S[2][2]));
+  const double w10 = fma(-S[3][1], Y10, fma(-S[3][0], Y00, S[3][2]));
+  const double w11 = fma(-S[3][1], Y11, fma(-S[3][0], Y01, S[3][3]));
+  const double detW = fma(w00, w11, -(w10 * w10));
+  const double iw = rcp64_1(detW);
+  // y1 = P^-1 r_1, r2' = r_2 - Q^T y1, x_2 = W'^-1 r2', x_1 = y1 - Y x_2.
+  const double y0 = fma(Pi10, r[1], Pi00 * r[0]);
+  const double y1 = fma(Pi11, r[1], Pi10 * r[0]);
+  const double s0 = fma(-S[2][1], y1, fma(-S[2][0], y0, r[2]));
+  const double s1 = fma(-S[3][1], y1, fma(-S[3][0], y0, r[3]));
+  x[2] = fma(-w10, s1, w11 * s0) * iw;
+  x[3] = fma(-w10, s0, w00 * s1) * iw;
+  x[0] = fma(-Y01, x[3], fma(-Y00, x[2], y0));
+  x[1] = fma(-Y11, x[3], fma(-Y10, x[2], y1));
+  pmin = fmin(pmin, fmin(fmin(p00, detP), fmin(w00, detW)));
+}
+
+template <int MF>
+__device__ inline void block_solve(const double (&S)[MF][MF], const double (&r)[MF],
+                                   double (&x)[MF], double& pmin) {
+  if constexpr (MF == 4)
+    block2_solve(S, r, x, pmin);
+  else
+    ldlt_solve<MF>(S, r, x, pmin);
+}
+
 // K doubles from / to LDS, 16-byte accesses for the pairs (callers keep the
 // addresses of rows 16-byte aligned).
 template <int K>
@@ -255,8 +299,7 @@ struct Solver {
   }
 
   __device__ void load_first_rows(const double* __restrict__ tab) {
-    const int nrows = (S - 1) * MF;
-    load_rows(tab, (lane < nrows ? lane : 0) % MF + 1);
+    load_rows(tab, lane % MF + 1);
   }
 
   __device__ void load_rows(const double* __restrict__ tab, int k) {
@@ -346,32 +389,39 @@ struct Solver {
       Ar[j] = fma(hMk[M + j + 1], ql[j + 1], hk[j + 1] * qr[j + 1]);
       Cr[j] = hk[M + j + 1] * qr[j + 1];
     }
-    const double fl = v == 1 ? 1.0 : 0.0, fr = v == S - 1 ? 1.0 : 0.0;
     const double cpos = fma(hMk[M], ql[0], hk[0] * qr[0]);  // p_v
     const double cprev = hMk[0] * ql[0];                     // p_{v-1}
     const double cnext = hk[M] * qr[0];                      // p_{v+1}
-    double el[MF], er[MF];  // fully fixed neighbours (vertex 0 / S)
-#pragma unroll
-    for (int l = 1; l < M; ++l) {
-      el[l - 1] = fl * (hMk[l] * ql[l]);
-      er[l - 1] = fr * (hk[M + l] * qr[l]);
-    }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       double s = cpos * dvp[(v * D + d) * MP];
       s = fma(cprev, dvp[((v - 1) * D + d) * MP], s);
       s = fma(cnext, dvp[((v + 1) * D + d) * MP], s);
-#pragma unroll
-      for (int l = 1; l < M; ++l) {
-        s = fma(el[l - 1], dvp[d * MP + l], s);
-        s = fma(er[l - 1], dvp[(S * D + d) * MP + l], s);
-      }
       sm[L.bz + (v * D + d) * RS + i] = -s;
     }
     lds_store(sm + L.Sb + v * BS + i * RS, Ar);
     lds_store(sm + L.Cs + v * BS + i * RS, Cr);
 #pragma unroll
     for (int j = 0; j < MF; ++j) sm[L.Ct + v * BS + j * RS + i] = Cr[j];
+  }
+
+  // The fully fixed end vertices' part of b_1 (vertex 0, segment 0) and of
+  // b_(S-1) (vertex S, segment S-1): lane (e, d, i) adds
+  // -sum_l H_seg(k, l) d_f(l) for its row after the row lanes stored theirs,
+  // so these 2 D MF products run once instead of in every row lane.  Needs
+  // the lane's H(1) rows at k = lane % MF + 1.
+  __device__ void assemble_ends() {
+    if (lane < 2 * D * MF) {
+      const int i = lane % MF, k = i + 1, ed = lane / MF;
+      const bool right = ed >= D;
+      const int d = right ? ed - D : ed;
+      const double* pp = pw() + (right ? S - 1 : 0) * PWP + N + 1 - 2 * R + k;
+      const double* dd = dv() + ((right ? S : 0) * D + d) * MP;
+      double s = 0.0;
+#pragma unroll
+      for (int l = 1; l < M; ++l) s = fma((right ? hk[M + l] : hMk[l]) * pp[l], dd[l], s);
+      atomicAdd(sm + L.bz + ((right ? S - 1 : 1) * D + d) * RS + i, -s);
+    }
   }
 
   // All rows; rows beyond the first pass (S > 17) reload their H(1) rows.
@@ -383,7 +433,9 @@ struct Solver {
       load_rows(tab, row % MF + 1);
       assemble_row(row);
     }
-    if (nrows > kWave) load_rows(tab, (lane < nrows ? lane : 0) % MF + 1);
+    if (nrows > kWave) load_rows(tab, lane % MF + 1);
+    asm volatile("" ::: "memory");  // the rows' b stores precede the end terms
+    assemble_ends();
   }
 
   // Twisted block LDL^T, middle vertex and back substitution: on return (after
@@ -442,7 +494,7 @@ struct Solver {
             for (int j = 0; j <= i; ++j) Sv[i][j] = row[j];
           }
           double x[MF];
-          ldlt_solve<MF>(Sv, u, x, pmin);
+          block_solve<MF>(Sv, u, x, pmin);
           const bool last_b = g == 1 && k == nst - 1;
           const double af = last_b ? 0.0 : 1.0;
           double out[MF];
@@ -450,7 +502,11 @@ struct Solver {
           for (int i = 0; i < MF; ++i) {
             double s = a[i] * af;
 #pragma unroll
-            for (int j = 0; j < MF; ++j) s = fma(-G[j][i], x[j], s);
+            for (int jj = 0; jj < MF; ++jj) {
+              // block2_solve finishes x[2], x[3] first: take them first.
+              const int j = MF == 4 ? (jj + 2) & 3 : jj;
+              s = fma(-G[j][i], x[j], s);
+            }
             out[i] = s;
           }
           lds_store(sm + xofs + k * ustep, x);
@@ -495,7 +551,7 @@ struct Solver {
 #pragma unroll
         for (int i = 0; i < MF; ++i) rr[i] = r0[i] + r1[i];
       }
-      ldlt_solve<MF>(Sv, rr, x, pmin);
+      block_solve<MF>(Sv, rr, x, pmin);
       MTG_STAMP(4);
       const int n_back = g == 0 ? m - 1 : S - 1 - m;
       const int vstep = g == 0 ? -1 : 1;
