@@ -583,14 +583,36 @@ struct Solver {
           zz = bz[(vv * D + d) * RS + pi];
         };
         int v = m + vstep;
-        if (n_back > 0) load_b(v);
-        for (int k = 0; k < n_back; ++k, v += vstep) {
-          double zc[MF], zzc = zz;
+        constexpr int kPre = 4;
+        if (n_back <= kPre) {
+          // Every step's operands in flight before the first step (S <= 10).
+          double zr4[kPre][MF], zz4[kPre];
 #pragma unroll
-          for (int c2 = 0; c2 < MF; ++c2) zc[c2] = zr[c2];
-          if (k + 1 < n_back) load_b(v + vstep);
-          step(zc, zzc);
-          dvp[(v * D + d) * MP + 1 + pi] = xi;
+          for (int k = 0; k < kPre; ++k) {
+            if (k < n_back) {
+              load_b(v + k * vstep);
+#pragma unroll
+              for (int c2 = 0; c2 < MF; ++c2) zr4[k][c2] = zr[c2];
+              zz4[k] = zz;
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < kPre; ++k) {
+            if (k < n_back) {
+              step(zr4[k], zz4[k]);
+              dvp[((v + k * vstep) * D + d) * MP + 1 + pi] = xi;
+            }
+          }
+        } else {
+          if (n_back > 0) load_b(v);
+          for (int k = 0; k < n_back; ++k, v += vstep) {
+            double zc[MF], zzc = zz;
+#pragma unroll
+            for (int c2 = 0; c2 < MF; ++c2) zc[c2] = zr[c2];
+            if (k + 1 < n_back) load_b(v + vstep);
+            step(zc, zzc);
+            dvp[(v * D + d) * MP + 1 + pi] = xi;
+          }
         }
       } else {
         if (g == 0) {
