@@ -772,21 +772,28 @@ TEST(gpu, ExtremaOfMagnitude) {
         EXPECT_TRUE(cand[j].time >= 0.0 && cand[j].time <= s.getTime());
         ++j;
       }
-      // f = sum_d v_d a_d in the monomial basis (segment.cpp:97-114); near
-      // a rest vertex f vanishes to high order and its values fall below
-      // the rounding of its coefficients (scale = sum |f_i| T^i): both
-      // searches then report roots of that noise, not necessarily the same
-      // ones.  Only simple roots, |f'| T > 1e-6 scale, are compared.
-      VectorXd fc(Polynomial::getConvolutionLength(9, 8));
-      for (int d = 0; d < f.D; ++d)
-        fc += Polynomial::convolve(s[d].getCoefficients(1).head(9), s[d].getCoefficients(2).head(8));
+      // The searched polynomial in the monomial basis: f = sum_d v_d a_d
+      // (segment.cpp:97-114), or a alone for D = 1 (:123-129).  Near a rest
+      // vertex it vanishes to high order and its values fall below the
+      // rounding of its coefficients (scale = sum |f_i| T^i): both searches
+      // then report roots of that noise, not necessarily the same ones.  Only
+      // simple roots, |f'| T > 1e-6 scale, are compared.
+      VectorXd fc;
+      if (f.D > 1) {
+        fc = VectorXd(Polynomial::getConvolutionLength(9, 8));
+        for (int d = 0; d < f.D; ++d)
+          fc += Polynomial::convolve(s[d].getCoefficients(1).head(9),
+                                     s[d].getCoefficients(2).head(8));
+      } else {
+        fc = s[0].getCoefficients(2).head(8);
+      }
       const Polynomial fp(fc);
       double fscale = 0.0;
       for (long q = 0; q < fc.size(); ++q) fscale += std::fabs(fc[q]) * std::pow(s.getTime(), q);
       for (size_t h = 2; h < host.size(); ++h) {
         const double t = host[h].time;
         if (t < 1e-6 * s.getTime() || t > s.getTime() * (1 - 1e-6)) continue;
-        if (f.D > 1 && std::fabs(fp.evaluate(t, 1)) * s.getTime() <= 1e-6 * fscale) continue;
+        if (std::fabs(fp.evaluate(t, 1)) * s.getTime() <= 1e-6 * fscale) continue;
         bool found = false;
         for (size_t k = i + 2; k < j; ++k) found = found || std::fabs(cand[k].time - t) <= 1e-7 * s.getTime();
         if (!found) {
