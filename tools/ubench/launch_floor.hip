@@ -1,6 +1,7 @@
 // Launch floor of back-to-back kernels in one HIP graph (the bench's timing
 // method): per-launch time of an empty kernel and of a one-load-one-store
-// kernel over 1024 / 8192 one-wave workgroups.
+// kernel over 1024 / 8192 one-wave workgroups, and the empty kernel with
+// the same waves in four-wave workgroups.
 //   hipcc --offload-arch=gfx950 -O3 -o /tmp/launch_floor tools/ubench/launch_floor.hip
 #include <hip/hip_runtime.h>
 
@@ -29,16 +30,19 @@ int main() {
   CHECK(hipMemset(a, 0, sizeof(double) * 8192 * 64));
   hipStream_t st;
   CHECK(hipStreamCreate(&st));
-  for (int kind = 0; kind < 2; ++kind) {
+  // kind 2: the 1024 one-wave workgroups as 256 workgroups of four waves.
+  for (int kind = 0; kind < 3; ++kind) {
     for (int blocks : {1024, 8192}) {
+      const int wg = kind == 2 ? 256 : 64;
+      const int nb = kind == 2 ? blocks / 4 : blocks;
       hipGraph_t g;
       hipGraphExec_t ge;
       CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
       for (int k = 0; k < K; ++k) {
-        if (kind == 0)
-          hipLaunchKernelGGL(empty_kernel, dim3(blocks), dim3(64), 0, st);
+        if (kind == 1)
+          hipLaunchKernelGGL(copy_kernel, dim3(nb), dim3(wg), 0, st, a, b);
         else
-          hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(64), 0, st, a, b);
+          hipLaunchKernelGGL(empty_kernel, dim3(nb), dim3(wg), 0, st);
       }
       CHECK(hipStreamEndCapture(st, &g));
       CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
@@ -52,8 +56,8 @@ int main() {
       CHECK(hipEventSynchronize(e1));
       float ms = 0;
       CHECK(hipEventElapsedTime(&ms, e0, e1));
-      std::printf("%s blocks=%d: %.3f us per launch\n", kind ? "copy " : "empty", blocks,
-                  1000.0 * ms / (5 * K));
+      std::printf("%s waves=%d (%d x %d): %.3f us per launch\n",
+                  kind == 1 ? "copy " : "empty", blocks, nb, wg, 1000.0 * ms / (5 * K));
       CHECK(hipGraphExecDestroy(ge));
       CHECK(hipGraphDestroy(g));
     }
