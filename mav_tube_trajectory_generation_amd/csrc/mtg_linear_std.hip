@@ -33,17 +33,21 @@ __global__ __launch_bounds__(kWave) void linear_std_kernel(
   const int lane = sv.lane, nf = sv.nf;
   const double* tb = times + b * S;
   const double* fb = fixed_vals + b * D * nf;
-  // Times first, then fixed values, then the table rows: loads retire in
-  // issue order, so the powers wait only for the times.
-  const double t_l = lane < S ? tb[lane] : 1.0;
-  const double f_l = lane < D * nf ? fb[lane] : 0.0;
+  // Fixed values first, then the times, then the table rows: loads retire in
+  // issue order, so the fixed values are stored to LDS while the times are
+  // still in flight, and the powers wait only for the times.
+  // Unconditional loads (clamped lanes re-read a valid element), so the
+  // wait before the fixed-value stores covers the first load only.
+  const double f_l = fb[lane < D * nf ? lane : D * nf - 1];
+  const double t_raw = tb[lane < S ? lane : S - 1];
+  const double t_l = lane < S ? t_raw : 1.0;
   sv.load_first_rows(tab);
+  sv.clear_mid_terms();
+  if (lane < D * nf) sv.put_fixed(lane, f_l);
+  for (int i = lane + kWave; i < D * nf; i += kWave) sv.put_fixed(i, fb[i]);
   bool bad = lane < S ? sv.powers(lane, t_l) : false;
   for (int s = lane + kWave; s < S; s += kWave) bad = sv.powers(s, tb[s]) || bad;
   MTG_STAMP(7);
-  if (lane < D * nf) sv.put_fixed(lane, f_l);
-  for (int i = lane + kWave; i < D * nf; i += kWave) sv.put_fixed(i, fb[i]);
-  sv.clear_mid_terms();
   const bool bad_time = __any(bad);
   __syncthreads();
   MTG_STAMP(1);
