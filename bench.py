@@ -54,6 +54,14 @@ def parse():
                    help="linear-solve kernel (mtg_plan_set_kernel); auto picks by batch size")
     p.add_argument("--soft", action="store_true",
                    help="time workload: soft constraints max|v| <= 3, max|a| <= 5 in the objective")
+    p.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--graph-head", type=int, default=0,
+                   help="steps in the first captured graph of the timed region (0: no head)")
+    p.add_argument("--graph-chunk", type=int, default=0,
+                   help="steps per captured graph after the head (0: all in one graph)")
+    p.add_argument("--sync", choices=["spin", "auto"], default=os.environ.get("MTG_BENCH_SYNC", "auto"),
+                   help="host wait mode of the HIP runtime (hipSetDeviceFlags): spin polls for "
+                        "completion, auto is the runtime's default")
     return p.parse_args()
 
 
@@ -291,10 +299,82 @@ def config_name(wl, B, world, S):
     return f"{wl}: {B} x {S}-segment per GPU"
 
 
-def main():
-    args = parse()
+def graph_chunks(k, head, chunk):
+    """Sizes of the graphs the K timed steps are captured into, in replay
+    order: `head` steps first (0: none), then graphs of `chunk` steps (0: the
+    rest in one graph).  Smaller first graphs let the device start while the
+    host still submits the later ones."""
+    sizes = []
+    if 0 < head < k:
+        sizes.append(head)
+    rest = k - sum(sizes)
+    c = chunk if chunk > 0 else rest
+    while rest > 0:
+        sizes.append(min(c, rest))
+        rest -= sizes[-1]
+    return sizes
+
+
+def launch_ranks(n, argv, port=None):
+    """`--gpus N` without a launcher: run N ranks of this script under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a
+    child process, before this process touches the GPU, and return its exit
+    code.  Rank 0 prints the JSON line on the inherited stdout."""
+    import socket
+    import subprocess
+    if port is None:
+        with socket.socket() as sk:  # a free port on the loopback interface
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check():
+    """`--launch-check` (tests): each rank joins a gloo group over the
+    launcher's rendezvous, all-reduces its rank and rank 0 prints one JSON line
+    {world, rank_sum}; no GPU is touched."""
     import torch
     import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(dist.get_rank())])
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"world": dist.get_world_size(), "rank_sum": t.item()}))
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if int(env_world or "1") != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU "
+              f"(torch.distributed.run --nproc-per-node {args.gpus}) or pass --gpus "
+              f"{env_world}", file=sys.stderr)
+        sys.exit(2)
+    if args.launch_check:
+        launch_check()
+        return
+    import torch
+    import torch.distributed as dist
+
+    if args.sync == "spin":
+        # Before the first HIP call of the process: the host polls for
+        # completion instead of sleeping on an interrupt.  Torch's runtime is
+        # the one in the process (libmtg_hip.so resolves to it by soname).
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        hip.hipSetDevice(ctypes.c_int(int(os.environ.get("LOCAL_RANK", "0"))))
+        rc = hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+        if rc != 0:
+            print(f"bench: hipSetDeviceFlags(spin) returned {rc}", file=sys.stderr)
 
     import mav_tube_trajectory_generation_amd as mtg
 
@@ -570,12 +650,17 @@ def main():
             dist.barrier()
     if use_graph:
         try:  # capture only: nothing executes (no collective runs) here
-            for name, n in (("warmup", args.warmup), ("timed", args.steps)):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for _ in range(n):
-                        step()
-                graphs[name] = g
+            for name, sizes in (("warmup", [args.warmup]),
+                                ("timed", graph_chunks(args.steps, args.graph_head,
+                                                       args.graph_chunk))):
+                gl = []
+                for n in sizes:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        for _ in range(n):
+                            step()
+                    gl.append(g)
+                graphs[name] = gl
         except Exception as exc:  # capture unsupported here: eager launches
             use_graph = False
             graph_note = f" (graph capture failed: {type(exc).__name__}; eager)"
@@ -590,7 +675,8 @@ def main():
                 use_graph = False
                 graph_note = " (graph capture failed on another rank; eager)"
         if use_graph:
-            graphs["warmup"].replay()
+            for g in graphs["warmup"]:
+                g.replay()
         else:
             graphs = {}
     if not use_graph:
@@ -605,7 +691,8 @@ def main():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
-        graphs["timed"].replay()
+        for g in graphs["timed"]:
+            g.replay()
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         if world > 1:

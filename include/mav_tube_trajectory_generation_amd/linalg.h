@@ -113,6 +113,18 @@ class VectorXd {
 
 inline VectorXd operator*(double s, const VectorXd& v) { return v * s; }
 
+// Eigen::Vector3d (the x, y, z triples of
+// PolynomialOptimizationNonLinear::getFreeConstraints,
+// polynomial_optimization_nonlinear.h:293): a VectorXd of size 3.
+class Vector3d : public VectorXd {
+ public:
+  Vector3d() : VectorXd(3) {}
+  Vector3d(double x, double y, double z) : VectorXd({x, y, z}) {}
+  double x() const { return (*this)[0]; }
+  double y() const { return (*this)[1]; }
+  double z() const { return (*this)[2]; }
+};
+
 inline std::ostream& operator<<(std::ostream& os, const VectorXd& v) {
   for (long i = 0; i < v.size(); ++i) os << (i ? " " : "") << v[i];
   return os;

@@ -300,6 +300,7 @@ class PolynomialOptimizationNonLinear {
     linear_.getSegmentTimes(&times);
     linear_.solveLinear();  // initial solution (nonlinear_impl:341-349)
     linear_.getTrajectory(&trajectory_initial_);
+    trajectory_initial_after_removing_pos_ = trajectory_initial_;  // :347-348, 416-417
     const size_t S = times.size();
     internal::DeviceBuffer<double> d_df, d_t, d_cost(1);
     internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
@@ -354,6 +355,61 @@ class PolynomialOptimizationNonLinear {
   }
   void getFreeConstraints(std::vector<VectorXd>* free_constraints) const {
     linear_.getFreeConstraints(free_constraints);
+  }
+  // polynomial_optimization_nonlinear.h:293-295: the free derivatives as x, y,
+  // z triples (D = 3), one per free derivative in the tube-pattern order of
+  // poly_opt_ (the problem the free-derivative objectives optimise).
+  void getFreeConstraints(std::vector<Vector3d>* free_constraints) const {
+    MTG_CHECK(free_constraints != nullptr, "free_constraints must not be null");
+    MTG_CHECK(dimension_ == 3, "Vector3d free constraints need dimension 3");
+    std::vector<VectorXd> f;
+    poly_opt_.getFreeConstraints(&f);
+    free_constraints->clear();
+    if (f.size() != 3) return;
+    for (long i = 0; i < f[0].size(); ++i)
+      free_constraints->push_back(Vector3d(f[0][i], f[1][i], f[2][i]));
+  }
+  // :307-314: the trajectory of the initial solution the optimiser starts
+  // from (after the intermediate positions became free derivatives).
+  void getInitialTrajectoryAfterRemovingPos(Trajectory* trajectory) const {
+    MTG_CHECK(trajectory != nullptr, "trajectory must not be null");
+    MTG_CHECK(!trajectory_initial_after_removing_pos_.empty(), "optimize() has not run");
+    *trajectory = trajectory_initial_after_removing_pos_;
+  }
+  // :316-331: the trajectory of every objective evaluation of the collision
+  // objectives (pushed at nonlinear_impl:1244, 1482; never cleared, as
+  // there), appended to *trajectories.
+  void getAllTrajectories(std::vector<Trajectory>* trajectories) const {
+    MTG_CHECK(trajectories != nullptr, "trajectories must not be null");
+    trajectories->reserve(trajectories->size() + all_trajectories_.size());
+    for (const Trajectory& t : all_trajectories_) {
+      MTG_CHECK(!t.empty(), "empty trajectory in the history");
+      trajectories->push_back(t);
+    }
+  }
+  // computeInitialSolutionWithPositionConstraints (nonlinear_impl:199-272):
+  // solveQCQP, keep its trajectory as the initial one, then express it in
+  // the pattern with the intermediate positions free.  The tube problem
+  // (poly_opt_) already has every intermediate derivative free (the kDim
+  // reordering, qcqp_impl:18-118), so re-deriving d_p from the coefficients
+  // (M_pinv A p) returns the solve's own d_p, which is set back.
+  bool computeInitialSolutionWithPositionConstraints() {
+    poly_opt_.solveQCQP();
+    poly_opt_.getTrajectory(&trajectory_initial_);
+    std::vector<double> t;
+    poly_opt_.getSegmentTimes(&t);
+    trajectory_time_initial_ = 0.0;
+    for (double ti : t) trajectory_time_initial_ += ti;  // computeTotalTrajectoryTime
+    std::vector<VectorXd> free;
+    poly_opt_.getFreeConstraints(&free);
+    poly_opt_.setFreeConstraints(free);
+    return true;
+  }
+  // Declared at polynomial_optimization_nonlinear.h:379; its definition is
+  // commented out in the reference (nonlinear_impl:122-196) with the same
+  // body as the WithPositionConstraints variant, which it runs here.
+  bool computeInitialSolutionWithoutPositionConstraints() {
+    return computeInitialSolutionWithPositionConstraints();
   }
   const PolynomialOptimization<N>& getPolynomialOptimizationRef() const { return linear_; }
   PolynomialOptimization<N>& getPolynomialOptimizationRef() { return linear_; }
@@ -616,7 +672,11 @@ class PolynomialOptimizationNonLinear {
   // setFreeEndpointDerivativeHardConstraints (nonlinear_impl:2858-2905) over
   // the free derivatives x (dimension-major), including the reference's
   // stride of derivative_to_optimize per vertex when
-  // solve_with_position_constraint is set (:2879-2880).
+  // solve_with_position_constraint is set (:2879-2880).  Indices are
+  // unsigned int and every write goes through .at(), as in the reference: a
+  // position-magnitude constraint with solve_with_position_constraint wraps
+  // (derivative - 1) and a derivative past the vertex stride runs off the
+  // end; both throw std::out_of_range instead of writing out of bounds.
   void freeEndpointBounds(size_t n, std::vector<double>* lo, std::vector<double>* hi) const {
     const size_t np = poly_opt_.getNumberFreeConstraints();
     const size_t S = poly_opt_.getNumberSegments();
@@ -625,19 +685,20 @@ class PolynomialOptimizationNonLinear {
     const int r = poly_opt_.getDerivativeToOptimize();
     for (size_t k = 0; k < dimension_; ++k)
       for (size_t v = 0; v + 1 < S; ++v) {
-        size_t start;
+        unsigned int start;
         if (params_.solve_with_position_constraint) {
-          start = k * np + v * r;
+          start = static_cast<unsigned int>(k * np + v * r);
         } else {
-          start = k * np + v * (r + 1);
-          (*lo)[start] = params_.min_bound[static_cast<long>(k)];
-          (*hi)[start] = params_.max_bound[static_cast<long>(k)];
+          start = static_cast<unsigned int>(k * np + v * (r + 1));
+          lo->at(start) = params_.min_bound[static_cast<long>(k)];
+          hi->at(start) = params_.max_bound[static_cast<long>(k)];
         }
         for (const auto& c : soft_) {
-          const size_t idx =
-              start + (params_.solve_with_position_constraint ? c.first - 1 : c.first);
-          (*lo)[idx] = -std::abs(c.second);
-          (*hi)[idx] = std::abs(c.second);
+          const unsigned int deriv = params_.solve_with_position_constraint
+                                         ? static_cast<unsigned int>(c.first - 1)
+                                         : static_cast<unsigned int>(c.first);
+          lo->at(static_cast<size_t>(start) + deriv) = -std::abs(c.second);
+          hi->at(static_cast<size_t>(start) + deriv) = std::abs(c.second);
         }
       }
   }
@@ -656,6 +717,7 @@ class PolynomialOptimizationNonLinear {
     const auto t0 = std::chrono::steady_clock::now();
     poly_opt_.solveQCQP();
     poly_opt_.getTrajectory(&trajectory_initial_);
+    trajectory_initial_after_removing_pos_ = trajectory_initial_;  // :347-348, 416-417
     std::vector<VectorXd> free;
     poly_opt_.getFreeConstraints(&free);
     MTG_CHECK(!free.empty() && free.front().size() > 0, "no free constraints (:516-517)");
@@ -688,27 +750,30 @@ class PolynomialOptimizationNonLinear {
     internal::DeviceBuffer<double> d_df, d_x, d_t, d_lo, d_hi, d_step, d_cost(1), d_terms(4);
     internal::DeviceBuffer<int32_t> d_ev(1), d_res(1), d_st(1);
     internal::DeviceBuffer<unsigned char> ws(static_cast<size_t>(nb));
-    d_df.upload(packFixedQcqp());
+    const std::vector<double> fixed = packFixedQcqp();
+    d_df.upload(fixed);
     d_x.upload(x);
     d_t.upload(times);
     d_lo.upload(lo);
     d_hi.upload(hi);
     d_step.upload(step);
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
+    internal::DeviceBuffer<double> d_hist(static_cast<size_t>(budget) * nv);
     internal::checkStatus(
-        mtg_coll_optimize(poly_opt_.getPlan(), 1, mode, d_df.get(), d_x.get(), d_t.get(),
-                          d_lo.get(), d_hi.get(), d_step.get(), occupancy_.get(), occ_dims_[0],
-                          occ_dims_[1], occ_dims_[2], nearField(cp.coll), &cp, budget,
-                          d_cost.get(), d_ev.get(),
-                          d_res.get(), d_st.get(), d_terms.get(), ws.get(),
-                          static_cast<size_t>(nb), nullptr),
-        "mtg_coll_optimize");
+        mtg_coll_optimize_trace(poly_opt_.getPlan(), 1, mode, d_df.get(), d_x.get(), d_t.get(),
+                                d_lo.get(), d_hi.get(), d_step.get(), occupancy_.get(),
+                                occ_dims_[0], occ_dims_[1], occ_dims_[2], nearField(cp.coll), &cp,
+                                budget, d_cost.get(), d_ev.get(), d_res.get(), d_st.get(),
+                                d_terms.get(), d_hist.get(), ws.get(), static_cast<size_t>(nb),
+                                nullptr),
+        "mtg_coll_optimize_trace");
     internal::synchronize();
     x = d_x.download();
     int32_t evals = 0, res = 0, st = 0;
     d_ev.download(&evals, 1);
     d_res.download(&res, 1);
     d_st.download(&st, 1);
+    appendHistory(d_hist, evals, nv, with_time, fixed, times);
     double terms[4] = {0, 0, 0, 0};
     d_terms.download(terms, 4);
     if (with_time) {
@@ -738,6 +803,7 @@ class PolynomialOptimizationNonLinear {
     std::vector<double> times = segmentTimesOfQcqp();
     poly_opt_.solveQCQP();
     poly_opt_.getTrajectory(&trajectory_initial_);
+    trajectory_initial_after_removing_pos_ = trajectory_initial_;  // :347-348, 416-417
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
     double J = 0.0;
     int32_t evals = 0;
@@ -759,6 +825,51 @@ class PolynomialOptimizationNonLinear {
     optimization_info_.optimization_time =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return optimization_info_.stopping_reason;
+  }
+
+  // all_trajectories_ (nonlinear_impl:1241-1244, 1479-1482): the trajectory
+  // of every counted evaluation, in order.  The evaluated points come from
+  // the device optimiser's history; their coefficients from one batched
+  // mtg_coeffs_from_constraints over the tube-pattern plan.
+  void appendHistory(const internal::DeviceBuffer<double>& d_hist, int evals, size_t nv,
+                     bool with_time, const std::vector<double>& fixed,
+                     const std::vector<double>& times0) {
+    if (evals <= 0) return;
+    const size_t S = times0.size(), off = with_time ? S : 0, nd = nv - off;
+    const size_t ne = static_cast<size_t>(evals), D = dimension_;
+    std::vector<double> hx(ne * nv);
+    d_hist.download(hx.data(), hx.size());
+    std::vector<double> df, dp, tt;
+    for (size_t e = 0; e < ne; ++e) {
+      df.insert(df.end(), fixed.begin(), fixed.end());
+      for (size_t i = 0; i < nd; ++i) dp.push_back(hx[e * nv + off + i]);
+      for (size_t i = 0; i < S; ++i) tt.push_back(with_time ? hx[e * nv + i] : times0[i]);
+    }
+    internal::DeviceBuffer<double> d_df, d_dp, d_t, d_c(ne * S * D * N);
+    d_df.upload(df);
+    d_dp.upload(dp);
+    d_t.upload(tt);
+    internal::checkStatus(mtg_coeffs_from_constraints(poly_opt_.getPlan(),
+                                                      static_cast<int64_t>(ne), d_df.get(),
+                                                      d_dp.get(), d_t.get(), d_c.get(), nullptr,
+                                                      nullptr, nullptr),
+                          "mtg_coeffs_from_constraints");
+    internal::synchronize();
+    const std::vector<double> c = d_c.download();
+    for (size_t e = 0; e < ne; ++e) {
+      Segment::Vector segs(S, Segment(N, static_cast<int>(D)));
+      for (size_t s = 0; s < S; ++s) {
+        segs[s].setTime(tt[e * S + s]);
+        for (size_t d = 0; d < D; ++d) {
+          VectorXd cd(N);
+          for (int k = 0; k < N; ++k) cd[k] = c[((e * S + s) * D + d) * N + k];
+          segs[s][static_cast<int>(d)] = Polynomial(N, cd);
+        }
+      }
+      Trajectory t;
+      t.setSegments(segs);
+      all_trajectories_.push_back(t);
+    }
   }
 
   std::vector<double> segmentTimesOfQcqp() const {
@@ -830,6 +941,7 @@ class PolynomialOptimizationNonLinear {
     const auto t0 = std::chrono::steady_clock::now();
     poly_opt_.solveQCQP();
     poly_opt_.getTrajectory(&trajectory_initial_);
+    trajectory_initial_after_removing_pos_ = trajectory_initial_;  // :347-348, 416-417
     std::vector<VectorXd> free;
     poly_opt_.getFreeConstraints(&free);
     const std::vector<double> x0 = packFree(free);
@@ -880,6 +992,7 @@ class PolynomialOptimizationNonLinear {
     const auto t0 = std::chrono::steady_clock::now();
     poly_opt_.solveQCQP();
     poly_opt_.getTrajectory(&trajectory_initial_);
+    trajectory_initial_after_removing_pos_ = trajectory_initial_;  // :347-348, 416-417
     std::vector<VectorXd> free;
     poly_opt_.getFreeConstraints(&free);
     MTG_CHECK(!free.empty() && free.front().size() > 0, "no free constraints (:619-621)");
@@ -967,7 +1080,10 @@ class PolynomialOptimizationNonLinear {
   PolynomialOptimizationConstrained<N> poly_opt_;
   PolynomialOptimization<N> linear_;
   Vertex::Vector vertices_;
+  double trajectory_time_initial_ = 0.0;
   Trajectory trajectory_initial_;
+  Trajectory trajectory_initial_after_removing_pos_;
+  std::vector<Trajectory> all_trajectories_;
   OptimizationInfo optimization_info_;
   std::vector<std::pair<int, double>> soft_;  // (derivative, maximum_value)
   internal::DeviceBuffer<float> occupancy_;

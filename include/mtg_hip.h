@@ -638,6 +638,20 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
                       const mtg_coll_params* params, int max_evals,
                       double* cost, int32_t* evals, int32_t* result, int32_t* status,
                       double* terms, void* workspace, size_t workspace_bytes, void* stream);
+/* mtg_coll_optimize with the evaluation history the reference keeps in
+ * all_trajectories_ (one trajectory pushed per objective evaluation,
+ * nonlinear_impl:1244, 1482; read by getAllTrajectories,
+ * polynomial_optimization_nonlinear.h:316-331): x_history (device,
+ * nullable) B x max_evals x nx, row k = the point of the (k+1)-th counted
+ * evaluation; rows at or past evals[b] are not written. */
+int mtg_coll_optimize_trace(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
+                            double* x_io, const double* times, const double* lower,
+                            const double* upper, const double* initial_step,
+                            const float* occupancy, int nx, int ny, int nz,
+                            const uint16_t* near_field, const mtg_coll_params* params,
+                            int max_evals, double* cost, int32_t* evals, int32_t* result,
+                            int32_t* status, double* terms, double* x_history, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Selection for the multi-GPU path (BASELINE config 4: the

@@ -162,6 +162,12 @@ SIGNATURES = {
                                          _vp, ctypes.POINTER(CollObjectiveParams), ctypes.c_int,
                                          _vp,
                                          _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "mtg_coll_optimize_trace": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp,
+                                               _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, _vp,
+                                               ctypes.POINTER(CollObjectiveParams), ctypes.c_int,
+                                               _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t,
+                                               _vp]),
     "mtg_min_max_magnitude": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp, _vp,
                                              _vp, _vp, _vp, _vp, _vp]),

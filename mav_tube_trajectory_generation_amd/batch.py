@@ -388,11 +388,13 @@ class LinearPlan:
 
     def coll_optimize(self, fixed_vals, x0, times, occupancy, params, mode=0, max_evals=25,
                       lower=None, upper=None, initial_step=None, workspace=None,
-                      near_field=None):
+                      near_field=None, history=False):
         """Device L-BFGS over the collision objective (mtg_coll_optimize;
         optimizeFreeConstraintsAndCollision / ...AndTime with NLopt
         replaced); near_field as coll_cost.  Returns dict(x, cost, evals,
-        result, status, terms)."""
+        result, status, terms); with history=True also x_history
+        (B x max_evals x nx, the evaluated points in order, rows past evals
+        unset: mtg_coll_optimize_trace)."""
         import torch
         B = self._coll_inputs(fixed_vals, x0, times, occupancy, mode)
         _check_field(near_field, occupancy)
@@ -410,14 +412,19 @@ class LinearPlan:
         terms = torch.empty((B, 4), dtype=torch.float64, device=dev)
         nb = self.coll_workspace_bytes(B, params, mode, True)
         ws = _workspace(workspace, nb, dev)
-        check(lib().mtg_coll_optimize(self._h, B, mode, _ptr(fixed_vals), _ptr(x),
-                                      _ptr(times) if mode == 0 else None, _ptr(lower),
-                                      _ptr(upper), _ptr(initial_step), _ptr(occupancy), nx, ny,
-                                      nz, _ptr(near_field), ctypes.byref(params), max_evals,
-                                      _ptr(cost), _ptr(ev),
-                                      _ptr(res), _ptr(st), _ptr(terms), _ptr(ws), nb,
-                                      _stream(dev)), "mtg_coll_optimize")
-        return dict(x=x, cost=cost, evals=ev, result=res, status=st, terms=terms)
+        hist = (torch.full((B, max_evals, nv), float("nan"), dtype=torch.float64, device=dev)
+                if history else None)
+        check(lib().mtg_coll_optimize_trace(self._h, B, mode, _ptr(fixed_vals), _ptr(x),
+                                            _ptr(times) if mode == 0 else None, _ptr(lower),
+                                            _ptr(upper), _ptr(initial_step), _ptr(occupancy), nx,
+                                            ny, nz, _ptr(near_field), ctypes.byref(params),
+                                            max_evals, _ptr(cost), _ptr(ev), _ptr(res), _ptr(st),
+                                            _ptr(terms), _ptr(hist), _ptr(ws), nb, _stream(dev)),
+              "mtg_coll_optimize_trace")
+        out = dict(x=x, cost=cost, evals=ev, result=res, status=st, terms=terms)
+        if history:
+            out["x_history"] = hist
+        return out
 
     # -- host (numpy) API ---------------------------------------------------
     def solve_host(self, fixed_vals, times):
@@ -676,7 +683,9 @@ def magnitude_candidates(coeffs, times, derivative, max_candidates=None):
     time / value [B, S, C] and count [B, S] int32: per segment t = 0, T and
     the real roots of d/dt |p^(derivative)|^2 in [0, T] ascending, with
     |p^(derivative)| at each; entries past count are unset.  C defaults to
-    2 (N - derivative) - 1, which always suffices.
+    2 (N - derivative) - 1, which always suffices.  count is clamped to C
+    (the stored entries); found [B, S] is the number the search found, which
+    exceeds count only when a smaller max_candidates truncated the list.
     """
     import torch
     B, S, D, N = coeffs.shape
@@ -691,6 +700,8 @@ def magnitude_candidates(coeffs, times, derivative, max_candidates=None):
                                          _ptr(out["time"]), _ptr(out["value"]),
                                          _ptr(out["count"]), _stream(dev)),
           "mtg_magnitude_candidates")
+    out["found"] = out["count"]
+    out["count"] = torch.clamp(out["found"], max=C)
     return out
 
 

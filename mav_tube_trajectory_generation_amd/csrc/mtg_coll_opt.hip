@@ -362,6 +362,9 @@ struct CombineOut {
   double* terms;
   int32_t* collision;
   int32_t* status;
+  // Optimiser only (nullable): B x max_evals x nv, row k = the point of the
+  // (k+1)-th counted evaluation (all_trajectories_, nonlinear_impl:1244,1482).
+  double* x_history;
 };
 
 struct Bounds {
@@ -548,6 +551,10 @@ __global__ __launch_bounds__(kWave) void coll_combine_kernel(CollDims cd, mtg_co
     double f = w.f[b], alpha = w.alpha[b];
     int result = 0;  // 0: continue
     bool place = false;
+    if (o.x_history) {  // the evaluated point, before the state machine moves xt
+      double* hrow = o.x_history + (b * max_evals + (evals - 1)) * nv;
+      for (int i = lane; i < nv; i += kWave) hrow[i] = xt[i];
+    }
     if (lane == 0) {
       if (phase == 0) w.Jref0[b] = J;  // total_cost_iter0_ (:1253-1257)
       w.Jlast[b] = J;                  // optimization_info_ of this evaluation
@@ -804,7 +811,7 @@ int coll_cost(const PlanDev& pl, int64_t B, int mode, const double* df, const do
   hipError_t e;
   MTG_COLL_DISPATCH(evaluate_n, pl, cd, B, df, x, times, occ, nx, ny, nz, field, p, w, st)
   if (e != hipSuccess) return MTG_ERR_HIP;
-  const CombineOut o{raise_ref, cost, grad, terms, collision, status};
+  const CombineOut o{raise_ref, cost, grad, terms, collision, status, nullptr};
   hipLaunchKernelGGL(coll_combine_kernel<false>, dim3(grid1(B)), dim3(kWave), 0, st, cd, p, 0,
                      Bounds{nullptr, nullptr}, w, o);
   return hipGetLastError() == hipSuccess ? MTG_OK : MTG_ERR_HIP;
@@ -814,8 +821,8 @@ int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, doub
                   const double* times, const double* lower, const double* upper,
                   const double* initial_step, const float* occ, int nx, int ny, int nz,
                   const uint16_t* field, const mtg_coll_params& p, int max_evals, double* cost, int32_t* evals,
-                  int32_t* result, int32_t* status, double* terms, void* workspace,
-                  size_t workspace_bytes, hipStream_t st) {
+                  int32_t* result, int32_t* status, double* terms, double* x_history,
+                  void* workspace, size_t workspace_bytes, hipStream_t st) {
   const CollDims cd = coll_dims(pl, mode, p);
   if (coll_workspace_bytes(pl, B, mode, p, true) > workspace_bytes) return MTG_ERR_INVALID_ARG;
   CollWs w;
@@ -824,13 +831,14 @@ int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, doub
   hipLaunchKernelGGL(coll_opt_init_kernel, dim3(grid1(B)), dim3(kWave), 0, st, B, cd.nv, x_io,
                      initial_step, bd, w);
   if (hipGetLastError() != hipSuccess) return MTG_ERR_HIP;
-  const CombineOut none{};
+  CombineOut hist{};
+  hist.x_history = x_history;
   for (int round = 0; round < max_evals; ++round) {
     hipError_t e;
     MTG_COLL_DISPATCH(evaluate_n, pl, cd, B, df, w.xt, times, occ, nx, ny, nz, field, p, w, st)
     if (e != hipSuccess) return MTG_ERR_HIP;
     hipLaunchKernelGGL(coll_combine_kernel<true>, dim3(grid1(B)), dim3(kWave), 0, st, cd, p,
-                       max_evals, bd, w, none);
+                       max_evals, bd, w, hist);
     if (hipGetLastError() != hipSuccess) return MTG_ERR_HIP;
   }
   hipLaunchKernelGGL(coll_opt_final_kernel, dim3(grid1(B)), dim3(kWave), 0, st, B, cd.nv, w,

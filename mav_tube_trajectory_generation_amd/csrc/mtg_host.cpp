@@ -536,13 +536,14 @@ int mtg_coll_cost(const mtg_plan* plan, int64_t B, int mode, const double* fixed
                         workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
-int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
-                      double* x_io, const double* times, const double* lower,
-                      const double* upper, const double* initial_step, const float* occupancy,
-                      int nx, int ny, int nz, const uint16_t* near_field,
-                      const mtg_coll_params* params, int max_evals,
-                      double* cost, int32_t* evals, int32_t* result, int32_t* status,
-                      double* terms, void* workspace, size_t workspace_bytes, void* stream) {
+int mtg_coll_optimize_trace(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
+                            double* x_io, const double* times, const double* lower,
+                            const double* upper, const double* initial_step,
+                            const float* occupancy, int nx, int ny, int nz,
+                            const uint16_t* near_field, const mtg_coll_params* params,
+                            int max_evals, double* cost, int32_t* evals, int32_t* result,
+                            int32_t* status, double* terms, double* x_history, void* workspace,
+                            size_t workspace_bytes, void* stream) {
   if (B < 0 || max_evals < 1 || !valid_coll_params(plan, mode, params) ||
       !valid_collision_params(params->coll, nx, ny, nz))
     return MTG_ERR_INVALID_ARG;
@@ -554,8 +555,21 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
   return mtg::coll_optimize(plan->dev, B, mode, fixed_vals, x_io, times, lower, upper,
                             initial_step, occupancy, nx, ny, nz, near_field, *params, max_evals,
                             cost, evals,
-                            result, status, terms, workspace, workspace_bytes,
+                            result, status, terms, x_history, workspace, workspace_bytes,
                             static_cast<hipStream_t>(stream));
+}
+
+int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
+                      double* x_io, const double* times, const double* lower,
+                      const double* upper, const double* initial_step, const float* occupancy,
+                      int nx, int ny, int nz, const uint16_t* near_field,
+                      const mtg_coll_params* params, int max_evals,
+                      double* cost, int32_t* evals, int32_t* result, int32_t* status,
+                      double* terms, void* workspace, size_t workspace_bytes, void* stream) {
+  return mtg_coll_optimize_trace(plan, B, mode, fixed_vals, x_io, times, lower, upper,
+                                 initial_step, occupancy, nx, ny, nz, near_field, params,
+                                 max_evals, cost, evals, result, status, terms, nullptr, workspace,
+                                 workspace_bytes, stream);
 }
 
 int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank, double* out,

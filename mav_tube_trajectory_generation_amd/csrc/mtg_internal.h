@@ -40,6 +40,12 @@ struct SelectArgs {
 // Workgroups of the fused solve (the partial slots the workspace needs).
 int64_t select_partials(const PlanDev& pl, int64_t B);
 
+// Standard-pattern linear solve at compile-time S (mtg_linear_wave.hip):
+// N = 10, r = 4, D = 3, 2 <= S <= 16, the kernel behind "standard" there.
+bool has_linear_wave(const PlanDev& pl);
+hipError_t launch_linear_solve_wave(const PlanDev& pl, int64_t B, const double* df,
+                                    const double* times, double* coeffs, double* cost,
+                                    double* free_vals, int32_t* status, hipStream_t st);
 // Standard-pattern linear solve (mtg_linear_std.hip).
 constexpr int kMaxStdS = 64;
 // Lane linear solve for large batches (mtg_linear_lane.hip): one
@@ -253,8 +259,8 @@ int coll_optimize(const PlanDev& pl, int64_t B, int mode, const double* df, doub
                   const double* times, const double* lower, const double* upper,
                   const double* initial_step, const float* occ, int nx, int ny, int nz,
                   const uint16_t* field, const mtg_coll_params& p, int max_evals, double* cost, int32_t* evals,
-                  int32_t* result, int32_t* status, double* terms, void* workspace,
-                  size_t workspace_bytes, hipStream_t st);
+                  int32_t* result, int32_t* status, double* terms, double* x_history,
+                  void* workspace, size_t workspace_bytes, hipStream_t st);
 
 // Multi-GPU selection (mtg_select.hip).
 hipError_t launch_select_local(const double* costs, int64_t count, int64_t start, int rank,

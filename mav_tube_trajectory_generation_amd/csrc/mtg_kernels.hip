@@ -39,6 +39,8 @@ __global__ __launch_bounds__(kWave) void linear_solve_kernel(
   const int64_t per = static_cast<int64_t>(S) * D * N;
   if (bad_time) {
     for (int i = t.lane; i < per; i += kWave) coeffs[b * per + i] = NAN;
+    if (free_vals)  // as every linear kernel: NaN free values on a bad time
+      for (int i = t.lane; i < D * np; i += kWave) free_vals[b * D * np + i] = NAN;
     if (cost && t.lane == 0) cost[b] = NAN;
   } else {
     const double J = t.template coeffs_and_cost<true>(pl.tab, coeffs + b * per);

@@ -207,6 +207,13 @@ struct LaneSolve {
         for (int dd = 0; dd < ND; ++dd)
 #pragma unroll
           for (int i = 0; i < N; ++i) cb[(s * D + d0 + dd) * N + i] = NAN;
+      if (free_vals) {
+        constexpr int np = (S - 1) * MF;
+#pragma unroll
+        for (int dd = 0; dd < ND; ++dd)
+#pragma unroll
+          for (int i = 0; i < np; ++i) free_vals[(b * D + d0 + dd) * np + i] = NAN;
+      }
       *cost_part = NAN;
       return 1;
     }

@@ -414,14 +414,26 @@ struct Half {
     return acc;
   }
 
-  // NaN coefficients of the half's segments (bad segment time).
-  __device__ void write_bad(int d, double* __restrict__ cb) const {
-    if (!cb) return;
+  // Bad segment time: NaN coefficients of the half's segments and NaN free
+  // values of the half's vertices (forward 1..MID, backward MID+1..S-1, the
+  // vertices finish() writes), as every other linear kernel reports them.
+  __device__ void write_bad(int64_t b, int d, double* __restrict__ cb,
+                            double* __restrict__ free_vals) const {
+    if (cb) {
 #pragma unroll
-    for (int j = 0; j < NSEG; ++j) {
-      const int s = BW ? MID + j : MID - 1 - j;
+      for (int j = 0; j < NSEG; ++j) {
+        const int s = BW ? MID + j : MID - 1 - j;
 #pragma unroll
-      for (int i = 0; i < N; ++i) cb[(s * D + d) * N + i] = NAN;
+        for (int i = 0; i < N; ++i) cb[(s * D + d) * N + i] = NAN;
+      }
+    }
+    if (free_vals) {
+      constexpr int np = (S - 1) * MF;
+      constexpr int v0 = BW ? MID + 1 : 1, v1 = BW ? S - 1 : MID;
+#pragma unroll
+      for (int v = v0; v <= v1; ++v)
+#pragma unroll
+        for (int i = 0; i < MF; ++i) free_vals[(b * D + d) * np + (v - 1) * MF + i] = NAN;
     }
   }
 };
@@ -466,13 +478,15 @@ __device__ __attribute__((always_inline)) inline void lane2_half(
   double* cb = (act && coeffs) ? coeffs + b * S * D * N : nullptr;
   double* fv = act ? free_vals : nullptr;
   double part;
+  // A bad time's solve values are not stored (write_bad fills NaN).
+  double* fv_ok = h.bad ? nullptr : fv;
   if (BW)
-    part = h.finish(bb, d, to, ro, tm, rm, cb, fv);
+    part = h.finish(bb, d, to, ro, tm, rm, cb, fv_ok);
   else
-    part = h.finish(bb, d, tm, rm, to, ro, cb, fv);
+    part = h.finish(bb, d, tm, rm, to, ro, cb, fv_ok);
   int st = h.bad ? 1 : (h.pmin > 0.0 ? 0 : 2);
   if (h.bad) {
-    h.write_bad(d, cb);
+    h.write_bad(bb, d, cb, fv);
     part = NAN;
   }
   if (BW) {

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "mtg_std_device.h"
 
@@ -55,6 +56,10 @@ __global__ __launch_bounds__(kWave) void linear_std_kernel(
   const int64_t per = static_cast<int64_t>(S) * D * N;
   if (bad_time) {
     for (int i = lane; i < per; i += kWave) coeffs[b * per + i] = NAN;
+    if (free_vals) {
+      const int64_t nfv = static_cast<int64_t>(D) * (S - 1) * Sv::MF;
+      for (int i = lane; i < nfv; i += kWave) free_vals[b * nfv + i] = NAN;
+    }
     if (cost && lane == 0) cost[b] = NAN;
     if (status && lane == 0) status[b] = MTG_TRAJ_BAD_TIME;
     return;
@@ -123,9 +128,21 @@ static hipError_t launch_std_n(int r, int D, int S, int64_t B, const double* tab
 #undef MTG_STD_R
 }
 
+// MTG_STD_RUNTIME_S=1 (diagnostics): the runtime-S kernel below also where
+// the compile-time-S kernel (mtg_linear_wave.hip) exists, for A/B runs.
+static bool runtime_s_forced() {
+  static const bool forced = [] {
+    const char* e = std::getenv("MTG_STD_RUNTIME_S");
+    return e && e[0] == '1';
+  }();
+  return forced;
+}
+
 hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
                                    const double* times, double* coeffs, double* cost,
                                    double* free_vals, int32_t* status, hipStream_t st) {
+  if (has_linear_wave(pl) && !runtime_s_forced())
+    return launch_linear_solve_wave(pl, B, df, times, coeffs, cost, free_vals, status, st);
   switch (pl.N) {
     case 4: return launch_std_n<4>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
     case 6: return launch_std_n<6>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);

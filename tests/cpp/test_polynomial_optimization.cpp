@@ -173,6 +173,17 @@ void checkCost(const Segment::Vector& segs, int r, double cost) {
   EXPECT_LE(std::fabs(num - cost), 0.1 * std::fabs(num));
 }
 
+// getMaximumMagnitude (test_utils.h:43-54): the sampled maximum of |p^(k)|,
+// dt = 0.01.
+double getMaximumMagnitude(const Trajectory& trajectory, int derivative, double dt = 0.01) {
+  double maximum = -1e9;
+  for (double ts = 0; ts < trajectory.getMaxTime(); ts += dt) {
+    const double v = trajectory.evaluate(ts, derivative).norm();
+    if (v > maximum) maximum = v;
+  }
+  return maximum;
+}
+
 struct Fixture {
   int D, r, S;
   unsigned seed;
@@ -352,6 +363,31 @@ void runFixture(const Fixture& f) {
 
 TEST(gpu, ReferenceFixturesN10) {
   for (const Fixture& f : kFixtures) runFixture<10>(f);
+}
+
+// test_polynomial_optimization.cpp:270-305 (UnconstrainedLinearEstimateSegmentTimes)
+// on every OptimizationParams instance: with estimateSegmentTimes' times the
+// solution's sampled maximum speed and acceleration stay below 2.5 times the
+// limits the times were estimated for, and checkPath / checkCost hold.
+TEST(gpu, UnconstrainedLinearEstimateSegmentTimes) {
+  for (const Fixture& f : kFixtures) {
+    const Vertex::Vector vs = fixtureVertices(f, 10);
+    const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
+    PolynomialOptimization<10> opt(f.D);
+    opt.setupFromVertices(vs, times, f.r);
+    EXPECT_TRUE(opt.solveLinear());
+    Segment::Vector segs;
+    opt.getSegments(&segs);
+    Trajectory traj;
+    opt.getTrajectory(&traj);
+    checkPath(vs, segs, 10);
+    const double v_max_traj = getMaximumMagnitude(traj, derivative_order::VELOCITY);
+    const double a_max_traj = getMaximumMagnitude(traj, derivative_order::ACCELERATION);
+    EXPECT_LE(v_max_traj, f.vmax * 2.5);
+    EXPECT_LE(a_max_traj, f.amax * 2.5);
+    EXPECT_TRUE(v_max_traj < f.vmax * 2.5 && a_max_traj < f.amax * 2.5);  // EXPECT_LT
+    checkCost(segs, f.r, opt.computeCost());
+  }
 }
 
 TEST(gpu, OtherOrders) {
@@ -1105,6 +1141,22 @@ TEST(host, SegmentMagnitudeCandidates) {
   EXPECT_TRUE(!s.selectMinMaxMagnitudeFromCandidates(1, 1.0, 0.0, {0, 1}, {}, &mn, &mx));
 }
 
+// test_polynomial.cpp:68-79 (PolynomialTest.Convolution): the product of
+// 1 + 2t and -1 + 3t, coefficient by coefficient.
+TEST(host, PolynomialConvolution) {
+  VectorXd c1(2), c2(2);
+  c1[0] = 1.0;
+  c1[1] = 2.0;
+  c2[0] = -1.0;
+  c2[1] = 3.0;
+  const Polynomial p(c1), q(c2);
+  const Polynomial conv = p * q;
+  const VectorXd got = conv.getCoefficients();
+  const double want[3] = {c1[0] * c2[0], c1[0] * c2[1] + c1[1] * c2[0], c1[1] * c2[1]};
+  EXPECT_TRUE(got.size() == 3);
+  for (int k = 0; k < 3 && k < got.size(); ++k) EXPECT_TRUE(got[k] == want[k]);
+}
+
 // Trajectory container operations (trajectory.cpp:136-251).
 TEST(host, TrajectoryContainers) {
   Segment::Vector segs;
@@ -1475,6 +1527,119 @@ TEST(gpu, DemoCollisionObjective) {
                 with_time ? "collision+time" : "collision", J0, J1, info.n_iterations, res, oJ,
                 oev);
   }
+}
+
+// getAllTrajectories (polynomial_optimization_nonlinear.h:316-331): one
+// trajectory per evaluation of the collision objective (nonlinear_impl:1244),
+// in order, accumulating over optimize() calls as the reference's
+// all_trajectories_ does.  The first is the start (the tube QCQP solution),
+// the result is one of them (the device optimiser keeps the best evaluated
+// point), and the initial trajectories match the start.
+TEST(gpu, AllTrajectoriesHistory) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> times = estimateSegmentTimesNfabian(vs, 2.0, 2.0, 6.5);
+  const std::vector<std::pair<double, double>> radii(4, {0.15, 0.15});
+  int nx, ny, nz;
+  const std::vector<float> occ = demoForest(&nx, &ny, &nz);
+  PolynomialOptimizationNonLinear<10> opt(3, demoParameters());
+  EXPECT_TRUE(opt.setupFromVertices(vs, times, radii, 4));
+  opt.setOccupancyGrid(occ, nx, ny, nz);
+  std::vector<Trajectory> none;
+  opt.getAllTrajectories(&none);
+  EXPECT_TRUE(none.empty());
+  opt.optimize();
+  const int n1 = opt.getOptimizationInfo().n_iterations;
+  std::vector<Trajectory> hist;
+  opt.getAllTrajectories(&hist);
+  EXPECT_TRUE(static_cast<int>(hist.size()) == n1 && n1 >= 2);
+  Trajectory init, init_rp, result;
+  opt.getInitialSolutionTrajectory(&init);
+  opt.getInitialTrajectoryAfterRemovingPos(&init_rp);
+  opt.getTrajectory(&result);
+  auto coeffDiff = [](const Trajectory& a, const Trajectory& b) {
+    Segment::Vector sa, sb;
+    a.getSegments(&sa);
+    b.getSegments(&sb);
+    if (sa.size() != sb.size()) return 1e300;
+    const std::vector<double> ca = coeffsOf(sa, 10), cb = coeffsOf(sb, 10);
+    double tdiff = 0.0;
+    for (size_t s = 0; s < sa.size(); ++s) tdiff += std::fabs(sa[s].getTime() - sb[s].getTime());
+    return relErr(ca, cb) + tdiff;
+  };
+  EXPECT_LE(coeffDiff(init_rp, init), 0.0);
+  if (!hist.empty()) EXPECT_LE(coeffDiff(hist.front(), init), 1e-9);
+  double best = 1e300;
+  for (const Trajectory& t : hist) best = std::min(best, coeffDiff(t, result));
+  EXPECT_LE(best, 1e-9);
+  // Free derivatives as x, y, z triples: the tube problem's d_p, per index.
+  std::vector<Vector3d> f3;
+  opt.getFreeConstraints(&f3);
+  std::vector<VectorXd> fx;
+  opt.getConstrainedOptimizationRef().getFreeConstraints(&fx);
+  EXPECT_TRUE(fx.size() == 3 && f3.size() == static_cast<size_t>(fx[0].size()));
+  for (size_t i = 0; i < f3.size() && fx.size() == 3; ++i)
+    EXPECT_TRUE(f3[i].x() == fx[0][static_cast<long>(i)] &&
+                f3[i].y() == fx[1][static_cast<long>(i)] &&
+                f3[i].z() == fx[2][static_cast<long>(i)]);
+  // A second run appends its evaluations.
+  opt.optimize();
+  const int n2 = opt.getOptimizationInfo().n_iterations;
+  std::vector<Trajectory> hist2;
+  opt.getAllTrajectories(&hist2);
+  EXPECT_TRUE(static_cast<int>(hist2.size()) == n1 + n2);
+  std::printf("  history: %d + %d evaluations\n", n1, n2);
+}
+
+// computeInitialSolutionWithPositionConstraints (nonlinear_impl:199-272) and
+// the declared WithoutPositionConstraints: the QCQP solution becomes the
+// initial trajectory and its d_p (intermediate positions free) the problem's
+// free constraints.
+TEST(gpu, ComputeInitialSolution) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> times = estimateSegmentTimesNfabian(vs, 2.0, 2.0, 6.5);
+  const std::vector<std::pair<double, double>> radii(4, {0.15, 0.15});
+  PolynomialOptimizationConstrained<10> qp(3);
+  qp.setupFromVertices(vs, times, radii, 4);
+  EXPECT_TRUE(qp.solveQCQP() == 0);
+  std::vector<VectorXd> want;
+  qp.getFreeConstraints(&want);
+  for (int variant = 0; variant < 2; ++variant) {
+    PolynomialOptimizationNonLinear<10> opt(3, demoParameters());
+    EXPECT_TRUE(opt.setupFromVertices(vs, times, radii, 4));
+    EXPECT_TRUE(variant ? opt.computeInitialSolutionWithoutPositionConstraints()
+                        : opt.computeInitialSolutionWithPositionConstraints());
+    std::vector<VectorXd> got;
+    opt.getConstrainedOptimizationRef().getFreeConstraints(&got);
+    EXPECT_TRUE(got.size() == want.size());
+    for (size_t d = 0; d < got.size() && d < want.size(); ++d)
+      EXPECT_LE(relErr(std::vector<double>(got[d].data(), got[d].data() + got[d].size()),
+                       std::vector<double>(want[d].data(), want[d].data() + want[d].size())),
+                1e-12);
+    Trajectory init;
+    opt.getInitialSolutionTrajectory(&init);
+    Segment::Vector segs;
+    qp.getSegments(&segs);
+    Segment::Vector isegs;
+    init.getSegments(&isegs);
+    EXPECT_LE(relErr(coeffsOf(isegs, 10), coeffsOf(segs, 10)), 1e-12);
+  }
+}
+
+// setFreeEndpointDerivativeHardConstraints (nonlinear_impl:2858-2905) writes
+// through .at(): a position-magnitude constraint with
+// solve_with_position_constraint wraps (derivative - 1) and throws
+// std::out_of_range instead of writing out of bounds.
+TEST(gpu, EndpointBoundsRejectPositionMagnitude) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> times = estimateSegmentTimesNfabian(vs, 2.0, 2.0, 6.5);
+  const std::vector<std::pair<double, double>> radii(4, {0.15, 0.15});
+  int nx, ny, nz;
+  const std::vector<float> occ = demoForest(&nx, &ny, &nz);
+  PolynomialOptimizationNonLinear<10> opt(3, demoParameters());
+  EXPECT_TRUE(opt.setupFromVertices(vs, times, radii, 4));
+  opt.setOccupancyGrid(occ, nx, ny, nz);
+  opt.addMaximumMagnitudeConstraint(derivative_order::POSITION, 20.0);
+  EXPECT_THROW(opt.optimize());
 }
 
 int main(int argc, char** argv) {

@@ -47,7 +47,7 @@ def test_lane_kernels_match_wavefront_kernel(ctx, dev, oracle, kernel, S):
         assert rel_err(out["cost"][b], o["cost"]) <= REL_TOL, b
 
 
-@pytest.mark.parametrize("kernel", ["lane", "lane_pair"])
+@pytest.mark.parametrize("kernel", ["lane", "lane_pair", "standard", "generic"])
 def test_lane_kernels_bad_time(ctx, dev, kernel):
     import mav_tube_trajectory_generation_amd as mtg
     S, B = 5, 70
@@ -61,8 +61,12 @@ def test_lane_kernels_bad_time(ctx, dev, kernel):
         if b in bad:
             assert out["status"][b] == 1 and np.isnan(out["cost"][b])
             assert np.isnan(out["coeffs"][b]).all()
+            # every kernel reports a bad time's free values as NaN (the same
+            # answer whatever kernel AUTO picks for the batch size)
+            assert np.isnan(out["free"][b]).all()
         else:
             assert out["status"][b] == 0 and np.isfinite(out["cost"][b])
+            assert np.isfinite(out["free"][b]).all()
 
 
 def test_auto_selection_by_batch(ctx):

@@ -109,13 +109,16 @@ def test_ipm_matches_scipy(oracle, case):
     # IPM stops at mu <= tol = 1e-10 (its complementarity target is kept at
     # >= 1e-2 x the infeasibility, so mu does not run to 1e-20): the ~100
     # inactive constraints (slack ~0.05) keep lambda ~ mu / s ~ 1e-9 each,
-    # which the active-set NNLS leaves out, hence 1e-7.
+    # which the active-set NNLS leaves out.  The bound is per case, each about
+    # 5x the measured residual: main_cpp (6 active constraints) 1.1e-9,
+    # random5 (16 active, more inactive multipliers left out) 2.3e-8.
     from scipy.optimize import nnls
     x = sol["x"]
     act = g > -1e-6
     Jg = (np.einsum("kij,j->ki", Qk, x) + lk)[act]
     _, resid = nnls(Jg.T, -(P @ x + q))
-    assert resid <= 1e-7 * max(1.0, np.linalg.norm(P @ x + q))
+    bound = {"main_cpp": 5e-9, "random5": 1e-7}[case]
+    assert resid <= bound * max(1.0, np.linalg.norm(P @ x + q))
 
 
 def test_tube_time_objective_oracle(oracle):

@@ -30,13 +30,15 @@ def main():
     fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
     out = plan.solve(fd, td)
     L = mtg.lib()
-    L.mtg_debug_stamps_std.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    # STAMPS_SYM=wave: the compile-time-S kernel (mtg_linear_wave.hip)
+    fn = getattr(L, "mtg_debug_stamps_" + os.environ.get("STAMPS_SYM", "std"))
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     runs = []
     for _ in range(7):
         plan.solve(fd, td, out=out)
         torch.cuda.synchronize()
         st = (ctypes.c_ulonglong * 512)()
-        L.mtg_debug_stamps_std(st, 512)
+        fn(st, 512)
         runs.append(np.array(st[:], dtype=np.int64))
     st = np.median(np.array(runs), axis=0)
     order = [(0, "start"), (7, "times arrived, powers"), (1, "fixed stored"),
@@ -55,6 +57,8 @@ def main():
     print(f"phase cycles (workgroup 0, median of 7, B={B}):")
     prev = st[0]
     for slot, name in order[1:]:
+        if st[slot] == 0:  # slot not stamped by this kernel
+            continue
         print(f"  {name:>24}: {st[slot] - prev:8.0f}")
         prev = st[slot]
     print(f"  total: {st[6] - st[0]:.0f} cycles")
