@@ -58,7 +58,8 @@ struct Geo {
   // LDS carve-up (doubles).
   static constexpr int L_DV = 0;                          // (S+1) x D x MP vertex derivatives
   static constexpr int L_SL = L_DV + (S + 1) * D * MP;    // 2 x NSL slots
-  static constexpr int L_N = L_SL + 2 * NSL * SLOT;
+  static constexpr int L_JUNK = L_SL + 2 * NSL * SLOT;  // stores nobody reads
+  static constexpr int L_N = L_JUNK + 16;
   static_assert(MF == 4, "4 x 4 blocks (block2_solve)");
   static_assert(NROW <= kWave && S * D <= kWave && 2 * 4 * (MF + D) <= kWave,
                 "one pass of the wave per phase");
@@ -146,8 +147,10 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
 
   // ---- inputs, all issued before the first use: fixed values, the times
   // each role needs, the assembly rows k and M+k of H(1).
-  const int row = lane < G::NROW ? lane : G::NROW - 1;  // assembly lane (v, i)
-  const int av = row / MF + 1, ai = row % MF;
+  // Assembly lane (v, i); lanes past the last row repeat vertex S-1's rows
+  // (same row i = lane % MF, which the end-term lanes below also use).
+  const int ai = lane % MF;
+  const int av = lane / MF + 1 < S - 1 ? lane / MF + 1 : S - 1;
   const int sd = lane < S * D ? lane : S * D - 1;       // coefficient lane (s, d)
   const int cs = sd / D, cd = sd - cs * D;
   const int ee = (lane / (D * MF)) & 1;                 // end-term lane (e, d, i)
@@ -155,6 +158,21 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   double f1 = 0.0;
   if constexpr (D * NFIX > kWave) f1 = fb[lane + kWave < D * NFIX ? lane + kWave : D * NFIX - 1];
   const double tl = tb[av - 1], tr = tb[av], ts = tb[cs], te = tb[ee ? S - 1 : 0];
+  // The assembly's operands straight from HBM / L2 (not through the LDS
+  // vertex table, which the fixed-value stores fill): positions p_(v-1),
+  // p_v, p_(v+1) of the row lane's vertex (d_f index 0 for vertex 0,
+  // M + w - 1 for w >= 1), and the end lane's end-vertex derivatives 1..M-1.
+  const int ed = (lane / MF) % D;
+  double pos[3][D], endd[M - 1];
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    const int vw = av - 1 + w;
+    const int fi = vw == 0 ? 0 : M + vw - 1;
+#pragma unroll
+    for (int d = 0; d < D; ++d) pos[w][d] = fb[d * NFIX + fi];
+  }
+#pragma unroll
+  for (int l = 1; l < M; ++l) endd[l - 1] = fb[ed * NFIX + (ee ? M + S - 1 : 0) + l];
   double hk[N], hMk[N];
   {
     const int k = ai + 1;
@@ -213,7 +231,7 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   auto slot_of = [&](int v) {  // v <= MID: forward slot v-1; else backward S-1-v
     return slots + (v <= MID ? v - 1 : NSL + S - 1 - v) * SLOT;
   };
-  if (lane < G::NROW) {
+  {
     double ql[M], qr[M];
     row_powers<M, R>(tl, i1, i2, i3, ql);
     row_powers<M, R>(tr, i1, i2, i3, qr);
@@ -229,9 +247,9 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     double* sl = slot_of(av);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      double s = cpos * dv[(av * D + d) * MP];
-      s = fma(cprev, dv[((av - 1) * D + d) * MP], s);
-      s = fma(cnext, dv[((av + 1) * D + d) * MP], s);
+      double s = cpos * pos[1][d];
+      s = fma(cprev, pos[0][d], s);
+      s = fma(cnext, pos[2][d], s);
       sl[O_R + d * MF + ai] = -s;
     }
     // lower triangle of row i (entries j > i go to the slot's Z area,
@@ -239,27 +257,27 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     const int rbase = O_S + tri(ai, 0);
 #pragma unroll
     for (int j = 0; j < MF; ++j) sl[j <= ai ? rbase + j : O_Z + 4 * ai + j] = Ar[j];
-    if (av < MID) {
-      // forward step at v: P = C_v, P^T by rows = C_v by columns
+    // forward step at v (v < MID): P = C_v, P^T by rows = C_v by columns;
+    // backward step at v+1 (MID <= v <= S-2): P = C_v^T, P^T = C_v by rows.
+    // The store a lane does not need goes to the junk area.
+    double* junk = sm + G::L_JUNK;
+    double* pf = av < MID ? sl + O_P + ai : junk;
+    double* pb = (av >= MID && av < S - 1) ? slot_of(av + 1) + O_P + ai * MF : junk + 8;
 #pragma unroll
-      for (int j = 0; j < MF; ++j) sl[O_P + j * MF + ai] = Cr[j];
-    } else if (av < S - 1) {
-      // backward step at v+1: P = C_v^T, P^T = C_v by rows
-      lds_st(slot_of(av + 1) + O_P + ai * MF, Cr);
-    }
+    for (int j = 0; j < MF; ++j) pf[j * MF] = Cr[j];
+    lds_st(pb, Cr);
   }
   lds_order();
   // The fully fixed end vertices' part of b_1 (segment 0) and b_(S-1)
   // (segment S-1): lane (e, d, i) adds -sum_l H_seg(k, l) d_f(l) for its row.
-  if (lane < 2 * D * MF) {
-    const int d = (lane / MF) % D;
+  {
     double q[M];
     row_powers<M, R>(te, i1, i2, i3, q);
-    const double* dd = dv + ((ee ? S : 0) * D + d) * MP;
     double s = 0.0;
 #pragma unroll
-    for (int l = 1; l < M; ++l) s = fma((ee ? hk[M + l] : hMk[l]) * q[l], dd[l], s);
-    atomicAdd(slot_of(ee ? S - 1 : 1) + O_R + d * MF + ai, -s);
+    for (int l = 1; l < M; ++l) s = fma((ee ? hk[M + l] : hMk[l]) * q[l], endd[l - 1], s);
+    // lanes past the 2 D MF end lanes repeat one and add nothing
+    atomicAdd(slot_of(ee ? S - 1 : 1) + O_R + ed * MF + ai, lane < 2 * D * MF ? -s : 0.0);
   }
   lds_order();
   MTG_STAMP(2);
@@ -271,19 +289,27 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   // right-hand side), x into slot k (Z column j, or z in place of r).
   double pmin = 1.0;
   const int g = lane >> 5, q = lane & 31, jj = q >> 2, ii = q & 3;
-  const bool colj = jj < MF;
   {
-    const bool act = jj < MF + D;
-    const int dd = jj - MF;
+    // lanes past the MF + D columns repeat column 0 (same values, same
+    // addresses), so the sweep needs no execution mask
+    const int jc = jj < MF + D ? jj : 0;
+    const bool colj = jc < MF;
+    const int dd = jc - MF;
     double* base = slots + g * NSL * SLOT;
-    const double* Up = base + (colj ? O_P + jj * MF : O_R + dd * MF);
+    const double* Up = base + (colj ? O_P + jc * MF : O_R + dd * MF);
     const double* Pp = base + O_P + ii * MF;
-    const int aoff = colj ? O_S + (ii >= jj ? tri(ii, jj) : tri(jj, ii)) : O_R + dd * MF + ii;
+    // a: entry (i, j) of the next Schur block (stored lower: (max, min)) or
+    // b_next[d][i]; out goes to the same place, column lanes above the
+    // diagonal to the next slot's Z area (their values duplicate (j, i)).
+    const int mx = ii > jc ? ii : jc, mn = ii > jc ? jc : ii;
+    const int lowr = O_S + ((mx * (mx + 1)) >> 1) + mn;
+    const int aoff = colj ? lowr : O_R + dd * MF + ii;
+    const int ooff = colj ? (ii >= jc ? lowr : O_Z + 4 * jc + ii) : aoff;
     const double* Ap = base + SLOT + aoff;
-    double* Xp = base + (colj ? O_Z + jj * MF : O_R + dd * MF);
-    double* Op = base + SLOT + (colj ? (ii >= jj ? O_S + tri(ii, jj) : O_Z + q) : aoff);
+    double* Xp = base + (colj ? O_Z + jc * MF : O_R + dd * MF);
+    double* Op = base + SLOT + ooff;
     const int nst = g ? NBW : NFW;
-    if (act && NK > 0) {
+    if (NK > 0) {
       double pc[MF], a;
       lds_ld(Pp, pc);
       a = Ap[0];
@@ -369,7 +395,8 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     xi = ii == 1 ? x[1] : xi;
     xi = ii == 2 ? x[2] : xi;
     xi = ii == 3 ? x[3] : xi;
-    if (p_act && g == 0) dv[(MID * D + d) * MP + 1 + ii] = xi;
+    double* junk = sm + G::L_JUNK;
+    *(p_act && g == 0 ? dv + (MID * D + d) * MP + 1 + ii : junk + ii) = xi;
 #pragma unroll
     for (int t = 0; t < NK; ++t) {
       if (NFW == NBW || t < nst) {
@@ -381,7 +408,7 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
         xi = fma(-zr[t][3], xb3, s2);
         const int sidx = NFW == NBW ? NK - 1 - t : nst - 1 - t;
         const int v = g ? S - 1 - sidx : 1 + sidx;
-        if (p_act) dv[(v * D + d) * MP + 1 + ii] = xi;
+        *(p_act ? dv + (v * D + d) * MP + 1 + ii : junk + 4 + ii) = xi;
       }
     }
   }

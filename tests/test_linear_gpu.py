@@ -368,6 +368,45 @@ def test_standard_kernel_matches_generic(ctx, dev, oracle, N, D, S):
     assert np.median(worse) <= 10.0, np.median(worse)
 
 
+@pytest.mark.parametrize("N,D,S,kernels", [
+    (10, 3, 2, ("standard",)), (10, 3, 3, ("standard", "lane", "lane_pair")),
+    (10, 3, 5, ("standard", "lane", "lane_pair")), (10, 3, 6, ("standard", "lane", "lane_pair")),
+    (10, 3, 9, ("standard", "lane", "lane_pair")), (10, 3, 10, ("standard", "lane", "lane_pair")),
+    (10, 3, 16, ("standard",)), (10, 3, 20, ("standard",)), (10, 2, 10, ("standard",)),
+    (8, 3, 7, ("standard",)), (10, 1, 4, ("standard",))])
+def test_standard_kernels_nonzero_end_derivatives(ctx, dev, oracle, N, D, S, kernels):
+    """The standard pattern with moving end vertices: random non-zero
+    derivatives 1..N/2-1 at the start and end vertex (createRandomVertices
+    fixes them to zero, so the fixtures never exercise the end vertices'
+    share of b, linear_impl:306-379).  Every kernel that runs the pattern —
+    the compile-time-S wave kernel (N = 10, D = 3, S <= 16), the runtime-S
+    kernel, the lane kernels — against the oracle, 1e-6."""
+    M = N // 2
+    r = M - 1
+    B = 8
+    rng = np.random.default_rng(4242 + S)
+    dfs, ts, refs = [], [], []
+    mask = None
+    for b in range(B):
+        v = standard_vertices(N, S, D, 7000 + S + b)
+        v.vals[0, 1:M, :] = rng.uniform(-2.0, 2.0, (M - 1, D))
+        v.vals[S, 1:M, :] = rng.uniform(-2.0, 2.0, (M - 1, D))
+        m, df = compact_fixed(v, N)
+        mask = m
+        t = oracle.estimate_segment_times(v, 3.0, 5.0)
+        dfs.append(df)
+        ts.append(t)
+        refs.append(oracle.linear_solve(N, r, v, t))
+    df_b, t_b = np.array(dfs), np.array(ts)
+    for kernel in kernels:
+        plan, out = _solve_gpu(ctx, dev, N, r, mask, df_b, t_b, kernel)
+        assert plan.kernel == kernel
+        assert (out["status"] == 0).all(), kernel
+        for b in range(B):
+            assert rel_err_coeffs(out["coeffs"][b], refs[b]["coeffs"]) <= REL_TOL, (kernel, b)
+            assert rel_err(out["cost"][b], refs[b]["cost"]) <= REL_TOL, (kernel, b)
+
+
 def test_kernel_selection(ctx):
     """AUTO picks the standard-pattern kernel exactly on the standard
     pattern; STANDARD is refused elsewhere."""
