@@ -236,14 +236,36 @@ def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None):
     return out
 
 
-def load_pmc_traffic(workload, config_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass, if any."""
+def device_kernel(wl, plan, B, N, D, r, S):
+    """rocprofv3 name (substring) of the launch's dominant kernel: the key,
+    with the workload / batch / segments, of its committed counter passes."""
+    if wl == "linear":
+        k = plan.kernel_for_batch(B)
+        if k == "standard":
+            return ("linear_wave_kernel" if (N, r, D) == (10, 4, 3) and 2 <= S <= 16 else
+                    "linear_std_kernel")
+        return {"lane": "linear_lane_kernel", "lane_pair": "linear_lane2_kernel",
+                "generic": "linear_solve_kernel"}[k]
+    if wl == "extrema":
+        return "soft_cost_kernel" if B < 4096 else "max_magnitude_kernel"
+    return {"time": "time_optimize_std_kernel", "tube": "tube_solve_kernel",
+            "time-qcqp": "tube_solve_kernel", "sample": "sample_kernel",
+            "collision": "coll_walk_kernel"}[wl]
+
+
+def load_pmc_traffic(key, kernel_ms):
+    """HBM bytes per launch of this workload's kernel from the committed
+    rocprofv3 PMC passes (profiles/pmc_traffic.json, keyed
+    workload:batch:segments:kernel), or None.  An entry whose kernel time
+    differs from this run's by more than 15 % was measured on another build
+    and is not used."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            data = json.load(f)
-        for entry in data.values():  # keyed by profile tag; matched by config
-            if entry.get("config") == config_key:
+            entry = json.load(f).get(key)
+        if entry and entry.get("avg_ns"):
+            ratio = entry["avg_ns"] * 1e-6 / kernel_ms
+            if 0.85 <= ratio <= 1.15:
                 return entry.get("bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -750,8 +772,9 @@ def main():
     value = total_units / elapsed
     alg_bytes = bytes_per_traj * B
     gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    config_key = f"{wl}:B{B}:S{S}"
-    traffic = load_pmc_traffic(wl, config_key)
+    config_key = f"{wl}:B{B}:S{S}" + (":soft" if getattr(args, "soft", False) else "")
+    dev_kernel = device_kernel(wl, plan, B, N, D, r, S)
+    traffic = load_pmc_traffic(f"{config_key}:{dev_kernel}", kernel_ms)
     timing = ("HIP events around one graph replay of the K steps, / K" if use_graph else
               "HIP event pair per step, mean") + graph_note
     hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
@@ -766,13 +789,12 @@ def main():
         roof = {"bound": "hbm", **{k: hbm[k] for k in ("achieved", "peak", "unit", "frac")},
                 "traffic": traffic, "alg_bytes_per_launch": alg_bytes}
     roof["kernel_ms"] = kernel_ms
+    roof["kernel"] = dev_kernel
     roof["kernel_timing"] = timing
     # Executed FP64 work beside the dense-equivalent count: the kernel's SQ
     # FP64 instruction counts x active lanes (a committed rocprofv3 pass at
     # this workload, batch and kernel) over this run's kernel time.
-    kname = (plan.kernel_for_batch(B) if wl == "linear" else
-             wl + ("_soft" if getattr(args, "soft", False) else ""))
-    ex_flop, ex_src = load_sq_executed(f"{config_key}:{kname}")
+    ex_flop, ex_src = load_sq_executed(f"{config_key}:{dev_kernel}")
     if ex_flop is not None:
         ex_tf = ex_flop * B / (kernel_ms * 1e-3) / 1e12
         roof["executed"] = {"achieved": ex_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -14,7 +14,7 @@
 //     backward chain's v = S-1 .. MID+1 sit in the slots (chain, step) in
 //     elimination order, each slot holding the vertex's Schur block (packed
 //     lower triangle), the step's coupling P^T by rows, the right-hand sides
-//     (then z) and Z by columns; slot (0, MID-1) is the middle vertex, slot
+//     (then z) and Z by rows; slot (0, MID-1) is the middle vertex, slot
 //     (1, NB) receives the backward chain's terms;
 //   * a step runs on lanes (chain, column j, row i): column lanes j < 4 solve
 //     for column j of the coupling, right-hand-side lanes j = 4 + d for
@@ -53,13 +53,15 @@ struct Geo {
   static constexpr int O_S = 0;                    // Schur block, packed lower triangle
   static constexpr int O_P = (TRI + 1) & ~1;       // P^T by rows (MF x MF)
   static constexpr int O_R = O_P + MF * MF;        // right-hand sides, then z (D x MF)
-  static constexpr int O_Z = O_R + D * MF;         // Z = S^-1 P by columns (MF x MF)
+  static constexpr int O_Z = O_R + D * MF;         // Z = S^-1 P by rows (MF x MF)
   static constexpr int SLOT = O_Z + MF * MF;
   // LDS carve-up (doubles).
   static constexpr int L_DV = 0;                          // (S+1) x D x MP vertex derivatives
   static constexpr int L_SL = L_DV + (S + 1) * D * MP;    // 2 x NSL slots
   static constexpr int L_JUNK = L_SL + 2 * NSL * SLOT;  // stores nobody reads
-  static constexpr int L_N = L_JUNK + 16;
+  static constexpr int L_H = L_JUNK + 16;                // H(1), N x N
+  static constexpr int L_T = L_H + N * N;                // segment times
+  static constexpr int L_N = L_T + ((S + 1) & ~1);
   static_assert(MF == 4, "4 x 4 blocks (block2_solve)");
   static_assert(NROW <= kWave && S * D <= kWave && 2 * 4 * (MF + D) <= kWave,
                 "one pass of the wave per phase");
@@ -145,8 +147,10 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   const double* tb = times + b * S;
   MTG_STAMP(0);
 
-  // ---- inputs, all issued before the first use: fixed values, the times
-  // each role needs, the assembly rows k and M+k of H(1).
+  // ---- inputs.  Each value is loaded from HBM by one lane only (the four
+  // waves of a CU share its L1 / TA path, which per-lane copies of the
+  // same values saturated) and handed out through LDS: fixed values into
+  // the vertex table dv, the times into tt, H(1) into hh.
   // Assembly lane (v, i); lanes past the last row repeat vertex S-1's rows
   // (same row i = lane % MF, which the end-term lanes below also use).
   const int ai = lane % MF;
@@ -154,38 +158,14 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   const int sd = lane < S * D ? lane : S * D - 1;       // coefficient lane (s, d)
   const int cs = sd / D, cd = sd - cs * D;
   const int ee = (lane / (D * MF)) & 1;                 // end-term lane (e, d, i)
+  const int ed = (lane / MF) % D;
+  double* tt = sm + G::L_T;
+  double* hh = sm + G::L_H;
   const double f0 = fb[lane < D * NFIX ? lane : D * NFIX - 1];
   double f1 = 0.0;
   if constexpr (D * NFIX > kWave) f1 = fb[lane + kWave < D * NFIX ? lane + kWave : D * NFIX - 1];
-  const double tl = tb[av - 1], tr = tb[av], ts = tb[cs], te = tb[ee ? S - 1 : 0];
-  // The assembly's operands straight from HBM / L2 (not through the LDS
-  // vertex table, which the fixed-value stores fill): positions p_(v-1),
-  // p_v, p_(v+1) of the row lane's vertex (d_f index 0 for vertex 0,
-  // M + w - 1 for w >= 1), and the end lane's end-vertex derivatives 1..M-1.
-  const int ed = (lane / MF) % D;
-  double pos[3][D], endd[M - 1];
-#pragma unroll
-  for (int w = 0; w < 3; ++w) {
-    const int vw = av - 1 + w;
-    const int fi = vw == 0 ? 0 : M + vw - 1;
-#pragma unroll
-    for (int d = 0; d < D; ++d) pos[w][d] = fb[d * NFIX + fi];
-  }
-#pragma unroll
-  for (int l = 1; l < M; ++l) endd[l - 1] = fb[ed * NFIX + (ee ? M + S - 1 : 0) + l];
-  double hk[N], hMk[N];
-  {
-    const int k = ai + 1;
-#pragma unroll
-    for (int j = 0; j < N; j += 2) {
-      const double2 x = *reinterpret_cast<const double2*>(tab + k * N + j);
-      const double2 y = *reinterpret_cast<const double2*>(tab + (M + k) * N + j);
-      hk[j] = x.x;
-      hk[j + 1] = x.y;
-      hMk[j] = y.x;
-      hMk[j + 1] = y.y;
-    }
-  }
+  const double t_own = tb[lane < S ? lane : S - 1];
+  const double2 h_own = *reinterpret_cast<const double2*>(tab + 2 * (lane < N * N / 2 ? lane : 0));
 
   // Fixed value i of d_f (D x NFIX, the standard order of linear_impl:171-252:
   // vertex 0 derivatives 0..M-1, intermediate positions, vertex S
@@ -202,6 +182,8 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   if (lane < D * NFIX) put_fixed(lane, f0);
   if constexpr (D * NFIX > kWave)
     if (lane + kWave < D * NFIX) put_fixed(lane + kWave, f1);
+  if (lane < S) tt[lane] = t_own;
+  if (lane < N * N / 2) *reinterpret_cast<double2*>(hh + 2 * lane) = h_own;
   // The backward chain's terminal slot starts at zero (its last step stores
   // 0 - P^T x there: the backward terms of the middle vertex).
   {
@@ -209,8 +191,25 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     if (lane < G::TRI) term[O_S + lane] = 0.0;
     if (lane < D * MF) term[O_R + lane] = 0.0;
   }
-  const bool bad_l = !(tl > 0.0) || !(tl < 1e300) || !(tr > 0.0) || !(tr < 1e300) ||
-                     !(ts > 0.0) || !(ts < 1e300);
+  lds_order();
+  // Every role's operands from LDS: the times, the rows k and M+k of H(1),
+  // the positions p_(v-1), p_v, p_(v+1) of the row lane's vertex and the end
+  // lane's end-vertex derivatives 1..M-1.
+  const double tl = tt[av - 1], tr = tt[av], ts = tt[cs], te = tt[ee ? S - 1 : 0];
+  double hk[N], hMk[N];
+  lds_ld(hh + (ai + 1) * N, hk);
+  lds_ld(hh + (M + ai + 1) * N, hMk);
+  double pos[3][D], endd[M - 1];
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int d = 0; d < D; ++d) pos[w][d] = dv[((av - 1 + w) * D + d) * MP];
+  {
+    const double* de = dv + ((ee ? S : 0) * D + ed) * MP;
+#pragma unroll
+    for (int l = 1; l < M; ++l) endd[l - 1] = de[l];
+  }
+  const bool bad_l = lane < S && (!(t_own > 0.0) || !(t_own < 1e300));
   const bool bad = __any(bad_l);
   MTG_STAMP(7);
   constexpr int64_t per = static_cast<int64_t>(S) * D * N;
@@ -306,7 +305,8 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     const int aoff = colj ? lowr : O_R + dd * MF + ii;
     const int ooff = colj ? (ii >= jc ? lowr : O_Z + 4 * jc + ii) : aoff;
     const double* Ap = base + SLOT + aoff;
-    double* Xp = base + (colj ? O_Z + jc * MF : O_R + dd * MF);
+    // x_i into Z (row-major: Z[i][j]) or z[d][i]
+    double* Xp = base + (colj ? O_Z + ii * MF + jc : O_R + dd * MF + ii);
     double* Op = base + SLOT + ooff;
     const int nst = g ? NBW : NFW;
     if (NK > 0) {
@@ -338,7 +338,11 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
           o = fma(-pc[3], x[3], o);
           o = fma(-pc[0], x[0], o);
           o = fma(-pc[1], x[1], o);
-          lds_st(Xp + k * SLOT, x);
+          // x is the same in the four row lanes: each stores its row's entry
+          double xi = i1 ? x[1] : x[0];
+          xi = i2 ? x[2] : xi;
+          xi = i3 ? x[3] : xi;
+          Xp[k * SLOT] = xi;
           Op[k * SLOT] = o;
           lds_order();
           if (k + 1 < NK) {
@@ -381,14 +385,13 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     const int nst = g ? NBW : NFW;
     const int dc = p_act ? d : 0;
     const double* zb = slots + g * NSL * SLOT + O_R + dc * MF + ii;
-    const double* Zb = slots + g * NSL * SLOT + O_Z + ii;
+    const double* Zb = slots + g * NSL * SLOT + O_Z + ii * MF;  // row i of Z
     double zz[NK > 0 ? NK : 1], zr[NK > 0 ? NK : 1][MF];
 #pragma unroll
     for (int t = 0; t < NK; ++t) {
       const int sidx = NFW == NBW ? NK - 1 - t : (nst - 1 - t > 0 ? nst - 1 - t : 0);
       zz[t] = zb[sidx * SLOT];
-#pragma unroll
-      for (int c = 0; c < MF; ++c) zr[t][c] = Zb[sidx * SLOT + c * MF];
+      lds_ld(Zb + sidx * SLOT, zr[t]);
     }
     block2_solve(Sv, rr, x, pmin);
     double xi = x[0];
@@ -455,9 +458,24 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     double cc[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) cc[i] = h[i] * tn[i];
+#ifdef MTG_WAVE_SC1_STORES
+    // write-through (sc1) coefficient stores: the lines leave L2 as they are
+    // written instead of in the end-of-kernel writeback
+    {
+      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(coeffs + b * per, 0,
+                                                        static_cast<int>(per * 8), 0x00020000);
+#pragma unroll
+      for (int i = 0; i < N / 2; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u4, make_double2(cc[2 * i], cc[2 * i + 1])), rs,
+            (lane * N + 2 * i) * 8, 0, 16);
+    }
+#else
     double2* o2 = reinterpret_cast<double2*>(coeffs + b * per + static_cast<int64_t>(lane) * N);
 #pragma unroll
     for (int i = 0; i < N / 2; ++i) o2[i] = make_double2(cc[2 * i], cc[2 * i + 1]);
+#endif
     acc = stdp::Solver<N, R, D>::q_form(h) * ipow<1 - 2 * R>(ts, inv);
   }
   const double J = wave_sum_dpp(acc);

@@ -1,10 +1,12 @@
 """Summarise a tools/profile.sh run into profiles/.
 
-python tools/pmc_summary.py <tag> <workload> <config_key> <kernel-substring>
+python tools/pmc_summary.py <tag> <config_key> <kernel-substring>
 
-Writes profiles/r01_<tag>_kernel_stats.csv (rocprofv3 --stats), and merges
-{workload: {config, kernel, avg_ns, fetch_kb, write_kb, bytes_per_launch}}
-into profiles/pmc_traffic.json.  HBM bytes per launch follow
+Writes profiles/<ROUND>_<tag>_kernel_stats.csv (rocprofv3 --stats), and merges
+{"<config_key>:<kernel>": {config, kernel, avg_ns, fetch_kb, write_kb,
+bytes_per_launch}} into profiles/pmc_traffic.json (bench.py reads the entry
+of its own workload, batch, segments and kernel, and only if its avg_ns is
+within 15 % of the run's kernel time).  HBM bytes per launch follow
 MI355X_MICROARCH.md's HBM section: FETCH_SIZE and WRITE_SIZE (KB) from
 separate --pmc passes, FETCH_SIZE doubled on gfx950.
 """
@@ -28,7 +30,7 @@ def counter(path, kernel, name):
 
 
 def main():
-    tag, workload, config_key, kernel = sys.argv[1:5]
+    tag, config_key, kernel = sys.argv[1:4]
     rnd = os.environ.get("ROUND", "r01")
     src = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
     prof = os.path.join(REPO, "profiles")
@@ -53,7 +55,7 @@ def main():
     if os.path.exists(path):
         with open(path) as f:
             data = json.load(f)
-    data[workload] = entry
+    data[f"{config_key}:{kernel}"] = entry
     with open(path, "w") as f:
         json.dump(data, f, indent=1)
     print(json.dumps(entry))

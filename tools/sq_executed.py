@@ -3,7 +3,8 @@ outputs into profiles/sq_executed.json (read by bench.py's roofline):
 
     python tools/sq_executed.py <bench config key> <summary json> [...]
 
-key = "<workload>:B<batch>:S<segments>:<kernel>", e.g. linear:B1024:S10:standard.
+key = "<workload>:B<batch>:S<segments>[:soft]:<device kernel>", e.g.
+linear:B1024:S10:linear_wave_kernel (bench.py device_kernel()).
 """
 import json
 import os
