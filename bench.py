@@ -248,7 +248,10 @@ def device_kernel(wl, plan, B, N, D, r, S):
                 "generic": "linear_solve_kernel"}[k]
     if wl == "extrema":
         return "soft_cost_kernel" if B < 4096 else "max_magnitude_kernel"
-    return {"time": "time_optimize_std_kernel", "tube": "tube_solve_kernel",
+    if wl == "time":
+        return ("time_optimize_wave_kernel" if (N, r, D) == (10, 4, 3) and 2 <= S <= 16 else
+                "time_optimize_std_kernel")
+    return {"tube": "tube_solve_kernel",
             "time-qcqp": "tube_solve_kernel", "sample": "sample_kernel",
             "collision": "coll_walk_kernel"}[wl]
 

@@ -9,9 +9,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "mtg_extrema_device.h"
 #include "mtg_std_device.h"
+#include "mtg_wave_device.h"
 
 namespace mtg {
 
@@ -19,6 +21,45 @@ namespace {
 
 template <int N, int R, int D>
 using StdSv = stdp::Solver<N, R, D>;
+
+// The inner solve and computeCost at the times T (LDS) on either solver:
+// stdp::Solver (runtime S) or wave::Solver (compile-time S, the C2 design).
+// Every lane calls; *bad is set (and NaN returned) when a time is invalid;
+// with cbuf the coefficients go there (LDS, soft searches).
+template <int N, int R, int D>
+__device__ __attribute__((always_inline)) double solve_cost(
+    stdp::Solver<N, R, D>& sv, const double* __restrict__ tab, const double* T, double* cbuf,
+    bool reload_rows, bool* bad, bool* not_spd) {
+  __syncthreads();
+  const bool b = sv.powers_from(T);
+  __syncthreads();
+  if (b) {
+    *bad = true;
+    return NAN;
+  }
+  // soft: the H(1) rows are reloaded per evaluation (L2 hits), so they are
+  // not live across the extremum searches.
+  if (reload_rows) sv.load_first_rows(tab);
+  sv.assemble(tab);
+  __syncthreads();
+  *not_spd = sv.solve() || *not_spd;
+  return sv.coeff_cost(cbuf);
+}
+
+template <int N, int R, int D, int S>
+__device__ __attribute__((always_inline)) double solve_cost(
+    wave::Solver<N, R, D, S>& sv, const double* __restrict__ /*tab*/, const double* T,
+    double* cbuf, bool /*reload_rows*/, bool* bad, bool* not_spd) {
+  __syncthreads();
+  const int l = sv.lane;
+  const double t = T[l < S ? l : S - 1];
+  if (__any(l < S && (!(t > 0.0) || !(t < 1e300)))) {
+    *bad = true;
+    return NAN;
+  }
+  *not_spd = sv.solve(T) || *not_spd;
+  return sv.coeff_cost(T, cbuf);
+}
 
 // J(T) = computeCost() + time_penalty (sum T)^2 [+ soft constraints] at the
 // times T (LDS, S values).  Every lane calls it; returns the wave-uniform J
@@ -28,29 +69,17 @@ using StdSv = stdp::Solver<N, R, D>;
 // p.hard_constraints the searches give *viol = max(0, max_c (max_c - limit_c
 // - tolerance)) (evaluateMaximumMagnitudeConstraint, :2687-2733) instead of
 // a cost term.
-template <int N, int R, int D, bool kSoft>
-__device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& sv, const double* __restrict__ tab,
-                                const double* T, const mtg_time_params& p, double* cbuf,
+template <int N, int D, bool kSoft, class SV>
+__device__ __attribute__((always_inline)) double std_objective(SV& sv, const double* __restrict__ tab,
+                                const double* T, int S, const mtg_time_params& p, double* cbuf,
                                 bool* bad, bool* not_spd, double* viol) {
   *viol = 0.0;
   unsigned long long tt = 0;
   MTG_TACC(511, tt);
-  __syncthreads();
-  const bool b = sv.powers_from(T);
-  __syncthreads();
-  if (b) {
-    *bad = true;
-    return NAN;
-  }
-  // kSoft: the H(1) rows are reloaded per evaluation (L2 hits), so they are
-  // not live across the extremum searches.
-  if constexpr (kSoft) sv.load_first_rows(tab);
-  sv.assemble(tab);
-  __syncthreads();
-  *not_spd = sv.solve() || *not_spd;
-  double J = sv.coeff_cost(kSoft ? cbuf : nullptr);
+  double J = solve_cost(sv, tab, T, kSoft ? cbuf : nullptr, kSoft, bad, not_spd);
+  if (*bad) return NAN;
   double tot = 0.0;
-  for (int i = 0; i < sv.S; ++i) tot += T[i];  // nonlinear_impl:2768-2774
+  for (int i = 0; i < S; ++i) tot += T[i];  // nonlinear_impl:2768-2774
   J += tot * tot * p.time_penalty;
   MTG_TACC(450, tt);  // diagnostic: solve + coefficients
   if constexpr (kSoft) {
@@ -63,9 +92,9 @@ __device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& s
       Ks[cc] = p.soft_derivative[cc];
       if (cc < p.n_soft && Ks[cc] < kmin) kmin = Ks[cc];
     }
-    double* scratch = cbuf + sv.S * D * N;
+    double* scratch = cbuf + S * D * N;
     double* maxima = scratch + kMaxSoftConstraints * (N + 1);
-    ext_soft_maxima_wave_k<N>(kmin, cbuf, T, sv.S, D, sv.lane, p.n_soft, Ks, scratch, maxima);
+    ext_soft_maxima_wave_k<N>(kmin, cbuf, T, S, D, sv.lane, p.n_soft, Ks, scratch, maxima);
     double soft = 0.0;
     for (int c = 0; c < p.n_soft; ++c) {
       double lim = 1.0;
@@ -86,11 +115,18 @@ __device__ __attribute__((always_inline)) double std_objective(StdSv<N, R, D>& s
   return J;
 }
 
-// Loads d_f into the solver (all lanes).
+// Loads d_f (and, for wave::Solver, H(1)) into the solver (all lanes).
 template <int N, int R, int D>
-__device__ void std_load_fixed(StdSv<N, R, D>& sv, const double* __restrict__ fb) {
+__device__ void std_load_fixed(StdSv<N, R, D>& sv, const double* __restrict__ /*tab*/,
+                               const double* __restrict__ fb) {
   const int nf = sv.nf;
   for (int i = sv.lane; i < D * nf; i += kWave) sv.put_fixed(i, fb[i]);
+}
+template <int N, int R, int D, int S>
+__device__ void std_load_fixed(wave::Solver<N, R, D, S>& sv, const double* __restrict__ tab,
+                               const double* __restrict__ fb) {
+  sv.load_constants(tab, fb);
+  wave::lds_order();
 }
 
 // Central-difference point gi (0 .. 2S-1) around base times Tb: segment
@@ -116,22 +152,21 @@ size_t time_std_lds_bytes(int N, int S, int D, bool soft) {
               : base;
 }
 
-template <int N, int R, int D, bool kSoft>
-__global__ __launch_bounds__(kWave) void time_cost_std_kernel(
-    int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
-    const double* __restrict__ times, mtg_time_params p, double* __restrict__ cost,
-    double* __restrict__ grad, int32_t* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+// objectiveFunctionTime / getCostAndGradientTime on one trajectory per
+// workgroup (either solver; cbuf: the soft searches' LDS).
+template <int N, int D, bool kSoft, class SV>
+__device__ __attribute__((always_inline)) void time_cost_body(
+    SV& sv, int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    const double* __restrict__ times, const mtg_time_params& p, double* __restrict__ cost,
+    double* __restrict__ grad, int32_t* __restrict__ status, double* cbuf) {
   const int64_t b = blockIdx.x;
-  StdSv<N, R, D> sv;
-  sv.init(S, smem, tab);
   const int lane = sv.lane;
-  double* cbuf = smem + (sv.L.n + 1) / 2 * 2;
+  const int nf = N + S - 1;
   double* T = sv.aux();  // evaluation point
   double* Tb = T + S;    // base times
   double* g = Tb + S;    // gradient
   double* E = g + S;     // 2S segment energies (grad_mode 1)
-  std_load_fixed(sv, fixed_vals + b * D * sv.nf);
+  std_load_fixed(sv, tab, fixed_vals + b * D * nf);
   for (int i = lane; i < S; i += kWave) T[i] = Tb[i] = times[b * S + i];
   const bool fd = grad && p.grad_mode == 2;
   const int nevals = 1 + (fd ? 2 * S : 0);
@@ -140,7 +175,7 @@ __global__ __launch_bounds__(kWave) void time_cost_std_kernel(
   for (int e = 0; e < nevals; ++e) {
     if (e > 0) std_set_fd_point(T, Tb, S, e - 1, p.increment, lane);
     double viol;
-    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd, &viol);
+    const double J = std_objective<N, D, kSoft>(sv, tab, T, S, p, cbuf, &bad, &not_spd, &viol);
     if (e == 0) {
       J0 = J;
       if (bad) break;
@@ -175,30 +210,54 @@ __global__ __launch_bounds__(kWave) void time_cost_std_kernel(
     for (int i = lane; i < S; i += kWave) grad[b * S + i] = bad ? NAN : g[i];
 }
 
+template <int N, int R, int D, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_cost_std_kernel(
+    int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    const double* __restrict__ times, mtg_time_params p, double* __restrict__ cost,
+    double* __restrict__ grad, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  StdSv<N, R, D> sv;
+  sv.init(S, smem, tab);
+  time_cost_body<N, D, kSoft>(sv, S, tab, fixed_vals, times, p, cost, grad, status,
+                              smem + (sv.L.n + 1) / 2 * 2);
+}
+
+// The same on the compile-time-S solver (N = 10, r = 4, D = 3, S = 2..16).
+template <int N, int R, int D, int S, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_cost_wave_kernel(
+    const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    const double* __restrict__ times, mtg_time_params p, double* __restrict__ cost,
+    double* __restrict__ grad, int32_t* __restrict__ status) {
+  using G = wave::Geo<N, R, D, S>;
+  constexpr int CB = kSoft ? S * D * N + kMaxSoftConstraints * (N + 2) : 0;
+  __shared__ __attribute__((aligned(16))) double sm[G::L_N + CB];
+  wave::Solver<N, R, D, S> sv;
+  sv.init(sm);
+  time_cost_body<N, D, kSoft>(sv, S, tab, fixed_vals, times, p, cost, grad, status,
+                              sm + G::L_N);
+}
+
 // Batched segment-time optimisation (optimizeTime, nonlinear_impl:332-397):
 // bounds [0.1, 2 T0]; projected, scaled steepest descent on the grad_mode 2
 // gradient with an expand/backtrack step rule; `max_evals` objective
 // evaluations (NLopt maxeval semantics, nonlinear_impl:101; gradient
 // evaluations are not counted).  A state machine with one objective call
 // site, as time_optimize_kernel.
-template <int N, int R, int D, bool kSoft>
-__global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
-    int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
-    double* __restrict__ times_io, mtg_time_params p, int max_evals,
+template <int N, int D, bool kSoft, class SV>
+__device__ __attribute__((always_inline)) void time_optimize_body(
+    SV& sv, int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    double* __restrict__ times_io, const mtg_time_params& p, int max_evals,
     double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
-    int32_t* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+    int32_t* __restrict__ status, double* cbuf) {
   const int64_t b = blockIdx.x;
-  StdSv<N, R, D> sv;
-  sv.init(S, smem, tab);
   const int lane = sv.lane;
-  double* cbuf = smem + (sv.L.n + 1) / 2 * 2;
+  const int nf = N + S - 1;
   double* T = sv.aux();   // evaluation point
   double* Tcur = T + S;   // accepted times
   double* T0 = Tcur + S;  // initial times (bounds)
   double* g = T0 + S;     // gradient at Tcur
   double* gv = g + S;     // gradient of the violation at Tcur (hard constraints)
-  std_load_fixed(sv, fixed_vals + b * D * sv.nf);
+  std_load_fixed(sv, tab, fixed_vals + b * D * nf);
   for (int i = lane; i < S; i += kWave) T[i] = Tcur[i] = T0[i] = times_io[b * S + i];
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
@@ -209,7 +268,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
   MTG_STAMP(460);
   while (phase != kDone) {
     double viol;
-    const double J = std_objective<N, R, D, kSoft>(sv, tab, T, p, cbuf, &bad, &not_spd, &viol);
+    const double J = std_objective<N, D, kSoft>(sv, tab, T, S, p, cbuf, &bad, &not_spd, &viol);
     ++nsolve;
     if (phase == kBase) {
       f = J;
@@ -280,6 +339,35 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
   }
 }
 
+template <int N, int R, int D, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
+    int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    double* __restrict__ times_io, mtg_time_params p, int max_evals,
+    double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
+    int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  StdSv<N, R, D> sv;
+  sv.init(S, smem, tab);
+  time_optimize_body<N, D, kSoft>(sv, S, tab, fixed_vals, times_io, p, max_evals, cost,
+                                  evals_out, solves_out, status, smem + (sv.L.n + 1) / 2 * 2);
+}
+
+// The same on the compile-time-S solver (N = 10, r = 4, D = 3, S = 2..16).
+template <int N, int R, int D, int S, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_optimize_wave_kernel(
+    const double* __restrict__ tab, const double* __restrict__ fixed_vals,
+    double* __restrict__ times_io, mtg_time_params p, int max_evals,
+    double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
+    int32_t* __restrict__ status) {
+  using G = wave::Geo<N, R, D, S>;
+  constexpr int CB = kSoft ? S * D * N + kMaxSoftConstraints * (N + 2) : 0;
+  __shared__ __attribute__((aligned(16))) double sm[G::L_N + CB];
+  wave::Solver<N, R, D, S> sv;
+  sv.init(sm);
+  time_optimize_body<N, D, kSoft>(sv, S, tab, fixed_vals, times_io, p, max_evals, cost,
+                                  evals_out, solves_out, status, sm + G::L_N);
+}
+
 namespace {
 template <typename K>
 hipError_t prepare_lds_std(K kernel, size_t bytes) {
@@ -331,6 +419,58 @@ hipError_t time_opt_nrd(const PlanDev& pl, int64_t B, const double* df, double* 
   }
   return hipGetLastError();
 }
+template <int S>
+hipError_t time_cost_wave_s(const PlanDev& pl, int64_t B, const double* df, const double* times,
+                            const mtg_time_params& p, double* cost, double* grad,
+                            int32_t* status, hipStream_t st) {
+  if (p.n_soft > 0)
+    hipLaunchKernelGGL((time_cost_wave_kernel<10, 4, 3, S, true>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), 0, st, pl.tab, df, times, p, cost, grad, status);
+  else
+    hipLaunchKernelGGL((time_cost_wave_kernel<10, 4, 3, S, false>),
+                       dim3(static_cast<unsigned>(B)), dim3(kWave), 0, st, pl.tab, df, times, p,
+                       cost, grad, status);
+  return hipGetLastError();
+}
+
+template <int S>
+hipError_t time_opt_wave_s(const PlanDev& pl, int64_t B, const double* df, double* times,
+                           const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
+                           int32_t* solves, int32_t* status, hipStream_t st) {
+  if (p.n_soft > 0)
+    hipLaunchKernelGGL((time_optimize_wave_kernel<10, 4, 3, S, true>),
+                       dim3(static_cast<unsigned>(B)), dim3(kWave), 0, st, pl.tab, df, times, p,
+                       max_evals, cost, evals, solves, status);
+  else
+    hipLaunchKernelGGL((time_optimize_wave_kernel<10, 4, 3, S, false>),
+                       dim3(static_cast<unsigned>(B)), dim3(kWave), 0, st, pl.tab, df, times, p,
+                       max_evals, cost, evals, solves, status);
+  return hipGetLastError();
+}
+
+// The compile-time-S kernels where the C2 kernel exists (MTG_STD_RUNTIME_S=1
+// forces the runtime-S ones, for A/B runs; launch_linear_solve_std reads the
+// same switch).
+bool use_time_wave(const PlanDev& pl) {
+  static const bool forced = [] {
+    const char* e = std::getenv("MTG_STD_RUNTIME_S");
+    return e && e[0] == '1';
+  }();
+  return has_linear_wave(pl) && !forced;
+}
+
+#define MTG_TIME_WAVE_DISPATCH(FN, ...)                                                      \
+  switch (pl.S) {                                                                            \
+    case 2: return FN<2>(__VA_ARGS__);   case 3: return FN<3>(__VA_ARGS__);                   \
+    case 4: return FN<4>(__VA_ARGS__);   case 5: return FN<5>(__VA_ARGS__);                   \
+    case 6: return FN<6>(__VA_ARGS__);   case 7: return FN<7>(__VA_ARGS__);                   \
+    case 8: return FN<8>(__VA_ARGS__);   case 9: return FN<9>(__VA_ARGS__);                   \
+    case 10: return FN<10>(__VA_ARGS__); case 11: return FN<11>(__VA_ARGS__);                 \
+    case 12: return FN<12>(__VA_ARGS__); case 13: return FN<13>(__VA_ARGS__);                 \
+    case 14: return FN<14>(__VA_ARGS__); case 15: return FN<15>(__VA_ARGS__);                 \
+    case 16: return FN<16>(__VA_ARGS__);                                                     \
+    default: return hipErrorInvalidValue;                                                    \
+  }
 }  // namespace
 
 bool has_time_std(const PlanDev& pl) {
@@ -355,6 +495,8 @@ hipError_t launch_time_cost_std(const PlanDev& pl, int64_t B, const double* df,
                                 const double* times, const mtg_time_params& p, double* cost,
                                 double* grad, int32_t* status, hipStream_t st) {
   if (!has_time_std(pl)) return hipErrorInvalidValue;
+  if (use_time_wave(pl))
+    MTG_TIME_WAVE_DISPATCH(time_cost_wave_s, pl, B, df, times, p, cost, grad, status, st)
   MTG_TIME_STD_DISPATCH(time_cost_nrd, pl, B, df, times, p, cost, grad, status, st)
 }
 
@@ -363,6 +505,9 @@ hipError_t launch_time_optimize_std(const PlanDev& pl, int64_t B, const double* 
                                     double* cost, int32_t* evals, int32_t* solves,
                                     int32_t* status, hipStream_t st) {
   if (!has_time_std(pl)) return hipErrorInvalidValue;
+  if (use_time_wave(pl))
+    MTG_TIME_WAVE_DISPATCH(time_opt_wave_s, pl, B, df, times, p, max_evals, cost, evals, solves,
+                           status, st)
   MTG_TIME_STD_DISPATCH(time_opt_nrd, pl, B, df, times, p, max_evals, cost, evals, solves, status,
                         st)
 }

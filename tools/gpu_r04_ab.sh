@@ -12,3 +12,18 @@ for i in 1 2 3; do
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/ab_a20_$i.json 2> gpurun_out/ab_a20_$i.err; line gpurun_out/ab_a20_$i.json base20
   MTG_LIB_PATH=$VAR timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/ab_b20_$i.json 2> gpurun_out/ab_b20_$i.err; line gpurun_out/ab_b20_$i.json var20
 done
+bash tools/pmc_sq.sh time --workload time --steps 3 --warmup 1 > gpurun_out/sq_time.log 2>&1 || { echo "pmc_sq time failed"; tail -5 gpurun_out/sq_time.log; }
+python3 tools/sq_summary.py time time_optimize_std_kernel 4096 || true
+bash tools/pmc_lds.sh time --workload time --steps 3 --warmup 1 > gpurun_out/lds_time.log 2>&1 || { echo "pmc_lds time failed"; }
+for p in p3 p4; do
+  f=gpurun_out/lds_time/$p/run_counter_collection.csv
+  [ -f $f ] && python3 -c "
+import csv,statistics
+per={}
+for r in csv.DictReader(open('$f')):
+    if 'time_optimize_std_kernel' not in r['Kernel_Name']: continue
+    per.setdefault(r['Counter_Name'],{}).setdefault(r['Dispatch_Id'],0.0)
+    per[r['Counter_Name']][r['Dispatch_Id']]+=float(r['Counter_Value'])
+for k,d in per.items(): print('$p',k,statistics.median(d.values()))
+" || echo "no $p csv"
+done
