@@ -459,11 +459,124 @@ struct ExtSoft {
     return sq;
   }
 
+  // Bernstein coefficients of q on [0, 1]: beta_i = sum_j C(i, j) / C(MF, j)
+  // q_j, the scaled q_j through the binomial transform as Pascal additions
+  // (MF + 1 constants instead of (MF + 1)(MF + 2) / 2 ratios held in
+  // registers).
+  __device__ static void bernstein(double (&bb)[MF + 1]) {
+#pragma unroll
+    for (int j = 0; j <= MF; ++j) bb[j] *= 1.0 / ext_binom(MF, j);
+#pragma unroll
+    for (int k = 1; k <= MF; ++k)
+#pragma unroll
+      for (int i = MF; i >= k; --i) bb[i] += bb[i - 1];
+  }
+
+  // A node's Bernstein coefficients bb of f on [a, e] (part coordinate u):
+  // pruned (g <= g(t_a) + 2 (t_e - t_a) max(0, max_i bb_i) mx cannot reach
+  // lb), the sign variations (zeros skipped), the first nonzero sign, and the
+  // control polygon's first + to - step (its index ci and coefficients b0, b1).
+  struct Scan {
+    bool pruned;
+    int var, ci;
+    double first, b0, b1;
+  };
+  __device__ static Scan scan(const double (&bb)[MF + 1], double a, double e, double ga, double hw,
+                              double lb) {
+    Scan r;
+    double bmax = 0.0;
+#pragma unroll
+    for (int i = 0; i <= MF; ++i) bmax = fmax(bmax, bb[i]);
+    r.pruned = fma(2.0 * (e - a) * hw, bmax, ga) < lb * (1.0 - 1.0e-12);
+    int var = 0;
+    double first = 0.0, last = 0.0;
+    bool found = false;
+    int ci = 0;  // an int select: no double constants held in registers
+    double b0 = 1.0, b1 = -1.0;
+#pragma unroll
+    for (int i = 0; i <= MF; ++i) {
+      const double x = bb[i];
+      const bool nz = x != 0.0;
+      var += (nz && last != 0.0 && ((x > 0.0) != (last > 0.0))) ? 1 : 0;
+      first = (first == 0.0) ? x : first;
+      last = nz ? x : last;
+      if (i < MF) {
+        const bool cross = !found && x > 0.0 && !(bb[i + 1] > 0.0);
+        ci = cross ? i : ci;
+        b0 = cross ? x : b0;
+        b1 = cross ? bb[i + 1] : b1;
+        found = found || cross;
+      }
+    }
+    r.var = var;
+    r.first = first;
+    r.ci = ci;
+    r.b0 = b0;
+    r.b1 = b1;
+    return r;
+  }
+
+  // The local maximum of g on a node [a, e] with one + to - sign change of
+  // f: Laguerre's method (the actual degree of f for this lane's K) on q
+  // (f in the part coordinate), started at the control polygon's zero
+  // crossing and safeguarded by the bracket, with approximate reciprocals
+  // and square root: cubic convergence from the polygon start, and the
+  // bracket keeps every step valid.  Stops at the rounding floor of the
+  // Horner sum or once a step is below kTol of the part: the error is then
+  // of order kTol^3, and the value's error of order its square times the
+  // part's width (below rounding).  Returns g there.
+  __device__ static double refine(const double (&q)[MF + 1], const double* c, const double* fk,
+                                  int K, int D, double T, double w0, double u0, double a, double e,
+                                  const Scan& sc, ExtStats* stats) {
+    const double dn = sc.b0 - sc.b1;
+    const double r0 = __builtin_amdgcn_rcp(dn);
+    const double fr = sc.b0 * fma(r0, fma(-dn, r0, 1.0), r0);
+    int ci = sc.ci;
+    __asm__ volatile("" : "+v"(ci));  // converted here, not as a select chain of doubles
+    const double x0 = fma(e - a, (static_cast<double>(ci) + fr) * (1.0 / MF), a);
+    constexpr double kTol = 1.0e-7;
+    const double nd = static_cast<double>(2 * (N - K) - 3);
+    double lo = a, hi = e, x = x0;
+    int its = 0;
+    for (int it = 0; it < 64; ++it) {
+      ++its;
+      if (stats) ++stats->iters;
+      double fx = q[MF], d1 = 0.0, d2 = 0.0, ab = fabs(q[MF]);
+#pragma unroll
+      for (int j = MF - 1; j >= 0; --j) {
+        d2 = fma(d2, x, d1);
+        d1 = fma(d1, x, fx);
+        fx = fma(fx, x, q[j]);
+        ab = fma(ab, x, fabs(q[j]));
+      }
+      if (fabs(fx) <= 32.0 * 2.220446049250313e-16 * ab) break;
+      if (fx > 0.0) lo = x; else hi = x;
+      const double s0 = __builtin_amdgcn_rcp(fx);
+      const double rf = fma(s0, fma(-fx, s0, 1.0), s0);
+      const double G = d1 * rf;
+      const double H = G * G - 2.0 * d2 * rf;
+      const double rad = fmax((nd - 1.0) * (nd * H - G * G), 0.0);
+      const double sq = __builtin_amdgcn_sqrt(rad);
+      const double den = G >= 0.0 ? G + sq : G - sq;
+      const double t0 = __builtin_amdgcn_rcp(den);
+      const double rden = fma(t0, fma(-den, t0, 1.0), t0);
+      double xn = den != 0.0 ? fma(-nd, rden, x) : 0.5 * (lo + hi);
+      if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
+      const bool done = fabs(xn - x) <= kTol || hi - lo <= kTol;
+      x = xn;
+      if (done) break;
+    }
+    if (stats) stats->maxit = stats->maxit > its ? stats->maxit : its;
+    return mag2(c, fk, K, D, fma(w0, x, u0) * T);
+  }
+
   // Largest |p^(K)|^2 on part p of P of a segment (coefficients c, time T)
   // that can matter: the part's end values gl, gr and the local maxima
   // inside it whose bound reaches lb, a value attained on the trajectory
   // (nodes bounded below it are pruned; a 1e-12 margin keeps rounding from
-  // pruning the node that holds the maximum).
+  // pruning the node that holds the maximum).  At most two coefficient
+  // arrays are live at any point (q and one node's), which keeps the time
+  // kernels that inline the search at two waves per SIMD.
   __device__ static double part_max(const double* c, const double* fk, int K, int D, double T,
                                     int p, int P, double gl, double gr, double lb,
                                     ExtStats* stats = nullptr) {
@@ -485,8 +598,12 @@ struct ExtSoft {
 #pragma unroll
         for (int e = 0; e + 1 < NK; ++e) q[i + e] = fma(a[i], (e + 1) * a[e + 1], q[i + e]);
     }
-    // q(u) = f(T (u0 + w0 u)) on the part, u in [0, 1].
-    const double w0 = 1.0 / P, u0 = p * w0;
+    // q(u) = f(T (u0 + w0 u)) on the part, u in [0, 1].  (w0 opaque: its
+    // powers below would otherwise be hoisted out of every enclosing loop
+    // and held in 28 registers.)
+    double w0 = 1.0 / P;
+    __asm__ volatile("" : "+v"(w0));
+    const double u0 = p * w0;
     {
       double tp = T;
 #pragma unroll
@@ -510,15 +627,12 @@ struct ExtSoft {
       }
     }
     double beta[MF + 1];
+#pragma unroll
+    for (int j = 0; j <= MF; ++j) beta[j] = q[j];
+    bernstein(beta);
     double mx = 0.0;
 #pragma unroll
-    for (int i = 0; i <= MF; ++i) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j <= i; ++j) acc = fma(ext_binom(i, j) / ext_binom(MF, j), q[j], acc);
-      beta[i] = acc;
-      mx = fmax(mx, fabs(acc));
-    }
+    for (int i = 0; i <= MF; ++i) mx = fmax(mx, fabs(beta[i]));
     if (!(mx > 0.0)) return best;  // f = 0: g constant on the part
     const double inv = 1.0 / mx;
 #pragma unroll
@@ -530,119 +644,56 @@ struct ExtSoft {
 #ifdef MTG_STAMPS
     MTG_TACC(471, m0_);  // setup of the part (lane 0)
 #endif
-    int level = 0, idx = 0;
+    // Root node [0, 1]: g(0) of the part is gl, already in best.
+    if (stats) ++stats->nodes;
+    const Scan rs = scan(beta, 0.0, 1.0, gl, hw, lb);
+#ifdef MTG_STAMPS
+    MTG_TACC(474, m0_);  // node: bound, sign scan
+#endif
+    // One sign change from + to - is a local maximum of g; from - to + a
+    // local minimum, never the maximum.
+    if (!rs.pruned && rs.var == 1 && rs.first > 0.0)
+      best = fmax(best, refine(q, c, fk, K, D, T, w0, u0, 0.0, 1.0, rs, stats));
+#ifdef MTG_STAMPS
+    MTG_TACC(476, m0_);  // refinement + value
+#endif
+    if (rs.pruned || rs.var <= 1) return best;
+    // Descent (rare): a node's coefficients come from q (Taylor shift to a,
+    // scale by its width, Bernstein conversion), so only q and one node's
+    // coefficients are live.
+    int level = 1, idx = 0;
     for (;;) {
+      // Keeps mag2's coefficient reads (LDS) in the loop rather than hoisted
+      // into registers.
+      __asm__ volatile("" ::: "memory");
       if (stats) ++stats->nodes;
       const double w = ldexp(1.0, -level);
       const double a = idx * w;
       const double e = a + w;
       double bb[MF + 1];
 #pragma unroll
-      for (int i = 0; i <= MF; ++i) bb[i] = beta[i];
-      if (level > 0) {
-        if (e < 1.0) {
+      for (int i = 0; i <= MF; ++i) bb[i] = q[i];
+      if (a > 0.0) {
 #pragma unroll
-          for (int r = 1; r <= MF; ++r)
+        for (int i = 0; i < MF; ++i)
 #pragma unroll
-            for (int i = MF; i >= r; --i) bb[i] = fma(e, bb[i] - bb[i - 1], bb[i - 1]);
-        }
-        if (a > 0.0) {
-          const double u = a / e;
+          for (int j = MF - 1; j >= i; --j) bb[j] = fma(a, bb[j + 1], bb[j]);
+      }
+      {
+        double wp = w;
 #pragma unroll
-          for (int r = 1; r <= MF; ++r)
-#pragma unroll
-            for (int i = 0; i <= MF - r; ++i) bb[i] = fma(u, bb[i + 1] - bb[i], bb[i]);
+        for (int j = 1; j <= MF; ++j) {
+          bb[j] *= wp;
+          wp *= w;
         }
       }
-      const double ta = fma(w0, a, u0) * T;
-      const double ga = level == 0 ? gl : mag2(c, fk, K, D, ta);
-      double bmax = 0.0;
-#pragma unroll
-      for (int i = 0; i <= MF; ++i) bmax = fmax(bmax, bb[i]);
-      // g <= g(t_a) + 2 (t_e - t_a) max(0, max_i beta_i) mx on the node.
-      const bool pruned = fma(2.0 * (e - a) * hw, bmax, ga) < lb * (1.0 - 1.0e-12);
-      // Sign variations (zeros skipped), the first nonzero sign, and the
-      // control polygon's first + to - step (its index and coefficients).
-      int var = 0;
-      double first = 0.0, last = 0.0;
-      bool found = false;
-      double ci = 0.0, b0 = 1.0, b1 = -1.0;
-#pragma unroll
-      for (int i = 0; i <= MF; ++i) {
-        const double x = bb[i];
-        const bool nz = x != 0.0;
-        var += (nz && last != 0.0 && ((x > 0.0) != (last > 0.0))) ? 1 : 0;
-        first = (first == 0.0) ? x : first;
-        last = nz ? x : last;
-        if (i < MF) {
-          const bool cross = !found && x > 0.0 && !(bb[i + 1] > 0.0);
-          ci = cross ? static_cast<double>(i) : ci;
-          b0 = cross ? x : b0;
-          b1 = cross ? bb[i + 1] : b1;
-          found = found || cross;
-        }
-      }
-      if (!pruned && bb[0] == 0.0 && (a > 0.0 || p > 0)) best = fmax(best, ga);
-#ifdef MTG_STAMPS
-      MTG_TACC(474, m0_);  // node: copy, bound, sign scan
-#endif
-      // One sign change from + to - is a local maximum of g; from - to + a
-      // local minimum, never the maximum.
-      if (!pruned && var == 1 && first > 0.0) {
-        // Start at the control polygon's zero crossing.
-        const double dn = b0 - b1;
-        const double r0 = __builtin_amdgcn_rcp(dn);
-        const double fr = b0 * fma(r0, fma(-dn, r0, 1.0), r0);
-        const double x0 = fma(e - a, (ci + fr) * (1.0 / MF), a);
-        // Laguerre's method (the actual degree of f for this lane's K),
-        // safeguarded by the bracket, with approximate reciprocals and
-        // square root: cubic convergence from the polygon start, and the
-        // bracket keeps every step valid.  Stops at the rounding floor of
-        // the Horner sum or once a step is below kTol of the part: the
-        // error is then of order kTol^3, and the value's error of order its
-        // square times the part's width (below rounding).
-        constexpr double kTol = 1.0e-7;
-        const double nd = static_cast<double>(2 * (N - K) - 3);
-        double lo = a, hi = e, x = x0;
-        int its = 0;
-        for (int it = 0; it < 64; ++it) {
-          ++its;
-          if (stats) ++stats->iters;
-          double fx = q[MF], d1 = 0.0, d2 = 0.0, ab = fabs(q[MF]);
-#pragma unroll
-          for (int j = MF - 1; j >= 0; --j) {
-            d2 = fma(d2, x, d1);
-            d1 = fma(d1, x, fx);
-            fx = fma(fx, x, q[j]);
-            ab = fma(ab, x, fabs(q[j]));
-          }
-          if (fabs(fx) <= 32.0 * 2.220446049250313e-16 * ab) break;
-          if (fx > 0.0) lo = x; else hi = x;
-          const double r0 = __builtin_amdgcn_rcp(fx);
-          const double rf = fma(r0, fma(-fx, r0, 1.0), r0);
-          const double G = d1 * rf;
-          const double H = G * G - 2.0 * d2 * rf;
-          const double rad = fmax((nd - 1.0) * (nd * H - G * G), 0.0);
-          const double sq = __builtin_amdgcn_sqrt(rad);
-          const double den = G >= 0.0 ? G + sq : G - sq;
-          const double s0 = __builtin_amdgcn_rcp(den);
-          const double rden = fma(s0, fma(-den, s0, 1.0), s0);
-          double xn = den != 0.0 ? fma(-nd, rden, x) : 0.5 * (lo + hi);
-          if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
-          const bool done = fabs(xn - x) <= kTol || hi - lo <= kTol;
-          x = xn;
-          if (done) break;
-        }
-        if (stats) stats->maxit = stats->maxit > its ? stats->maxit : its;
-#ifdef MTG_STAMPS
-        MTG_TACC(475, m0_);  // refinement (lane 0 only if it refines)
-#endif
-        best = fmax(best, mag2(c, fk, K, D, fma(w0, x, u0) * T));
-      }
-#ifdef MTG_STAMPS
-      MTG_TACC(476, m0_);  // refinement + value
-#endif
-      if (!pruned && var > 1) {
+      bernstein(bb);
+      const double ga = mag2(c, fk, K, D, fma(w0, a, u0) * T);
+      const Scan sc = scan(bb, a, e, ga, hw, lb);
+      if (!sc.pruned && bb[0] == 0.0 && (a > 0.0 || p > 0)) best = fmax(best, ga);
+      if (!sc.pruned && sc.var == 1 && sc.first > 0.0)
+        best = fmax(best, refine(q, c, fk, K, D, T, w0, u0, a, e, sc, stats));
+      if (!sc.pruned && sc.var > 1) {
         if (level >= kExtMaxLevel) {
           best = fmax(best, mag2(c, fk, K, D, fma(w0, 0.5 * (a + e), u0) * T));
         } else {
