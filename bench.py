@@ -251,9 +251,9 @@ def device_kernel(wl, plan, B, N, D, r, S):
     if wl == "time":
         return ("time_optimize_wave_kernel" if (N, r, D) == (10, 4, 3) and 2 <= S <= 16 else
                 "time_optimize_std_kernel")
-    return {"tube": "tube_solve_kernel",
-            "time-qcqp": "tube_solve_kernel", "sample": "sample_kernel",
-            "collision": "coll_walk_kernel"}[wl]
+    if wl in ("tube", "time-qcqp"):
+        return "tube_solve_s_kernel" if N == 10 and 2 <= S <= 16 else "tube_solve_kernel"
+    return {"sample": "sample_kernel", "collision": "coll_walk_kernel"}[wl]
 
 
 def load_pmc_traffic(key, kernel_ms):
@@ -627,7 +627,11 @@ def main():
             def step():
                 return mtg.tube_solve(ctx, N, r, pos_d, tfix, times_d, times_d, radii)
 
-            bytes_per_traj = ((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8 + (S * 3 * N + 1) * 8
+            # inputs (positions, fixed values, two time vectors, radii) + outputs
+            # (x: 3 (S-1) N/2 free control-point values, coefficients, cost,
+            # iteration count, status)
+            bytes_per_traj = (((S + 1) * 3 + 3 * N + 2 * S + 2 * S) * 8
+                              + (3 * (S - 1) * (N // 2) + S * 3 * N + 1) * 8 + 4 + 4)
             metric = "converged tube QCQP solves/sec (4096 x 10-seg, N=10, 3D)"
             useful_per_step = conv
             flops_per_step = f_iter * iters

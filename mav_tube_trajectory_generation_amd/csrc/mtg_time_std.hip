@@ -353,12 +353,8 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
 }
 
 // The same on the compile-time-S solver (N = 10, r = 4, D = 3, S = 2..16).
-#ifndef MTG_TIME_SOFT_WPE
-#define MTG_TIME_SOFT_WPE 1
-#endif
 template <int N, int R, int D, int S, bool kSoft>
-__global__ __launch_bounds__(kWave)
-__attribute__((amdgpu_waves_per_eu(kSoft ? MTG_TIME_SOFT_WPE : 1))) void time_optimize_wave_kernel(
+__global__ __launch_bounds__(kWave) void time_optimize_wave_kernel(
     const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     double* __restrict__ times_io, mtg_time_params p, int max_evals,
     double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
@@ -463,10 +459,6 @@ bool use_time_wave(const PlanDev& pl) {
   return has_linear_wave(pl) && !forced;
 }
 
-#ifdef MTG_EXP_S10_ONLY  // experiment builds: one S only (compile time)
-#define MTG_TIME_WAVE_DISPATCH(FN, ...) \
-  switch (pl.S) { case 10: return FN<10>(__VA_ARGS__); default: return hipErrorInvalidValue; }
-#else
 #define MTG_TIME_WAVE_DISPATCH(FN, ...)                                                      \
   switch (pl.S) {                                                                            \
     case 2: return FN<2>(__VA_ARGS__);   case 3: return FN<3>(__VA_ARGS__);                   \
@@ -479,7 +471,6 @@ bool use_time_wave(const PlanDev& pl) {
     case 16: return FN<16>(__VA_ARGS__);                                                     \
     default: return hipErrorInvalidValue;                                                    \
   }
-#endif
 }  // namespace
 
 bool has_time_std(const PlanDev& pl) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "mtg_internal.h"
 #include "mtg_tube_device.h"
@@ -56,10 +57,10 @@ __global__ __launch_bounds__(kWave) void tube_residuals_kernel(
 template <int N>
 constexpr int tube_threads() { return N <= 10 ? 2 * kWave : kWave; }
 
+// The kernel body for S segments (a kernel argument, or a compile-time
+// constant in tube_solve_s_kernel).
 template <int N>
-__global__ __launch_bounds__(tube_threads<N>())
-__attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
-void tube_solve_kernel(
+__device__ __attribute__((always_inline)) void tube_solve_body(
     int S, int r, int rep, const double* __restrict__ tab, const double* __restrict__ positions,
     const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,
     const double* __restrict__ times, const double* __restrict__ radii, double tol,
@@ -122,6 +123,33 @@ void tube_solve_kernel(
   }
 }
 
+#define MTG_TUBE_SOLVE_PARAMS                                                                  \
+  int S, int r, int rep, const double* __restrict__ tab, const double* __restrict__ positions, \
+      const double* __restrict__ fixed_vals, const double* __restrict__ times_cp,              \
+      const double* __restrict__ times, const double* __restrict__ radii, double tol,          \
+      int max_iter, const int32_t* __restrict__ skip, double* __restrict__ x_out,              \
+      double* __restrict__ coeffs, double* __restrict__ cost, int32_t* __restrict__ iters,     \
+      int32_t* __restrict__ status
+
+template <int N>
+__global__ __launch_bounds__(tube_threads<N>())
+__attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
+void tube_solve_kernel(MTG_TUBE_SOLVE_PARAMS) {
+  tube_solve_body<N>(S, r, rep, tab, positions, fixed_vals, times_cp, times, radii, tol, max_iter,
+                     skip, x_out, coeffs, cost, iters, status);
+}
+
+// S a compile-time constant (the argument S is ignored): every layout
+// offset, loop bound and index division by S folds into the code, which
+// frees the registers that held them (N = 10, S = 2..16).
+template <int N, int SC>
+__global__ __launch_bounds__(tube_threads<N>())
+__attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
+void tube_solve_s_kernel(MTG_TUBE_SOLVE_PARAMS) {
+  tube_solve_body<N>(SC, r, rep, tab, positions, fixed_vals, times_cp, times, radii, tol, max_iter,
+                     skip, x_out, coeffs, cost, iters, status);
+}
+
 #ifdef MTG_STAMPS
 extern "C" int mtg_debug_tube_stamps(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mtg_stamps), sizeof(unsigned long long) * n) ==
@@ -155,16 +183,49 @@ hipError_t residuals_n(const TubeArgs& a, const double* x, double* resid, hipStr
   return hipGetLastError();
 }
 
+template <typename K>
+hipError_t solve_launch(K kernel, int threads, const TubeArgs& a, double tol, int max_iter,
+                        double* x, double* coeffs, double* cost, int32_t* iters, int32_t* status,
+                        hipStream_t st) {
+  const size_t bytes = tube_lds_bytes(a.N, a.S);
+  hipError_t e = prepare_lds(kernel, bytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(threads), bytes, st, a.S,
+                     a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp, a.times, a.radii,
+                     tol, max_iter, a.skip, x, coeffs, cost, iters, status);
+  return hipGetLastError();
+}
+
+// The compile-time-S kernels unless MTG_TUBE_RUNTIME_S=1 (A/B runs).
+bool tube_runtime_s_forced() {
+  static const bool forced = [] {
+    const char* e = std::getenv("MTG_TUBE_RUNTIME_S");
+    return e && e[0] == '1';
+  }();
+  return forced;
+}
+
 template <int N>
 hipError_t solve_n(const TubeArgs& a, double tol, int max_iter, double* x, double* coeffs,
                    double* cost, int32_t* iters, int32_t* status, hipStream_t st) {
-  const size_t bytes = tube_lds_bytes(N, a.S);
-  hipError_t e = prepare_lds(tube_solve_kernel<N>, bytes);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tube_solve_kernel<N>, dim3(static_cast<unsigned>(a.B)), dim3(tube_threads<N>()),
-                     bytes, st, a.S, a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp,
-                     a.times, a.radii, tol, max_iter, a.skip, x, coeffs, cost, iters, status);
-  return hipGetLastError();
+  constexpr int T = tube_threads<N>();
+  if constexpr (N == 10) {
+    if (!tube_runtime_s_forced()) {
+      switch (a.S) {
+#define MTG_TUBE_S(SS)                                                                     \
+  case SS:                                                                                 \
+    return solve_launch(tube_solve_s_kernel<10, SS>, T, a, tol, max_iter, x, coeffs, cost, \
+                        iters, status, st);
+        MTG_TUBE_S(2) MTG_TUBE_S(3) MTG_TUBE_S(4) MTG_TUBE_S(5) MTG_TUBE_S(6) MTG_TUBE_S(7)
+        MTG_TUBE_S(8) MTG_TUBE_S(9) MTG_TUBE_S(10) MTG_TUBE_S(11) MTG_TUBE_S(12) MTG_TUBE_S(13)
+        MTG_TUBE_S(14) MTG_TUBE_S(15) MTG_TUBE_S(16)
+#undef MTG_TUBE_S
+        default: break;
+      }
+    }
+  }
+  return solve_launch(tube_solve_kernel<N>, T, a, tol, max_iter, x, coeffs, cost, iters, status,
+                      st);
 }
 }  // namespace
 
