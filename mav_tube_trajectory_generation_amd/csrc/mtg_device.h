@@ -76,6 +76,21 @@ namespace mtg {
 
 constexpr int kWave = 64;
 
+// XCD-aware problem index of a one-problem-per-workgroup launch.  The
+// dispatcher deals workgroups to the eight XCDs round-robin (workgroup i to
+// XCD i mod 8: tools/tube_order.py fits that model), and each XCD has its
+// own L2, so with b = blockIdx.x neighbouring problems, which share the cache
+// lines at the edges of their input rows, land on different XCDs and each
+// of them fetches those lines from HBM.  This bijection gives XCD x the
+// contiguous range of problems [x q + min(x, r), ...) (q = G / 8,
+// r = G mod 8), so shared lines are read once.
+constexpr int kXcds = 8;
+__device__ inline int64_t xcd_problem(int64_t i, int64_t G) {
+  const int64_t q = G / kXcds, r = G % kXcds;
+  const int64_t x = i % kXcds, k = i / kXcds;
+  return x * q + (x < r ? x : r) + k;
+}
+
 // LDS carve-up (in doubles, then ints), identical for every kernel.
 struct Layout {
   int tabH, tabA;  // H(1), A(1)^-1: N*N each

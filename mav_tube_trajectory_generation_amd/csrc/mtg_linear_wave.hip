@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   Sv sv;
   sv.init(sm);
   const int lane = sv.lane;
-  const int64_t b = blockIdx.x;
+  const int64_t b = xcd_problem(blockIdx.x, gridDim.x);
   const double* fb = fixed_vals + b * D * NFIX;
   const double* tb = times + b * S;
   MTG_STAMP(0);
