@@ -68,7 +68,7 @@ __device__ __attribute__((always_inline)) void tube_solve_body(
     double* __restrict__ coeffs, double* __restrict__ cost, int32_t* __restrict__ iters,
     int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int64_t b = blockIdx.x;
+  const int64_t b = xcd_problem(blockIdx.x, gridDim.x);  // mtg_device.h
   if (skip && skip[b / rep]) return;  // workgroup-uniform
   const TubeLayout L = make_tube_layout(N, S);
   Tube<N> t = make_tube<N>(&L, smem, S, r, tab);
