@@ -271,3 +271,24 @@ def test_hard_constraints_only_where_implemented(ctx, dev):
     with pytest.raises(MTGError):
         plan.time_cost(fd, td, soft=[(1, 3.0)], hard=True, hard_tolerance=-1.0)
     check(0, "ok")
+
+
+@pytest.mark.parametrize("S", [2, 3, 5, 7, 11, 13, 16])
+def test_time_cost_wave_kernels_every_s(ctx, dev, oracle, S):
+    """time_cost_wave_kernel<10, 4, 3, S> (AUTO on the standard pattern,
+    S = 2..16) against the oracle's objective and mode-2 gradient."""
+    import mav_tube_trajectory_generation_amd as mtg
+    B = 4
+    mask, fixed, times, _ = _batch(S, B, 900 + 10 * S)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    out = plan.time_cost(torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev),
+                         grad_mode=2, increment=0.1, w_d=0.1, w_t=1.0)
+    cost = out["cost"].cpu().numpy()
+    grad = out["grad"].cpu().numpy()
+    assert (out["status"].cpu().numpy() == 0).all()
+    for b in range(B):
+        v = standard_vertices(N, S, D, 900 + 10 * S + b)
+        J, g = oracle.time_cost(N, R, v, times[b], grad_mode=2, increment=0.1, w_d=0.1, w_t=1.0)
+        tol = 1e-9 if times[b].min() > 0.5 else 1e-6
+        assert rel_err(cost[b], J) <= tol, (S, b)
+        assert np.max(np.abs(grad[b] - g)) <= 1e-5 * np.max(np.abs(g)) + 1e-9, (S, b)

@@ -169,3 +169,23 @@ def test_polynomial_orders_vs_oracle(ctx, dev, oracle, n, r, S):
         assert rel_err_coeffs(o["coeffs"][b], ref["coeffs"]) <= 1e-6, b
         assert rel_err(o["cost"][b], ref["cost"]) <= 1e-6, b
     assert agree >= B // 2
+
+
+@pytest.mark.parametrize("S", [2, 3, 5, 7, 9, 11, 13, 16])
+def test_compile_time_s_kernels_vs_oracle(ctx, dev, oracle, S):
+    """tube_solve_s_kernel<10, S> (every S it is instantiated for is one of
+    these or between them) against the oracle IPM on a small batch."""
+    B = 3
+    items = []
+    for b in range(B):
+        v = oracle.random_vertices(M - 1, S, 3, -10.0, 10.0, 300 + 7 * S + b)
+        items.append((v, oracle.estimate_segment_times(v, 3.0, 5.0)))
+    out = _gpu(ctx, dev, items)
+    radii = np.full((S, 2), 0.15)
+    for b, (v, t) in enumerate(items):
+        ref = oracle.tube_solve(N, R, v, t, radii, tol=1e-10, max_iter=100)
+        assert out["status"][b] == ref["status"], (S, b)
+        if ref["status"] != 0:
+            continue
+        assert rel_err_coeffs(out["coeffs"][b], ref["coeffs"]) <= 1e-6, (S, b)
+        assert rel_err(out["cost"][b], ref["cost"]) <= 1e-6, (S, b)
