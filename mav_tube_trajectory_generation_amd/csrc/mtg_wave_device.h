@@ -248,6 +248,7 @@ struct Solver {
       const double cpos = fma(hMk[M], ql[0], hk[0] * qr[0]);  // p_v
       const double cprev = hMk[0] * ql[0];                     // p_{v-1}
       const double cnext = hk[M] * qr[0];                      // p_{v+1}
+      MTG_STAMP(1);
       double* sl = slot_of(av);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
@@ -271,6 +272,7 @@ struct Solver {
       lds_st(pb, Cr);
     }
     lds_order();
+    MTG_STAMP(12);
     // The fully fixed end vertices' part of b_1 (segment 0) and b_(S-1)
     // (segment S-1): lane (e, d, i) adds -sum_l H_seg(k, l) d_f(l) for its row.
     {

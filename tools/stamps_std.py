@@ -42,7 +42,7 @@ def main():
         runs.append(np.array(st[:], dtype=np.int64))
     st = np.median(np.array(runs), axis=0)
     order = [(0, "start"), (7, "times arrived, powers"), (1, "fixed stored"),
-             (2, "assembly")]
+             (12, "assembly stores"), (2, "assembly")]
     k = 0
     while st[100 + 2 * k] > 0:
         order.append((100 + 2 * k, f"(sweep step {k} start)"))
@@ -62,6 +62,7 @@ def main():
         print(f"  {name:>24}: {st[slot] - prev:8.0f}")
         prev = st[slot]
     print(f"  total: {st[6] - st[0]:.0f} cycles")
+
 
 
 if __name__ == "__main__":
