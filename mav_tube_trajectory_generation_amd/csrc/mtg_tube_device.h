@@ -113,6 +113,7 @@ struct Tube {
   int lane;                          // lane in its wave
   const double* __restrict__ gtab;
   int tid, nthr, wv;                 // thread, threads (64 or 128), wave
+  int redp = 0;                      // block_red's slot pair (alternates)
   // With two waves per trajectory the data-parallel phases use both; the
   // block LDL^T and the block solves run on wave 0 (wave 1 meets the same
   // barriers with nothing to do).  // plan table: H(1) N*N, A(1)^-1 N*N, C^-1 M*M (global)
@@ -814,16 +815,38 @@ struct Tube {
     __syncthreads();
   }
 
-  __device__ static double wave_max(double x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x = fmax(x, __shfl_xor(x, off, kWave));
-    return x;
+  // x op (x moved by DPP control CTRL); lanes with no source, or in rows
+  // RM leaves out, take their own value (op(x, x) = x).
+  template <int CTRL, int RM, bool kMax>
+  __device__ static double dpp_op(double x) {
+    const long long u = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_update_dpp(static_cast<int>(u), static_cast<int>(u), CTRL, RM,
+                                               0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(static_cast<int>(u >> 32),
+                                               static_cast<int>(u >> 32), CTRL, RM, 0xf, false);
+    const double y = __builtin_bit_cast(
+        double, (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+    return kMax ? fmax(x, y) : fmin(x, y);
   }
-  __device__ static double wave_min(double x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x = fmin(x, __shfl_xor(x, off, kWave));
-    return x;
+  // Wave maximum / minimum in every lane: DPP scans in rows of 16, the row
+  // broadcasts, then lane 63's value (VALU moves instead of the six LDS
+  // permutes of a shuffle butterfly; max and min do not depend on the order).
+  template <bool kMax>
+  __device__ static double wave_ext(double x) {
+    x = dpp_op<0x111, 0xf, kMax>(x);
+    x = dpp_op<0x112, 0xf, kMax>(x);
+    x = dpp_op<0x114, 0xf, kMax>(x);
+    x = dpp_op<0x118, 0xf, kMax>(x);
+    x = dpp_op<0x142, 0xa, kMax>(x);
+    x = dpp_op<0x143, 0xc, kMax>(x);
+    const long long u = __builtin_bit_cast(long long, x);
+    return __builtin_bit_cast(
+        double, (static_cast<long long>(__builtin_amdgcn_readlane(static_cast<int>(u >> 32), 63))
+                 << 32) |
+                    static_cast<unsigned int>(__builtin_amdgcn_readlane(static_cast<int>(u), 63)));
   }
+  __device__ static double wave_max(double x) { return wave_ext<true>(x); }
+  __device__ static double wave_min(double x) { return wave_ext<false>(x); }
   __device__ static double wave_sum(double x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
@@ -834,10 +857,14 @@ struct Tube {
   __device__ double block_red(double x) {
     x = kOp == 0 ? wave_max(x) : kOp == 1 ? wave_min(x) : wave_sum(x);
     if (nthr == kWave) return x;
-    if (lane == 0) sm[L->red + wv] = x;
+    // Consecutive reductions alternate between two slot pairs, so one
+    // barrier suffices: a wave that writes a pair again has passed the next
+    // reduction's barrier, which the other wave reaches only after reading.
+    const int p = L->red + 2 * redp;
+    redp ^= 1;
+    if (lane == 0) sm[p + wv] = x;
     __syncthreads();
-    const double a = sm[L->red], c = sm[L->red + 1];
-    __syncthreads();
+    const double a = sm[p], c = sm[p + 1];
     return kOp == 0 ? fmax(a, c) : kOp == 1 ? fmin(a, c) : a + c;
   }
   __device__ double block_max(double x) { return block_red<0>(x); }
