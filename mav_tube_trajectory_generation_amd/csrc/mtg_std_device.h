@@ -190,14 +190,24 @@ __device__ inline double quad_bcast(double x) {
   return join64(lo, hi);
 }
 
+// x + (x moved by DPP control CTRL) with every row enabled: lanes with no
+// source read 0 through bound_ctrl, so no zeroed destination is needed.
+template <int CTRL>
+__device__ inline double dpp_add_bc(double x) {
+  const long long u = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(u), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(u >> 32), CTRL, 0xf, 0xf, true);
+  return x + join64(lo, hi);
+}
+
 // Sum over the 64 lanes (all active), returned wave-uniform: inclusive scan
 // in rows of 16 (row_shr 1, 2, 4, 8), then row_bcast 15 and 31; lane 63
 // holds the total.
 __device__ inline double wave_sum_dpp(double x) {
-  x = dpp_add<0x111, 0xf, 0xf>(x);
-  x = dpp_add<0x112, 0xf, 0xf>(x);
-  x = dpp_add<0x114, 0xf, 0xf>(x);
-  x = dpp_add<0x118, 0xf, 0xf>(x);
+  x = dpp_add_bc<0x111>(x);
+  x = dpp_add_bc<0x112>(x);
+  x = dpp_add_bc<0x114>(x);
+  x = dpp_add_bc<0x118>(x);
   x = dpp_add<0x142, 0xa, 0xf>(x);
   x = dpp_add<0x143, 0xc, 0xf>(x);
   const long long u = __builtin_bit_cast(long long, x);
