@@ -264,12 +264,15 @@ struct Solver {
       for (int j = 0; j < MF; ++j) sl[j <= ai ? rbase + j : O_Z + 4 * ai + j] = Ar[j];
       // forward step at v (v < MID): P = C_v, P^T by rows = C_v by columns;
       // backward step at v+1 (MID <= v <= S-2): P = C_v^T, P^T = C_v by rows.
-      // The store a lane does not need goes to the junk area.
-      double* pf = av < MID ? sl + O_P + ai : junk;
-      double* pb = (av >= MID && av < S - 1) ? slot_of(av + 1) + O_P + ai * MF : junk + 8;
+      // A lane needs at most one of the two, so one set of stores with a
+      // per-lane base and stride (LDS stores cost about three times a read's
+      // time per byte and the four waves of a CU share them); lanes that
+      // need neither store to the junk area.
+      const bool fw = av < MID, bk = av >= MID && av < S - 1;
+      double* pc = fw ? sl + O_P + ai : (bk ? slot_of(av + 1) + O_P + ai * MF : junk);
+      const int ps = fw ? MF : 1;
 #pragma unroll
-      for (int j = 0; j < MF; ++j) pf[j * MF] = Cr[j];
-      lds_st(pb, Cr);
+      for (int j = 0; j < MF; ++j) pc[j * ps] = Cr[j];
     }
     lds_order();
     MTG_STAMP(12);
