@@ -208,10 +208,10 @@ struct Solver {
   // vertex derivative.  Returns true if a pivot was not positive
   // (wave-uniform).  All lanes call.
   __device__ bool solve(const double* T) {
-    // The backward chain's terminal slot starts at zero (its last step stores
-    // 0 - P^T x there: the backward terms of the middle vertex).
-    {
-      double* term = slots + (NSL + NBW) * SLOT;
+    // With no backward step (S = 2) the middle vertex reads the backward
+    // chain's terminal slot as zero; otherwise its last step writes it.
+    if constexpr (NBW == 0) {
+      double* term = slots + NSL * SLOT;
       if (lane < G::TRI) term[O_S + lane] = 0.0;
       if (lane < D * MF) term[O_R + lane] = 0.0;
     }
@@ -340,6 +340,10 @@ struct Solver {
               an = Ap[(k + 1) * SLOT];
             }
             block2_solve(Sv, u, x, pmin);
+            // The backward chain's last step stores 0 - P^T x into its
+            // terminal slot (the backward terms of the middle vertex): a is
+            // 0 there instead of a zeroed slot's entry (no zeroing stores).
+            if (k == NBW - 1) a = g ? 0.0 : a;
             // block2_solve finishes x[2], x[3] first
             double o = fma(-pc[2], x[2], a);
             o = fma(-pc[3], x[3], o);
