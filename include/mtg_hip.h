@@ -95,7 +95,7 @@ int mtg_plan_destroy(mtg_plan* plan);
  * createRandomVertices / makeStartOrEnd, vertex.cpp:27-82, 147-153) and
  * 2 <= S <= 64, else the generic kernel.  Among the standard-pattern kernels
  * it picks by batch size: STANDARD (one wavefront per trajectory, lowest
- * latency) below 4096 trajectories, LANE_PAIR from 4096.  LANE gives each
+ * latency) up to 2048 trajectories, LANE_PAIR above.  LANE gives each
  * (trajectory, dimension) one lane that walks the whole vertex chain;
  * LANE_PAIR gives it two lanes in two wavefronts of one workgroup that
  * eliminate the chain from both ends toward the middle vertex (a twisted

@@ -51,9 +51,12 @@ constexpr int kMaxStdS = 64;
 // Lane linear solve for large batches (mtg_linear_lane.hip): one
 // (trajectory, dimension) per lane; standard pattern, N = 10, r = 4, D = 3,
 // 2 <= S <= kMaxLaneS.  AUTO runs the two-lane variant (mtg_linear_lane2.hip)
-// from kLaneMinBatch trajectories.
+// from kLaneMinBatch trajectories: the wave kernel holds at most two waves per
+// SIMD up to 2048 trajectories (1024 SIMDs); with a third the lane-pair kernel
+// is faster (S = 10: 2048 6.69 vs 7.09 us, 2560 8.03 vs 7.44 us,
+// tools/gpu_r04_cross2.sh).
 constexpr int kMaxLaneS = 12;
-constexpr int64_t kLaneMinBatch = 4096;
+constexpr int64_t kLaneMinBatch = 2049;
 struct PlanDev;
 bool has_linear_lane(const PlanDev& pl);
 hipError_t launch_linear_solve_lane(const PlanDev& pl, int64_t B, const double* df,

@@ -76,7 +76,8 @@ def test_auto_selection_by_batch(ctx):
     plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
     assert plan.kernel == "standard"
     assert plan.kernel_for_batch(1024) == "standard"
-    assert plan.kernel_for_batch(4095) == "standard"
+    assert plan.kernel_for_batch(2048) == "standard"
+    assert plan.kernel_for_batch(2049) == "lane_pair"
     assert plan.kernel_for_batch(4096) == "lane_pair"
     assert plan.kernel_for_batch(65536) == "lane_pair"
     assert plan.set_kernel("standard").kernel_for_batch(65536) == "standard"
