@@ -91,6 +91,30 @@ __device__ inline int64_t xcd_problem(int64_t i, int64_t G) {
   return x * q + (x < r ? x : r) + k;
 }
 
+// Copy NCH 16-byte pieces of a staged output from LDS to global memory, lane
+// t of a group of W lanes taking pieces t, t + W, ...: consecutive lanes
+// store consecutive addresses (one instruction covers W x 16 contiguous
+// bytes), and four LDS reads are in flight per batch (named registers: an
+// array here is promoted to LDS before the loop is unrolled).
+template <int W, int NCH>
+__device__ inline void copy_out16(const double2* __restrict__ src, double2* __restrict__ dst,
+                                  int t) {
+  constexpr int IT = (NCH + W - 1) / W;
+#pragma unroll
+  for (int k0 = 0; k0 < IT; k0 += 4) {
+    const int c0 = t + k0 * W, c1 = c0 + W, c2 = c1 + W, c3 = c2 + W;
+    double2 a0 = {}, a1 = {}, a2 = {}, a3 = {};
+    if (c0 < NCH) a0 = src[c0];
+    if (k0 + 1 < IT && c1 < NCH) a1 = src[c1];
+    if (k0 + 2 < IT && c2 < NCH) a2 = src[c2];
+    if (k0 + 3 < IT && c3 < NCH) a3 = src[c3];
+    if (c0 < NCH) dst[c0] = a0;
+    if (k0 + 1 < IT && c1 < NCH) dst[c1] = a1;
+    if (k0 + 2 < IT && c2 < NCH) dst[c2] = a2;
+    if (k0 + 3 < IT && c3 < NCH) dst[c3] = a3;
+  }
+}
+
 // LDS carve-up (in doubles, then ints), identical for every kernel.
 struct Layout {
   int tabH, tabA;  // H(1), A(1)^-1: N*N each

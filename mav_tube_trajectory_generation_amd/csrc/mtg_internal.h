@@ -57,6 +57,8 @@ constexpr int kMaxStdS = 64;
 // tools/gpu_r04_cross2.sh).
 constexpr int kMaxLaneS = 12;
 constexpr int64_t kLaneMinBatch = 2049;
+// The lane-pair kernel stages its coefficients in LDS from this batch size.
+constexpr int64_t kLane2StageMinBatch = 4096;
 struct PlanDev;
 bool has_linear_lane(const PlanDev& pl);
 hipError_t launch_linear_solve_lane(const PlanDev& pl, int64_t B, const double* df,

@@ -446,7 +446,8 @@ template <int N, int R, int D, int S, bool BW>
 __device__ __attribute__((always_inline)) inline void lane2_half(
     int64_t B, const double* __restrict__ fixed_vals, const double* __restrict__ times,
     double* __restrict__ coeffs, double* __restrict__ cost, double* __restrict__ free_vals,
-    int32_t* __restrict__ status, const SelectArgs& sel, double* xch, double* cxch, int* sxch) {
+    int32_t* __restrict__ status, const SelectArgs& sel, double* xch, double* cxch, int* sxch,
+    double* stage) {
   using H = Half<N, R, D, S, BW>;
   constexpr int NT = H::NT, MF = H::MF;
   constexpr int TPW = kWave / D;
@@ -475,7 +476,16 @@ __device__ __attribute__((always_inline)) inline void lane2_half(
   for (int q = 0; q < NT; ++q) to[q] = other[q * kWave + lane];
 #pragma unroll
   for (int i = 0; i < MF; ++i) ro[i] = other[(NT + i) * kWave + lane];
-  double* cb = (act && coeffs) ? coeffs + b * S * D * N : nullptr;
+  // From kLane2StageMinBatch trajectories the coefficients go to the
+  // workgroup's staging area in LDS (the output layout of its TPW
+  // trajectories) and leave in one coalesced copy below; under it each lane
+  // stores its own (the copy's barrier and latency then cost more than the
+  // scattered stores: B = 2048 7.09 -> 7.69 us staged).
+  constexpr int PER = S * D * N;
+  const bool stg = B >= kLane2StageMinBatch;
+  double* cb = !coeffs ? nullptr
+               : stg   ? (tl < TPW ? stage + tl * PER : nullptr)
+                       : (act ? coeffs + b * PER : nullptr);
   double* fv = act ? free_vals : nullptr;
   double part;
   // A bad time's solve values are not stored (write_bad fills NaN).
@@ -494,6 +504,23 @@ __device__ __attribute__((always_inline)) inline void lane2_half(
     sxch[lane] = st;
   }
   __syncthreads();
+  if (coeffs && stg) {
+    // The workgroup's TPW x S x D x N coefficients are one contiguous range
+    // of the output: both waves copy it out in 16-byte pieces, consecutive
+    // lanes on consecutive addresses (the per-lane stores touch 64 cache
+    // lines per instruction: B = 8192 13.0 -> 10.9 us).
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * TPW;
+    const int nt = B - b0 < TPW ? static_cast<int>(B - b0) : TPW;
+    const int nch = nt * (PER / 2);
+    const double2* src = reinterpret_cast<const double2*>(stage);
+    double2* dst = reinterpret_cast<double2*>(coeffs + b0 * PER);
+    const int t = static_cast<int>(threadIdx.x);
+    if (nt == TPW) {
+      copy_out16<2 * kWave, TPW * (PER / 2)>(src, dst, t);
+    } else {
+      for (int c = t; c < nch; c += 2 * kWave) dst[c] = src[c];
+    }
+  }
   if (BW) return;
   part += cxch[lane];
   st = max(st, sxch[lane]);
@@ -525,12 +552,13 @@ __global__ __launch_bounds__(2 * kWave) void linear_lane2_kernel(
   __shared__ double xch[2 * (H::NT + H::MF) * kWave];
   __shared__ double cxch[kWave];
   __shared__ int sxch[kWave];
+  __shared__ __attribute__((aligned(16))) double stage[(kWave / D) * S * D * N];
   if (threadIdx.x < kWave)
     lane2::lane2_half<N, R, D, S, false>(B, fixed_vals, times, coeffs, cost, free_vals, status,
-                                         sel, xch, cxch, sxch);
+                                         sel, xch, cxch, sxch, stage);
   else
     lane2::lane2_half<N, R, D, S, true>(B, fixed_vals, times, coeffs, cost, free_vals, status,
-                                        sel, xch, cxch, sxch);
+                                        sel, xch, cxch, sxch, stage);
 }
 
 namespace {

@@ -47,6 +47,30 @@ def test_lane_kernels_match_wavefront_kernel(ctx, dev, oracle, kernel, S):
         assert rel_err(out["cost"][b], o["cost"]) <= REL_TOL, b
 
 
+@pytest.mark.parametrize("S", [2, 3, 7, 10, 12])
+def test_lane_pair_staged_outputs(ctx, dev, S):
+    """From 4096 trajectories the lane-pair kernel stages its coefficients in
+    LDS and copies each workgroup's range out coalesced (kLane2StageMinBatch):
+    a batch whose last workgroup is ragged (4096 + 5 = 195 x 21 + 2), one bad
+    time, against the wavefront kernel on every trajectory."""
+    import mav_tube_trajectory_generation_amd as mtg
+    B = 4096 + 5
+    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=7000 + S)
+    times[4095, 0] = 0.0
+    plan, out = _solve(ctx, dev, mask, fixed, times, "lane_pair")
+    assert plan.kernel == "lane_pair"
+    _, ref = _solve(ctx, dev, mask, fixed, times, "standard")
+    np.testing.assert_array_equal(out["status"], ref["status"])
+    assert out["status"][4095] == 1 and np.isnan(out["coeffs"][4095]).all()
+    ok = out["status"] == 0
+    assert ok.sum() == B - 1
+    c, r = out["coeffs"][ok], ref["coeffs"][ok]
+    # rel_err_coeffs over the whole batch: per (trajectory, segment, dim)
+    err = np.linalg.norm(c - r, axis=-1) / np.maximum(np.linalg.norm(r, axis=-1), 1e-12)
+    assert err.max() <= 1e-9, float(err.max())
+    np.testing.assert_allclose(out["cost"][ok], ref["cost"][ok], rtol=1e-8)
+
+
 @pytest.mark.parametrize("kernel", ["lane", "lane_pair", "standard", "generic"])
 def test_lane_kernels_bad_time(ctx, dev, kernel):
     import mav_tube_trajectory_generation_amd as mtg
