@@ -3,6 +3,11 @@
 # built with the lane-pair object compiled with -DMTG_EXP_SAME_LOAD (every
 # lane loads trajectory 0's inputs: one cache line per load instruction) or
 # -DMTG_EXP_NO_COEFF (no coefficient stores), against the product build.
+# The two flags were a temporary patch of mtg_linear_lane2.hip at commit
+# 1cdf1a5 (before the staged outputs): in Half::load, `b = 0; d = 0;` under
+# MTG_EXP_SAME_LOAD; in lane2_half, `cb = nullptr;` under MTG_EXP_NO_COEFF.
+# Libraries: the lane-pair object rebuilt with the flag, linked with the
+# other objects of the product build into libmtg_hip_exp_<FLAG>.so.
 set -e -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
