@@ -239,20 +239,24 @@ def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None):
 def device_kernel(wl, plan, B, N, D, r, S):
     """rocprofv3 name (substring) of the launch's dominant kernel: the key,
     with the workload / batch / segments, of its committed counter passes."""
+    # the library's A/B switches (mtg_linear_std.hip, mtg_time_std.hip,
+    # mtg_tube.hip) force the runtime-S kernels
+    std_rt = os.environ.get("MTG_STD_RUNTIME_S", "").startswith("1")
+    tube_rt = os.environ.get("MTG_TUBE_RUNTIME_S", "").startswith("1")
+    wave_ok = (N, r, D) == (10, 4, 3) and 2 <= S <= 16 and not std_rt
     if wl == "linear":
         k = plan.kernel_for_batch(B)
         if k == "standard":
-            return ("linear_wave_kernel" if (N, r, D) == (10, 4, 3) and 2 <= S <= 16 else
-                    "linear_std_kernel")
+            return "linear_wave_kernel" if wave_ok else "linear_std_kernel"
         return {"lane": "linear_lane_kernel", "lane_pair": "linear_lane2_kernel",
                 "generic": "linear_solve_kernel"}[k]
     if wl == "extrema":
         return "soft_cost_kernel" if B < 4096 else "max_magnitude_kernel"
     if wl == "time":
-        return ("time_optimize_wave_kernel" if (N, r, D) == (10, 4, 3) and 2 <= S <= 16 else
-                "time_optimize_std_kernel")
+        return "time_optimize_wave_kernel" if wave_ok else "time_optimize_std_kernel"
     if wl in ("tube", "time-qcqp"):
-        return "tube_solve_s_kernel" if N == 10 and 2 <= S <= 16 else "tube_solve_kernel"
+        return ("tube_solve_s_kernel" if N == 10 and 2 <= S <= 16 and not tube_rt else
+                "tube_solve_kernel")
     return {"sample": "sample_kernel", "collision": "coll_walk_kernel"}[wl]
 
 
@@ -275,16 +279,20 @@ def load_pmc_traffic(key, kernel_ms):
     return None
 
 
-def load_sq_executed(config_key):
+def load_sq_executed(config_key, kernel_ms):
     """Executed FP64 FLOP per trajectory (SQ instruction counts x active
     lanes, tools/sq_summary.py) from the committed profiles/sq_executed.json,
-    for the workload/batch/kernel key, if measured."""
+    for the workload/batch/kernel key, if measured on this build: like the
+    traffic entries, only when the pass's kernel time (avg_ns, from the same
+    build's kernel-trace pass) is within 15 % of this run's."""
     path = os.path.join(REPO, "profiles", "sq_executed.json")
     try:
         with open(path) as f:
             entry = json.load(f).get(config_key)
-        if entry:
-            return entry["executed_f64_flop_per_trajectory"], entry["source"]
+        if entry and entry.get("avg_ns"):
+            ratio = entry["avg_ns"] * 1e-6 / kernel_ms
+            if 0.85 <= ratio <= 1.15:
+                return entry["executed_f64_flop_per_trajectory"], entry["source"]
     except (OSError, ValueError, KeyError):
         pass
     return None, None
@@ -309,9 +317,10 @@ def linear_flops(N, D, S, nf, np_):
             + 2 * np_ ** 2 * D + 2 * N ** 2 * D * S + D * S * (2 * N ** 2 + 2 * N))
 
 
-def config_name(wl, B, world, S):
+def config_name(wl, B, world, S, global_batch=None):
+    global_batch = B * world if global_batch is None else global_batch
     if wl == "linear" and S == 10:
-        if B * world == 65536:
+        if global_batch == 65536:
             return f"C4: 65536 x 10-segment sharded {world} way(s)"
         if world == 1 and B == 1024:
             return "C2: 1024 x 10-segment linear solve"
@@ -390,16 +399,23 @@ def main():
     import torch
     import torch.distributed as dist
 
+    spin_note = None
     if args.sync == "spin":
         # Before the first HIP call of the process: the host polls for
-        # completion instead of sleeping on an interrupt.  Torch's runtime is
-        # the one in the process (libmtg_hip.so resolves to it by soname).
+        # completion instead of sleeping on an interrupt.  The flag must go
+        # to the runtime torch uses, so it is resolved from torch's own
+        # library directory (importing torch does not initialise HIP).
         import ctypes
-        hip = ctypes.CDLL("libamdhip64.so.7")
-        hip.hipSetDevice(ctypes.c_int(int(os.environ.get("LOCAL_RANK", "0"))))
-        rc = hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+        import glob
+        import torch
+        cands = sorted(glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib",
+                                              "libamdhip64.so*")))
+        hip = ctypes.CDLL(cands[0] if cands else "libamdhip64.so")
+        rc = hip.hipSetDevice(ctypes.c_int(int(os.environ.get("LOCAL_RANK", "0"))))
+        rc = rc or hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
         if rc != 0:
-            print(f"bench: hipSetDeviceFlags(spin) returned {rc}", file=sys.stderr)
+            print(f"bench: setting spin-wait failed (HIP {rc})", file=sys.stderr)
+            sys.exit(2)
 
     import mav_tube_trajectory_generation_amd as mtg
 
@@ -436,10 +452,19 @@ def main():
 
     N, D, r, S = 10, 3, 4, args.segments
     wl = args.workload
-    B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "time-qcqp": 1024,
-                       "sample": 1024, "extrema": 1024, "collision": 4096}[wl]
-    from mav_tube_trajectory_generation_amd.shard import select_best_device, shard_range
-    global_batch = B * world
+    from mav_tube_trajectory_generation_amd.shard import SelectionPipeline, shard_range
+    # --gpus N > 1 without --batch: BASELINE config 4, a 65 536-trajectory
+    # global batch in contiguous shards (8 192 per GPU at N = 8): total work
+    # fixed as N grows ("strong").  N = 1 stays config 2 (1024), the
+    # configuration the metric is quoted on.  --batch B: B per GPU ("weak").
+    c4_default = wl == "linear" and world > 1 and args.batch is None and S == 10
+    if c4_default:
+        global_batch = 65536
+        B = shard_range(global_batch, world, rank)[1]
+    else:
+        B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "time-qcqp": 1024,
+                           "sample": 1024, "extrema": 1024, "collision": 4096}[wl]
+        global_batch = B * world
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
     mask, fixed, times, pos = mtg.generate_random_problems(N, D, S, B, seed0=seed0)
     ctx = mtg.Context(local_rank)
@@ -455,23 +480,28 @@ def main():
     metric_base = "trajectories/sec (10-seg, N=10, 3D minimum-snap) at 1/2/4/8 MI355X"
     coll = None  # collision workload inputs (also the CPU baseline's)
     extra_cfg = {}
+    pipe = None  # linear: the selection pipeline (its side stream joins in end_steps)
+
+    def end_steps():
+        if pipe is not None:
+            pipe.drain()
 
     if wl == "linear":
         out = plan.solve(fixed_d, times_d, free=False)
         shard_start = shard_range(global_batch, world, rank)[0]
-        sel_ws = plan.select_workspace(B, dev)
+        # The selection step (shard argmin, RCCL all-gather of the triples,
+        # global argmin) runs on a side stream, off the solve's critical path:
+        # step k + 1's solve overlaps step k's selection, two output sets
+        # alternate (shard.SelectionPipeline).  On one GPU without a process
+        # group the all-gather and the global argmin of one triple are the
+        # identity.
+        pipe = SelectionPipeline(
+            lambda o: plan.solve(fixed_d, times_d, free=False, out=o),
+            [out, plan.solve(fixed_d, times_d, free=False)], global_batch, shard_start, rank,
+            dev, use_dist=select)
 
         def step_selected():
-            # The solve with the shard's argmin (lane kernels: per-workgroup
-            # partials from the solve's epilogue, one reduction launch), then
-            # (world > 1) the RCCL all-gather of the triples and the global
-            # argmin kernel.  On one GPU without a process group the
-            # all-gather and the global argmin of one triple are the identity:
-            # the shard's triple is the winner.
-            plan.solve_select(fixed_d, times_d, shard_start, rank, sel_ws, out=out)
-            if select:
-                return select_best_device(None, global_batch, local_triple=out["triple"])
-            return out["triple"]
+            return pipe.step()
 
         def step():
             if select:
@@ -661,23 +691,25 @@ def main():
         unit = "trajectories/s"
         units_per_step = B
 
-    # World 1: the K timed steps are captured into one HIP graph and replayed,
-    # so launches are back to back (no host launch gaps) and the per-step
-    # device time is (end - start) / K from two HIP events on the launch
-    # stream.  World > 1 (linear): the step, RCCL all-gather included, is
-    # captured the same way after eager warm-up steps (the communicator is
-    # initialised outside the capture); if the capture fails the loop runs
-    # eagerly with one event pair per step.
+    # The K timed steps are captured into one HIP graph and replayed, so
+    # launches are back to back (no host launch gaps) and the per-step device
+    # time is (end - start) / K from two HIP events on the launch stream.
+    # World > 1 (linear): the step, RCCL all-gather included, is captured the
+    # same way after eager warm-up steps (the communicator is initialised
+    # outside the capture).  A failed capture is fatal (exit 3) on every
+    # rank: the line never carries eager timings unless --no-graph asks for
+    # them.
     use_graph = not args.no_graph
-    graph_note = ""
     graphs = {}
     if select:  # communicator set up and first collectives outside any capture
         with stdout_to_stderr():
             for _ in range(max(args.warmup, 2)):
                 step()
+            end_steps()
             torch.cuda.synchronize(dev)
             dist.barrier()
     if use_graph:
+        capture_error = None
         try:  # capture only: nothing executes (no collective runs) here
             for name, sizes in (("warmup", [args.warmup]),
                                 ("timed", graph_chunks(args.steps, args.graph_head,
@@ -688,29 +720,31 @@ def main():
                     with torch.cuda.graph(g):
                         for _ in range(n):
                             step()
+                        end_steps()
                     gl.append(g)
                 graphs[name] = gl
-        except Exception as exc:  # capture unsupported here: eager launches
-            use_graph = False
-            graph_note = f" (graph capture failed: {type(exc).__name__}; eager)"
-            torch.cuda.synchronize(dev)
-            print(f"bench: graph capture failed, eager: {exc}", file=sys.stderr)
+        except Exception as exc:
+            capture_error = f"{type(exc).__name__}: {exc}"
         if world > 1:
-            # Every rank must take the same path, or a replayed all-gather on
-            # one rank would wait for an eager one that never comes.
-            ok = torch.tensor([1.0 if use_graph else 0.0], dtype=torch.float64, device=dev)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if ok.item() < 0.5 and use_graph:
-                use_graph = False
-                graph_note = " (graph capture failed on another rank; eager)"
-        if use_graph:
-            for g in graphs["warmup"]:
-                g.replay()
-        else:
-            graphs = {}
-    if not use_graph:
+            # Every rank takes the same path (a replayed all-gather on one
+            # rank would wait for a collective that never comes).
+            ok = torch.tensor([0.0 if capture_error else 1.0], dtype=torch.float64, device=dev)
+            try:
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if ok.item() < 0.5 and capture_error is None:
+                    capture_error = "graph capture failed on another rank"
+            except Exception as exc:
+                capture_error = capture_error or f"capture agreement failed: {exc}"
+        if capture_error is not None:
+            print(f"bench: graph capture failed ({capture_error}); not publishing eager "
+                  "timings (pass --no-graph to time eager launches)", file=sys.stderr)
+            sys.exit(3)
+        for g in graphs["warmup"]:
+            g.replay()
+    else:
         for _ in range(args.warmup):
             step()
+        end_steps()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -737,6 +771,7 @@ def main():
             ev[i][0].record(stream)
             step()
             ev[i][1].record(stream)
+        end_steps()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -755,27 +790,38 @@ def main():
     if wl == "linear" and not select:
         for _ in range(3):
             step_selected()
+        end_steps()
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        try:
-            gs = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gs):
-                for _ in range(args.steps):
-                    step_selected()
+        if use_graph:
+            try:
+                gs = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gs):
+                    for _ in range(args.steps):
+                        step_selected()
+                    end_steps()
+            except Exception as exc:
+                print(f"bench: graph capture of the selection step failed ({exc})",
+                      file=sys.stderr)
+                sys.exit(3)
+            gs.replay()  # warm replay, then the timed one
+            torch.cuda.synchronize(dev)
             e0.record(stream)
             gs.replay()
             e1.record(stream)
-        except Exception:  # eager fallback
-            torch.cuda.synchronize(dev)
+        else:
             e0.record(stream)
             for _ in range(args.steps):
                 step_selected()
+            end_steps()
             e1.record(stream)
         torch.cuda.synchronize(dev)
         selection_ms = e0.elapsed_time(e1) / args.steps
 
-    counted = useful_per_step if useful_per_step is not None else units_per_step
-    total_units = counted * args.steps * world
+    if useful_per_step is not None:
+        total_units = useful_per_step * args.steps * world
+    else:  # every rank's shard (shards differ by one when world does not divide)
+        total_units = units_per_step * global_batch // B * args.steps
     value = total_units / elapsed
     alg_bytes = bytes_per_traj * B
     gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
@@ -783,7 +829,7 @@ def main():
     dev_kernel = device_kernel(wl, plan, B, N, D, r, S)
     traffic = load_pmc_traffic(f"{config_key}:{dev_kernel}", kernel_ms)
     timing = ("HIP events around one graph replay of the K steps, / K" if use_graph else
-              "HIP event pair per step, mean") + graph_note
+              "HIP event pair per step, mean (--no-graph)")
     hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
            "alg_bytes_per_launch": alg_bytes, "traffic": traffic}
     if flops_per_step is not None:
@@ -801,16 +847,16 @@ def main():
     # Executed FP64 work beside the dense-equivalent count: the kernel's SQ
     # FP64 instruction counts x active lanes (a committed rocprofv3 pass at
     # this workload, batch and kernel) over this run's kernel time.
-    ex_flop, ex_src = load_sq_executed(f"{config_key}:{dev_kernel}")
+    ex_flop, ex_src = load_sq_executed(f"{config_key}:{dev_kernel}", kernel_ms)
     if ex_flop is not None:
         ex_tf = ex_flop * B / (kernel_ms * 1e-3) / 1e12
         roof["executed"] = {"achieved": ex_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                             "frac": ex_tf / FP64_PEAK_TFLOPS,
                             "flop_per_trajectory": ex_flop, "source": ex_src}
     if select and wl == "linear":
-        roof["kernel_timing"] += ("; per-step device time includes the selection (solve with "
-                                  "per-workgroup partials, shard reduction launch, RCCL "
-                                  "all-gather, global argmin kernel)")
+        roof["kernel_timing"] += ("; per-step device time includes the selection (shard "
+                                  "argmin, RCCL all-gather, global argmin) on a side stream "
+                                  "overlapping the next step's solve")
 
     if rank == 0:
         cpu = None
@@ -821,7 +867,8 @@ def main():
                 cpu = cpu_baseline(wl, N, D, r, S, args.cpu_seconds, args.cpu_reps,
                                    sample_args=(0.01, 4) if wl == "sample" else None)
             cpu["unit"] = unit
-        cfg = {"workload": config_name(wl, B, world, S), "global_batch": global_batch,
+        cfg = {"workload": config_name(wl, B, world, S, global_batch),
+               "global_batch": global_batch,
                "kernel": plan.kernel_for_batch(B) if wl == "linear" else None,
                "batch_per_gpu": B, "segments": S, "N": N, "D": D, "r": r,
                "parallelism": f"shard{world}",
@@ -842,7 +889,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if c4_default else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (main.cpp's vertices, starts perturbed around the device tube "

@@ -642,8 +642,11 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
  * all_trajectories_ (one trajectory pushed per objective evaluation,
  * nonlinear_impl:1244, 1482; read by getAllTrajectories,
  * polynomial_optimization_nonlinear.h:316-331): x_history (device,
- * nullable) B x max_evals x nx, row k = the point of the (k+1)-th counted
- * evaluation; rows at or past evals[b] are not written. */
+ * nullable) B x max_evals x nv doubles, where nv is the number of
+ * optimisation variables (NOT the grid's nx): nv = D * n_free in mode 0
+ * (x = d_p), S + D * n_free in mode 1 (x = [T; d_p]), n_free from
+ * mtg_plan_counts.  Row k = the point of the (k+1)-th counted evaluation;
+ * rows at or past evals[b] are not written. */
 int mtg_coll_optimize_trace(const mtg_plan* plan, int64_t B, int mode, const double* fixed_vals,
                             double* x_io, const double* times, const double* lower,
                             const double* upper, const double* initial_step,

@@ -393,8 +393,10 @@ class LinearPlan:
         optimizeFreeConstraintsAndCollision / ...AndTime with NLopt
         replaced); near_field as coll_cost.  Returns dict(x, cost, evals,
         result, status, terms); with history=True also x_history
-        (B x max_evals x nx, the evaluated points in order, rows past evals
-        unset: mtg_coll_optimize_trace)."""
+        (B x max_evals x nv, nv = the number of optimisation variables,
+        _n_vars(mode): D * n_free in mode 0, S + D * n_free in mode 1; the
+        evaluated points in order, rows past evals unset:
+        mtg_coll_optimize_trace)."""
         import torch
         B = self._coll_inputs(fixed_vals, x0, times, occupancy, mode)
         _check_field(near_field, occupancy)
@@ -682,10 +684,13 @@ def magnitude_candidates(coeffs, times, derivative, max_candidates=None):
     coeffs [B, S, D, N], times [B, S] (float64, CUDA).  Returns a dict of
     time / value [B, S, C] and count [B, S] int32: per segment t = 0, T and
     the real roots of d/dt |p^(derivative)|^2 in [0, T] ascending, with
-    |p^(derivative)| at each; entries past count are unset.  C defaults to
-    2 (N - derivative) - 1, which always suffices.  count is clamped to C
-    (the stored entries); found [B, S] is the number the search found, which
-    exceeds count only when a smaller max_candidates truncated the list.
+    |p^(derivative)| at each.  C defaults to 2 (N - derivative) - 1, which
+    always suffices.  count is the number of candidates the search found, as
+    the C ABI returns it (a count above C means a smaller max_candidates
+    truncated the list); stored [B, S] = min(count, C) is the number of
+    valid entries, and entries past it are unset.  (Round 4 had briefly
+    clamped count and moved the found number to a "found" key; that
+    alias is kept for callers written against it.)
     """
     import torch
     B, S, D, N = coeffs.shape
@@ -700,8 +705,8 @@ def magnitude_candidates(coeffs, times, derivative, max_candidates=None):
                                          _ptr(out["time"]), _ptr(out["value"]),
                                          _ptr(out["count"]), _stream(dev)),
           "mtg_magnitude_candidates")
+    out["stored"] = torch.clamp(out["count"], max=C)
     out["found"] = out["count"]
-    out["count"] = torch.clamp(out["found"], max=C)
     return out
 
 

@@ -34,6 +34,15 @@ using mtg::PlanDev;
 
 int from_hip(hipError_t e) { return e == hipSuccess ? MTG_OK : MTG_ERR_HIP; }
 
+// The launch helpers report hipGetLastError() after their launches, and the
+// runtime keeps the last error of ANY failed HIP call on this thread (the
+// caller's, or another library's) until it is read.  Every entry point
+// therefore clears that slot first, so a stale error is never returned as
+// this call's MTG_ERR_HIP.  Round 4's failed graph captures were exactly
+// that: an experiment's event-record call failed inside the capture and the
+// next mtg_linear_solve reported it ("Graph capture").
+void clear_stale_error() { (void)hipGetLastError(); }
+
 bool valid_N(int N) { return N >= 4 && N <= 12 && N % 2 == 0; }
 
 // Constant tables for (N, r), computed in long double (layout: H(1) N*N,
@@ -171,6 +180,7 @@ const char* mtg_status_string(int status) {
 int mtg_version(void) { return 100; }
 
 int mtg_ctx_create(int device, mtg_ctx** out) {
+  clear_stale_error();
   if (!out) return MTG_ERR_INVALID_ARG;
   *out = nullptr;
   int n = 0;
@@ -184,6 +194,7 @@ int mtg_ctx_create(int device, mtg_ctx** out) {
 }
 
 int mtg_ctx_destroy(mtg_ctx* ctx) {
+  clear_stale_error();
   if (!ctx) return MTG_ERR_INVALID_ARG;
   (void)hipSetDevice(ctx->device);
   for (auto& kv : ctx->tables) (void)hipFree(kv.second);
@@ -195,6 +206,7 @@ int mtg_ctx_device(const mtg_ctx* ctx) { return ctx ? ctx->device : MTG_ERR_INVA
 
 int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fixed_mask,
                     mtg_plan** out) {
+  clear_stale_error();
   if (!ctx || !out || !fixed_mask) return MTG_ERR_INVALID_ARG;
   *out = nullptr;
   if (!valid_N(N) || D < 1 || D > mtg::kMaxD || r < 0 || r > N / 2 - 1 || S < 1)
@@ -264,6 +276,7 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fix
 }
 
 int mtg_plan_destroy(mtg_plan* plan) {
+  clear_stale_error();
   if (!plan) return MTG_ERR_INVALID_ARG;
   (void)hipFree(plan->d_slots);
   (void)hipFree(plan->d_free_map);
@@ -273,6 +286,7 @@ int mtg_plan_destroy(mtg_plan* plan) {
 }
 
 int mtg_plan_set_kernel(mtg_plan* plan, int kernel) {
+  clear_stale_error();
   if (!plan || kernel < MTG_KERNEL_AUTO || kernel > MTG_KERNEL_LANE_PAIR)
     return MTG_ERR_INVALID_ARG;
   if (kernel == MTG_KERNEL_STANDARD && !plan->dev.std_pattern) return MTG_ERR_UNSUPPORTED;
@@ -286,17 +300,20 @@ int mtg_plan_set_kernel(mtg_plan* plan, int kernel) {
 }
 
 int mtg_plan_kernel(const mtg_plan* plan) {
+  clear_stale_error();
   if (!plan) return MTG_ERR_INVALID_ARG;
   if (plan->dev.kernel >= MTG_KERNEL_LANE) return plan->dev.kernel;
   return mtg::use_std_kernel(plan->dev) ? MTG_KERNEL_STANDARD : MTG_KERNEL_GENERIC;
 }
 
 int mtg_plan_kernel_for_batch(const mtg_plan* plan, int64_t B) {
+  clear_stale_error();
   if (!plan || B < 0) return MTG_ERR_INVALID_ARG;
   return mtg::linear_kernel_for_batch(plan->dev, B);
 }
 
 int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free) {
+  clear_stale_error();
   if (!plan) return MTG_ERR_INVALID_ARG;
   if (n_fixed) *n_fixed = plan->dev.nf;
   if (n_free) *n_free = plan->dev.np;
@@ -306,6 +323,7 @@ int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free) {
 int mtg_linear_solve(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                      const double* times, double* coeffs, double* cost, double* free_vals,
                      int32_t* status, void* stream) {
+  clear_stale_error();
   if (!plan || B < 0 || B > 0x7fffffff || !times || !coeffs) return MTG_ERR_INVALID_ARG;
   if (plan->dev.nf > 0 && !fixed_vals) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
@@ -317,6 +335,7 @@ int mtg_linear_solve(const mtg_plan* plan, int64_t B, const double* fixed_vals,
 int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                           const double* times, double* coeffs, double* cost,
                           double* free_vals, int32_t* status) {
+  clear_stale_error();
   if (!plan || B < 0 || !times || !coeffs) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   const PlanDev& pl = plan->dev;
@@ -354,6 +373,7 @@ int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_v
 int mtg_coeffs_from_constraints(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                                 const double* free_vals, const double* times, double* coeffs,
                                 double* cost, int32_t* status, void* stream) {
+  clear_stale_error();
   if (!plan || B < 0 || B > 0x7fffffff || !times || !coeffs) return MTG_ERR_INVALID_ARG;
   if ((plan->dev.nf > 0 && !fixed_vals) || (plan->dev.np > 0 && !free_vals))
     return MTG_ERR_INVALID_ARG;
@@ -367,6 +387,7 @@ int mtg_sample_trajectories(int N, int D, int S, int64_t B, const double* coeffs
                             const double* times, double t_start, double t_end, double dt,
                             int n_max, int max_derivative, double* samples,
                             double* sample_times, int32_t* n_samples, void* stream) {
+  clear_stale_error();
   if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > mtg::kMaxSampleS || B < 0 ||
       B > 65535 || n_max < 0 || max_derivative < 0 || max_derivative >= N || !(dt > 0.0) ||
       !(t_start >= 0.0))
@@ -382,6 +403,7 @@ int mtg_magnitude_candidates(int N, int D, int S, int64_t B, const double* coeff
                              const double* times, int derivative, int max_candidates,
                              double* cand_time, double* cand_value, int32_t* n_candidates,
                              void* stream) {
+  clear_stale_error();
   if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || B < 0 || derivative < 0 ||
       derivative > mtg::kMaxExtremaDerivative || N - derivative - 1 <= 0 || max_candidates < 2)
     return MTG_ERR_INVALID_ARG;
@@ -396,6 +418,7 @@ int mtg_magnitude_candidates(int N, int D, int S, int64_t B, const double* coeff
 int mtg_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                       const double* times, int derivative, double* max_time,
                       double* max_value, int32_t* max_segment, void* stream) {
+  clear_stale_error();
   if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > 256 || B < 0 || derivative < 0 ||
       derivative > mtg::kMaxExtremaDerivative || N - derivative - 1 <= 0)
     return MTG_ERR_INVALID_ARG;
@@ -419,6 +442,7 @@ int mtg_collision_cost(const mtg_plan* plan, int64_t B, const double* coeffs,
                        const double* times, const float* occupancy, int nx, int ny, int nz,
                        const mtg_collision_params* params, double* cost, int32_t* collision,
                        double* grad_coeffs, double* grad_free, void* stream) {
+  clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || plan->dev.D != 3) return MTG_ERR_INVALID_ARG;
   const mtg_collision_params& p = *params;
   if (!valid_collision_params(p, nx, ny, nz)) return MTG_ERR_INVALID_ARG;
@@ -435,6 +459,7 @@ int mtg_min_max_magnitude(int N, int D, int S, int64_t B, const double* coeffs,
                           const double* times, int derivative, double* min_time,
                           double* min_value, int32_t* min_segment, double* max_time,
                           double* max_value, int32_t* max_segment, void* stream) {
+  clear_stale_error();
   if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > 256 || B < 0 || derivative < 0 ||
       derivative > mtg::kMaxExtremaDerivative || N - derivative - 1 <= 0)
     return MTG_ERR_INVALID_ARG;
@@ -451,6 +476,7 @@ int mtg_soft_constraint_cost(int N, int D, int S, int64_t B, const double* coeff
                              const double* times, int n_constraints, const int* derivatives,
                              const double* limits, double weight, double maximum_cost,
                              double* maxima, double* cost, void* stream) {
+  clear_stale_error();
   if (!valid_N(N) || D < 1 || D > mtg::kMaxD || S < 1 || S > 256 || B < 0 ||
       n_constraints < 1 || n_constraints > mtg::kMaxSoftConstraints || !derivatives ||
       !limits)
@@ -495,6 +521,7 @@ static bool valid_coll_params(const mtg_plan* plan, int mode, const mtg_coll_par
 
 int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
                                  const mtg_coll_params* params, int optimize) {
+  clear_stale_error();
   if (B < 0 || !valid_coll_params(plan, mode, params)) return MTG_ERR_INVALID_ARG;
   if (mtg::coll_problems(plan->dev, B, mode, *params) > 0x7fffffff) return MTG_ERR_INVALID_ARG;
   return static_cast<int64_t>(
@@ -502,12 +529,14 @@ int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
 }
 
 int64_t mtg_coll_field_bytes(int nx, int ny, int nz) {
+  clear_stale_error();
   if (nx < 0 || ny < 0 || nz < 0) return MTG_ERR_INVALID_ARG;
   return static_cast<int64_t>(nx) * ny * nz * mtg::kFieldSlots * sizeof(uint16_t);
 }
 
 int mtg_coll_field(const float* occupancy, int nx, int ny, int nz,
                    const mtg_collision_params* params, uint16_t* field, void* stream) {
+  clear_stale_error();
   if (!params || !valid_collision_params(*params, nx, ny, nz) ||
       !mtg::coll_field_supported(params->box_side))
     return MTG_ERR_INVALID_ARG;
@@ -523,6 +552,7 @@ int mtg_coll_cost(const mtg_plan* plan, int64_t B, int mode, const double* fixed
                   const double* raise_ref,
                   double* cost, double* grad, double* terms, int32_t* collision,
                   int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
+  clear_stale_error();
   if (B < 0 || !valid_coll_params(plan, mode, params) ||
       !valid_collision_params(params->coll, nx, ny, nz))
     return MTG_ERR_INVALID_ARG;
@@ -544,6 +574,7 @@ int mtg_coll_optimize_trace(const mtg_plan* plan, int64_t B, int mode, const dou
                             int max_evals, double* cost, int32_t* evals, int32_t* result,
                             int32_t* status, double* terms, double* x_history, void* workspace,
                             size_t workspace_bytes, void* stream) {
+  clear_stale_error();
   if (B < 0 || max_evals < 1 || !valid_coll_params(plan, mode, params) ||
       !valid_collision_params(params->coll, nx, ny, nz))
     return MTG_ERR_INVALID_ARG;
@@ -566,6 +597,7 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
                       const mtg_coll_params* params, int max_evals,
                       double* cost, int32_t* evals, int32_t* result, int32_t* status,
                       double* terms, void* workspace, size_t workspace_bytes, void* stream) {
+  clear_stale_error();
   return mtg_coll_optimize_trace(plan, B, mode, fixed_vals, x_io, times, lower, upper,
                                  initial_step, occupancy, nx, ny, nz, near_field, params,
                                  max_evals, cost, evals, result, status, terms, nullptr, workspace,
@@ -574,6 +606,7 @@ int mtg_coll_optimize(const mtg_plan* plan, int64_t B, int mode, const double* f
 
 int mtg_select_local(const double* costs, int64_t count, int64_t start, int rank, double* out,
                      void* stream) {
+  clear_stale_error();
   if (count < 0 || start < 0 || rank < 0 || !out || (count > 0 && !costs))
     return MTG_ERR_INVALID_ARG;
   return from_hip(mtg::launch_select_local(costs, count, start, rank, out,
@@ -591,6 +624,7 @@ static size_t select_ws_layout(const mtg_plan* plan, int64_t B, size_t* off_cost
 }
 
 int64_t mtg_select_workspace_bytes(const mtg_plan* plan, int64_t B) {
+  clear_stale_error();
   if (!plan || B < 0) return MTG_ERR_INVALID_ARG;
   size_t a, b;
   return static_cast<int64_t>(select_ws_layout(plan, B, &a, &b));
@@ -601,6 +635,7 @@ int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed
                             double* free_vals, int32_t* status, int64_t start, int rank,
                             double* triple, void* workspace, size_t workspace_bytes,
                             void* stream) {
+  clear_stale_error();
   if (!plan || B < 0 || B > 0x7fffffff || start < 0 || rank < 0 || !triple)
     return MTG_ERR_INVALID_ARG;
   const hipStream_t st = static_cast<hipStream_t>(stream);
@@ -621,6 +656,7 @@ int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed
 }
 
 int mtg_select_global(const double* triples, int world, double* out, void* stream) {
+  clear_stale_error();
   if (world < 1 || !triples || !out) return MTG_ERR_INVALID_ARG;
   return from_hip(mtg::launch_select_global(triples, world, out,
                                             static_cast<hipStream_t>(stream)));
@@ -628,6 +664,7 @@ int mtg_select_global(const double* triples, int world, double* out, void* strea
 
 int mtg_segment_matrices(mtg_ctx* ctx, int N, int r, int64_t n, const double* times,
                          double* Q, double* A, double* Ainv, double* H, void* stream) {
+  clear_stale_error();
   if (!ctx || !valid_N(N) || r < 0 || r > N / 2 - 1 || n < 0 || (n && !times))
     return MTG_ERR_INVALID_ARG;
   if (n == 0) return MTG_OK;
@@ -661,6 +698,7 @@ static bool valid_soft(const mtg_plan* plan, const mtg_time_params* p, bool allo
 int mtg_free_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                   const double* free_vals, const double* times, const mtg_time_params* params,
                   int mode, double* cost, double* grad, int32_t* status, void* stream) {
+  clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times || mode < 0 || mode > 1)
     return MTG_ERR_INVALID_ARG;
   if ((plan->dev.nf > 0 && !fixed_vals) || (plan->dev.np > 0 && !free_vals))
@@ -679,6 +717,7 @@ int mtg_time_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_
                            double* free_io, double* times_io, const mtg_time_params* params,
                            int max_evals, double* cost, int32_t* evals, int32_t* status,
                            void* stream) {
+  clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if ((plan->dev.nf > 0 && !fixed_vals) || plan->dev.np < 1 || !free_io)
@@ -698,6 +737,7 @@ int mtg_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       double* free_io, const double* times, const double* lower,
                       const double* upper, const mtg_time_params* params, int max_evals,
                       double* cost, int32_t* evals, int32_t* status, void* stream) {
+  clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if ((plan->dev.nf > 0 && !fixed_vals) || plan->dev.np < 1 || !free_io)
@@ -715,6 +755,7 @@ int mtg_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
 int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                   const double* times, const mtg_time_params* params, double* cost,
                   double* grad, int32_t* status, void* stream) {
+  clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times) return MTG_ERR_INVALID_ARG;
   if (params->grad_mode < 0 || params->grad_mode > 2) return MTG_ERR_INVALID_ARG;
   if (params->grad_mode && !(params->increment > 0)) return MTG_ERR_INVALID_ARG;
@@ -728,6 +769,7 @@ int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       double* times_io, const mtg_time_params* params, int max_evals,
                       double* cost, int32_t* evals, int32_t* solves, int32_t* status,
                       void* stream) {
+  clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
@@ -739,6 +781,7 @@ int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
 }
 
 int mtg_tube_num_constraints(int N, int S) {
+  clear_stale_error();
   if (!valid_N(N) || S < 1) return MTG_ERR_INVALID_ARG;
   return (S - 1) + S * (N - 2) + 2 * S * (N - 2);
 }
@@ -770,6 +813,7 @@ static int tube_args(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double*
 int mtg_tube_residuals(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* positions,
                        const double* fixed_vals, const double* times_cp, const double* times,
                        const double* radii, const double* x, double* resid, void* stream) {
+  clear_stale_error();
   mtg::TubeArgs a;
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_cp, times, radii, &a);
   if (rc) return rc;
@@ -782,6 +826,7 @@ int mtg_tube_solve(mtg_ctx* ctx, int N, int r, int S, int64_t B, const double* p
                    const double* fixed_vals, const double* times_cp, const double* times,
                    const double* radii, double tol, int max_iter, double* x, double* coeffs,
                    double* cost, int32_t* iters, int32_t* status, void* stream) {
+  clear_stale_error();
   mtg::TubeArgs a;
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_cp, times, radii, &a);
   if (rc) return rc;
@@ -806,6 +851,7 @@ static bool valid_tube_time_params(int N, int S, const mtg_time_params* p) {
 
 int64_t mtg_tube_time_workspace_bytes(int N, int S, int64_t B, const mtg_time_params* params,
                                       int optimize) {
+  clear_stale_error();
   if (!valid_N(N) || S < 2 || B < 0 || !valid_tube_time_params(N, S, params))
     return MTG_ERR_INVALID_ARG;
   if (!tube_grid_ok(S, mtg::tube_time_problems(S, B, *params, optimize != 0)))
@@ -819,6 +865,7 @@ int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B, const doubl
                        const mtg_time_params* params, double* cost, double* grad,
                        int32_t* status, void* workspace, size_t workspace_bytes,
                        void* stream) {
+  clear_stale_error();
   mtg::TubeArgs a;
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_cp, times, radii, &a);
   if (rc) return rc;
@@ -842,6 +889,7 @@ int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                            const mtg_time_params* params, int max_evals, double* cost,
                            int32_t* evals, int32_t* status, void* workspace,
                            size_t workspace_bytes, void* stream) {
+  clear_stale_error();
   mtg::TubeArgs a;
   // times_cp = the initial times (read before the first write of times_io).
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_io, times_io, radii, &a);
@@ -860,6 +908,7 @@ int mtg_generate_random_problems(int N, int D, int S, int64_t B, uint64_t seed0,
                                  double pos_bound, double v_max, double a_max,
                                  uint8_t* fixed_mask, double* fixed_vals, double* times,
                                  double* positions) {
+  clear_stale_error();
   using namespace mav_trajectory_generation;
   if (!valid_N(N) || D < 1 || S < 1 || B < 0 || !(pos_bound > 0) || !(v_max > 0) ||
       !(a_max > 0))

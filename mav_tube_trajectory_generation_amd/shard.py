@@ -119,6 +119,78 @@ def select_best_device(local_costs, global_batch, group=None, local_triple=None)
     return allv[w]
 
 
+class SelectionPipeline:
+    """The multi-GPU step with the selection off the solve's critical path.
+
+    Step k solves into output set k % depth on the current stream; a side
+    stream then reduces that set's costs to the shard's triple
+    (mtg_select_local), all-gathers the triples (RCCL) and takes the global
+    argmin (mtg_select_global), while the current stream already runs step
+    k + 1's solve.  The selection never feeds a later solve; the only
+    ordering is that solve k + depth, which overwrites output set k % depth,
+    waits for selection k to have read it.  Every call sequence ends with
+    drain() (the side stream joins the current one), so a captured graph or
+    an eager batch of steps is closed and `best` is final after it.
+
+    solve_into(out): enqueue one solve writing out["cost"] (and the rest of
+    the output set) on the current stream.  use_dist=False (one process, no
+    process group): the all-gather and the global argmin of one triple are
+    the identity, so the shard's triple is the winner."""
+
+    def __init__(self, solve_into, outs, global_batch, start, rank, device, use_dist=True,
+                 group=None):
+        self.solve_into = solve_into
+        self.outs = list(outs)
+        self.global_batch = int(global_batch)
+        self.start = int(start)
+        self.rank = int(rank)
+        self.use_dist = use_dist
+        self.group = group
+        self.side = torch.cuda.Stream(device)
+        self.triples = [torch.empty(3, dtype=torch.float64, device=device) for _ in self.outs]
+        self.best = torch.empty(3, dtype=torch.float64, device=device)
+        self.k = 0
+        self._read = [None] * len(self.outs)  # event: selection done reading set i
+        self._pending = False  # side stream forked from the current one since drain()
+
+    def step(self):
+        lib, check, ptr, stream = _hip()
+        main = torch.cuda.current_stream()
+        i = self.k % len(self.outs)
+        if self._read[i] is not None:
+            main.wait_event(self._read[i])
+        o = self.outs[i]
+        self.solve_into(o)
+        solved = torch.cuda.Event()
+        solved.record(main)
+        self.side.wait_event(solved)
+        with torch.cuda.stream(self.side):
+            cost = o["cost"]
+            t = self.triples[i]
+            check(lib.mtg_select_local(ptr(cost), cost.numel(), self.start, self.rank, ptr(t),
+                                       stream(cost.device)), "mtg_select_local")
+            if self.use_dist:
+                self.best = select_best_device(None, self.global_batch, self.group,
+                                               local_triple=t)
+            else:
+                self.best = t
+            done = torch.cuda.Event()
+            done.record(self.side)
+        self._read[i] = done
+        self._pending = True
+        self.k += 1
+        return self.best
+
+    def drain(self):
+        """Join the side stream into the current one (end of a captured
+        sequence or of an eager batch of steps)."""
+        if self._pending:
+            torch.cuda.current_stream().wait_stream(self.side)
+        self._pending = False
+        self._read = [None] * len(self.outs)
+        return self.best
+
+
 def select_best(local_costs, global_batch, group=None):
     """Global argmin over all shards (NaN costs never win).  Returns
     (global index, cost, owner rank) as Python numbers; identical on every

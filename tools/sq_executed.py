@@ -26,6 +26,7 @@ def main():
             summ = json.load(f)
         data[key] = {"executed_f64_flop_per_trajectory": summ["executed_f64_flop_per_trajectory"],
                      "valu_lane_utilisation": summ.get("valu_lane_utilisation"),
+                     "avg_ns": summ.get("avg_ns"),
                      "source": os.path.relpath(src, REPO)}
     with open(path, "w") as f:
         json.dump(data, f, indent=1, sort_keys=True)

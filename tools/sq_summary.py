@@ -56,6 +56,16 @@ def main():
             flop_instr * 64.0 * out["valu_lane_utilisation"] / units)
     out["kernel"] = kernel
     out["trajectories_per_launch"] = units
+    # the kernel's average duration in the same build's kernel-trace pass:
+    # bench.py uses the entry only for a run within 15 % of it
+    stats = os.path.join(base, "trace", "run_kernel_stats.csv")
+    try:
+        with open(stats) as f:
+            rows = [r for r in csv.DictReader(f) if kernel in r["Name"]]
+        if rows:
+            out["avg_ns"] = float(rows[0]["AverageNs"])
+    except (OSError, KeyError, ValueError):
+        pass
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 4:
         with open(sys.argv[4], "w") as f:
