@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--kernel", default="auto",
                    choices=["auto", "generic", "standard", "lane", "lane_pair"],
                    help="linear-solve kernel (mtg_plan_set_kernel); auto picks by batch size")
+    p.add_argument("--optimizer", choices=["fd", "sbplx"], default="fd",
+                   help="time workload: the device optimiser (fd: projected central-difference "
+                        "descent; sbplx: LN_SBPLX, the reference's default algorithm)")
     p.add_argument("--soft", action="store_true",
                    help="time workload: soft constraints max|v| <= 3, max|a| <= 5 in the objective")
     p.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
@@ -154,7 +157,7 @@ def cpu_baseline_collision(N, r, coll, seconds, reps):
     }
 
 
-def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None):
+def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None, optimizer="fd"):
     """Oracle (reference-faithful C++ port, oracle/mtg_oracle.cpp, built
     -O3 -march=x86-64-v3) on a bounded sample of the same workload, on the GPU
     host: 1 thread and all cores (std::thread pool over independent
@@ -195,7 +198,9 @@ def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None):
         what = "solves (setupFromVertices + solveLinear + computeCost)"
     else:
         kind, pi, pd, rad, what = {
-            "time": (1, 50, 0.0, None, "50-evaluation time optimisations (orc_time_optimize)"),
+            "time": ((6, 50, 0.0, None, "50-evaluation LN_SBPLX time optimisations "
+                      "(orc_time_optimize_sbplx)") if optimizer == "sbplx" else
+                     (1, 50, 0.0, None, "50-evaluation time optimisations (orc_time_optimize)")),
             "tube": (2, 0, 0.0, radii, "tube QCQP solves (oracle primal-dual IPM, tol 1e-10)"),
             "time-qcqp": (5, 0, 0.0, radii,
                           "time-objective evaluations with the QCQP inner solve and the central-"
@@ -310,9 +315,46 @@ def tube_flops_per_iter(N, S):
     return m * (2 * v * v + 2 * v) + m * v * v + (S - 1) * (b ** 3 / 3 + b ** 3 + 2 * b ** 3)
 
 
+def linear_flops_alg(N, D, S, r):
+    """FP64 operations of the algorithm the linear kernels run, per solve
+    ("FLOP counts"): 11 036 at S = 10, N = 10, D = 3, r = 4.
+    Symbols as SURVEY.md 8(d); M = N/2, MF = M - 1 free derivatives per
+    intermediate vertex (the standard pattern), TRI = MF (MF + 1) / 2.
+      powers     S (2N + M - 4): T^e chains + one reciprocal per segment
+      assembly   (S-1) (3 TRI + MF^2 + 5 MF + 5 D MF): A_v = H11(v-1) + H00(v)
+                 (two table x power products per entry), C_v = H01(v), the
+                 row coefficients and b_v (time-scaled H, no 4N^3 S GEMMs)
+                 + 2 (MF^2 + 2 D MF^2): the fixed end vertices' share of b
+      LDL^T      (S-2) [MF^3/3 + 2 MF^2 (MF + D) + 2 MF TRI + 2 MF^2 D]:
+                 factor, solve for the coupling and right-hand-side columns,
+                 symmetric Schur and right-hand-side updates, per block step;
+                 + the middle block MF^3/3 + 2 MF^2 D + TRI + D MF
+                 + (S-2) 2 MF^2 D back substitution
+      recovery   S D (N-2 + M + 2 nnz - M + N-1): f = e T^(j mod M), h =
+                 A(1)^-1 f over its nnz = M N structural non-zeros of the
+                 lower half, c = T^-i h
+      cost       S D ((N-r)(N-r+1) + 2 (N-r) + 2): 0.5 c^T Q c as the
+                 quadratic form of h with the constant weights"""
+    M = N // 2
+    MF = M - 1
+    TRI = MF * (MF + 1) // 2
+    powers = S * (2 * N + M - 4)
+    assembly = (S - 1) * (3 * TRI + MF * MF + 5 * MF + 5 * D * MF) + 2 * (MF * MF + 2 * D * MF * MF)
+    ldlt = 0.0
+    if S >= 2:
+        step = MF ** 3 / 3 + 2 * MF * MF * (MF + D) + 2 * MF * TRI + 2 * MF * MF * D
+        ldlt = ((S - 2) * (step + 2 * MF * MF * D)
+                + MF ** 3 / 3 + 2 * MF * MF * D + TRI + D * MF)
+    recovery = S * D * ((N - 2) + M + (2 * M * N - M) + (N - 1))
+    cost = S * D * ((N - r) * (N - r + 1) + 2 * (N - r) + 2)
+    return powers + assembly + ldlt + recovery + cost
+
+
 def linear_flops(N, D, S, nf, np_):
     """SURVEY.md 8(d) dense algorithmic FLOP count of one linear solve (81 032
-    at S = 10); the kernel's banded / time-scaled route does fewer."""
+    at S = 10): every entry of the dense blocks.  Kept beside the count above
+    as roofline.dense_equiv_frac; the kernels' time-scaled, banded route does
+    about 7x fewer operations, so this one is not a bound."""
     return (4 * N ** 3 * S + N ** 2 * S + np_ ** 3 / 3 + 2 * np_ * nf * D
             + 2 * np_ ** 2 * D + 2 * N ** 2 * D * S + D * S * (2 * N ** 2 + 2 * N))
 
@@ -475,6 +517,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     bound = "fp64_vector"
     flops_per_step = None   # algorithmic FP64 work of one step (None: not FP64-bound)
+    dense_per_step = None   # SURVEY 8(d)'s dense-equivalent count, where it differs
     flop_note = None
     useful_per_step = None  # units that count towards `value` (converged solves)
     metric_base = "trajectories/sec (10-seg, N=10, 3D minimum-snap) at 1/2/4/8 MI355X"
@@ -513,15 +556,18 @@ def main():
         metric = metric_base
         unit = "trajectories/s"
         units_per_step = B
-        flops_per_step = linear_flops(N, D, S, nf, plan.n_free) * B
-        flop_note = "SURVEY 8(d) dense count per solve x B"
+        flops_per_step = linear_flops_alg(N, D, S, r) * B
+        dense_per_step = linear_flops(N, D, S, nf, plan.n_free) * B
+        flop_note = (f"the kernels' algorithm, {linear_flops_alg(N, D, S, r):.0f} FLOP per solve "
+                     "(bench.linear_flops_alg, DESIGN 6) x B")
     elif wl == "time":
         max_evals = 50
 
         soft = [(1, 3.0), (2, 5.0)] if args.soft else None
 
         def step():
-            return plan.time_optimize(fixed_d, times_d, max_evals=max_evals, soft=soft)
+            return plan.time_optimize(fixed_d, times_d, max_evals=max_evals, soft=soft,
+                                      optimizer=args.optimizer)
 
         probe = step()
         torch.cuda.synchronize(dev)
@@ -529,13 +575,20 @@ def main():
         evals_mean = float(probe["evals"].float().mean().item())
         bytes_per_traj = (D * nf + S) * 8 + (S + 2) * 8
         metric = "time-allocation optimisations/sec (4096 traj x 50 evals, 10-seg, N=10, 3D)"
+        if args.optimizer == "sbplx":
+            metric += ", LN_SBPLX"
+            res_np = probe["result"].cpu().numpy()
+            extra_cfg = {"optimizer": "LN_SBPLX (device restatement)",
+                         "results": {int(k): int(v) for k, v in
+                                     zip(*np.unique(res_np, return_counts=True))}}
         if args.soft:
             metric += " + soft max|v|<=3, max|a|<=5"
             bound = "fp64_vector (soft: extremum search not counted)"
         unit = "trajectories/s"
         units_per_step = B
-        flops_per_step = linear_flops(N, D, S, nf, plan.n_free) * solves
-        flop_note = (f"dense solve count x {solves} inner solves per launch (measured, gradient "
+        flops_per_step = linear_flops_alg(N, D, S, r) * solves
+        dense_per_step = linear_flops(N, D, S, nf, plan.n_free) * solves
+        flop_note = (f"the solve's algorithm count x {solves} inner solves per launch (measured, gradient "
                      f"points included; {solves / B:.1f} per trajectory, {evals_mean:.1f} "
                      "counted evaluations)")
     elif wl == "sample":
@@ -838,6 +891,12 @@ def main():
                 "frac": tfl / FP64_PEAK_TFLOPS, "traffic": traffic,
                 "alg_flops_per_launch": flops_per_step, "flop_count": flop_note,
                 "hbm": hbm}
+        if dense_per_step is not None:
+            # SURVEY 8(d)'s dense count over the same time (not a bound: the
+            # kernels skip the structural zeros and the H-block GEMMs)
+            roof["dense_equiv_frac"] = (dense_per_step / (kernel_ms * 1e-3) / 1e12
+                                        / FP64_PEAK_TFLOPS)
+            roof["dense_flops_per_launch"] = dense_per_step
     else:
         roof = {"bound": "hbm", **{k: hbm[k] for k in ("achieved", "peak", "unit", "frac")},
                 "traffic": traffic, "alg_bytes_per_launch": alg_bytes}
@@ -865,7 +924,8 @@ def main():
                 cpu = cpu_baseline_collision(N, r, coll, args.cpu_seconds, args.cpu_reps)
             else:
                 cpu = cpu_baseline(wl, N, D, r, S, args.cpu_seconds, args.cpu_reps,
-                                   sample_args=(0.01, 4) if wl == "sample" else None)
+                                   sample_args=(0.01, 4) if wl == "sample" else None,
+                                   optimizer=args.optimizer)
             cpu["unit"] = unit
         cfg = {"workload": config_name(wl, B, world, S, global_batch),
                "global_batch": global_batch,

@@ -16,12 +16,15 @@
 //     With the build's extension field `solve_time_with_qcqp` the callback
 //     re-solves the tube QCQP instead, as the fork does (solveQCQP at
 //     nonlinear_impl:892; mtg_tube_time_cost / mtg_tube_time_optimize);
-//   * NLopt (LN_SBPLX, nonlinear_impl:95-107) is absent; the optimiser is the
-//     device-side projected descent of mtg_time_optimize with the same
-//     bounds [0.1, 2 T0] (:350-378), initial relative step 0.1 (the
-//     initial_stepsize_rel default) and evaluation budget max_iterations
-//     (NLopt maxeval, :101).  Optimiser trajectories therefore differ from NLopt's
-//     (parity unpinned); the callback value is pinned;
+//   * NLopt (LN_SBPLX, nonlinear_impl:95-107) is absent.  kOptimizeTime with
+//     the default algorithm LN_SBPLX runs the device restatement of NLopt's
+//     Subplex (mtg_time_optimize_ex, optimizer 1: bounds [0.1, 2 T0],
+//     :350-378, initial step initial_stepsize_rel T0, maxeval
+//     max_iterations, :101, ftol f_rel / f_abs, :97-98); any other algorithm
+//     runs the projected central-difference descent (optimizer 0), and so
+//     does the QCQP-inner-solve form.  NLopt itself is absent, so optimiser
+//     parity is pinned to the oracle restatement only; the
+//     callback value is pinned;
 //   * the collision cost reads a dense occupancy grid (setOccupancyGrid) in
 //     place of the supereight octree (setOctree).  kOptimizeFreeConstraints
 //     AndCollision and kOptimizeFreeConstraintsAndCollisionAndTime (the
@@ -308,15 +311,17 @@ class PolynomialOptimizationNonLinear {
     d_t.upload(times);
     const mtg_time_params p = timeParams(0, true);
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
-    internal::checkStatus(mtg_time_optimize(planOf(), 1, d_df.get(), d_t.get(), &p, budget,
-                                            d_cost.get(), d_ev.get(), nullptr, d_st.get(),
-                                            nullptr),
-                          "mtg_time_optimize");
+    internal::DeviceBuffer<int32_t> d_res(1);
+    internal::checkStatus(mtg_time_optimize_ex(planOf(), 1, d_df.get(), d_t.get(), &p, budget,
+                                               d_cost.get(), d_ev.get(), nullptr, d_res.get(),
+                                               d_st.get(), nullptr),
+                          "mtg_time_optimize_ex");
     internal::synchronize();
     d_t.download(times.data(), S);
-    int32_t evals = 0, st = 0;
+    int32_t evals = 0, st = 0, res = 0;
     d_ev.download(&evals, 1);
     d_st.download(&st, 1);
+    d_res.download(&res, 1);
     linear_.updateSegmentTimes(times);
     linear_.solveLinear();
     double tot = 0.0;
@@ -332,7 +337,7 @@ class PolynomialOptimizationNonLinear {
     for (const auto& c : soft_)
       optimization_info_.maxima[c.first] =
           linear_.computeMaximumOfMagnitude(c.first, nullptr);
-    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? res : -1;  // nlopt_result
     optimization_info_.optimization_time =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return optimization_info_.stopping_reason;
@@ -807,7 +812,9 @@ class PolynomialOptimizationNonLinear {
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
     double J = 0.0;
     int32_t evals = 0;
-    const int st = poly_opt_.optimizeTimeQCQP(timeParams(2), budget, &times, &J, &evals);
+    mtg_time_params tp = timeParams(2);
+    tp.optimizer = 0;  // the QCQP form runs the descent (mtg_tube_time_optimize)
+    const int st = poly_opt_.optimizeTimeQCQP(tp, budget, &times, &J, &evals);
     poly_opt_.updateSegmentTimes(times);
     poly_opt_.solveQCQP();
     qcqp_time_optimized_ = true;
@@ -1039,7 +1046,16 @@ class PolynomialOptimizationNonLinear {
   // hard_ok: the entry point takes hard constraints (mtg_time_cost /
   // mtg_time_optimize); elsewhere hard constraints are dropped with a warning.
   mtg_time_params timeParams(int grad_mode, bool hard_ok = false) const {
-    mtg_time_params p;
+    mtg_time_params p{};
+    // LN_SBPLX (the default) is restated on the device; it takes no
+    // inequality constraints, so use_soft_constraints = false leaves the
+    // magnitude constraints without effect, as NLopt does
+    // (nonlinear_impl:861-872 registers them only for algorithms taking them)
+    const bool sbplx = params_.algorithm == nlopt::LN_SBPLX;
+    p.optimizer = sbplx ? 1 : 0;
+    p.f_rel = params_.f_rel;
+    p.f_abs = params_.f_abs;
+    p.initial_stepsize_rel = params_.initial_stepsize_rel;
     p.time_penalty = params_.time_penalty;
     p.increment = params_.increment_time;
     p.w_d = params_.weights.w_d;
@@ -1049,8 +1065,9 @@ class PolynomialOptimizationNonLinear {
     if (hard && !hard_ok && !soft_.empty())
       internal::warn("hard magnitude constraints are only applied by kOptimizeTime with the "
                      "linear inner solve; ignored here");
-    p.n_soft = (!hard || hard_ok) ? static_cast<int>(soft_.size()) : 0;
-    p.hard_constraints = hard && hard_ok ? 1 : 0;
+    const bool take_hard = hard && hard_ok && !sbplx;
+    p.n_soft = (!hard || take_hard) ? static_cast<int>(soft_.size()) : 0;
+    p.hard_constraints = take_hard ? 1 : 0;
     p.hard_tolerance = params_.inequality_constraint_tolerance;
     for (int c = 0; c < 8; ++c) {
       p.soft_derivative[c] = c < p.n_soft ? soft_[c].first : 0;

@@ -219,6 +219,20 @@ typedef struct mtg_time_params {
                                1: hard inequalities (use_soft_constraints =
                                false, nonlinear_impl:861-872) */
   double hard_tolerance;    /* ::inequality_constraint_tolerance (0.1) */
+  /* The optimiser of mtg_time_optimize (round 5; a zero-filled struct keeps
+   * the earlier behaviour):
+   *   0  projected central-difference descent (below);
+   *   1  LN_SBPLX, the reference's default algorithm (nlopt::LN_SBPLX,
+   *      polynomial_optimization_nonlinear.h:61): NLopt's Subplex with its
+   *      bounded Nelder-Mead restated on the device (mtg_sbplx_device.h),
+   *      gradient-free, stopping at max_evals evaluations or at f_rel /
+   *      f_abs (NLopt's ftol_rel / ftol_abs, nonlinear_impl:97-98; <= 0
+   *      disables).  Soft constraints enter the objective; hard constraints
+   *      are rejected (NLopt's SBPLX takes no inequality constraints). */
+  int optimizer;
+  double f_rel;                /* ::f_rel (0.05) */
+  double f_abs;                /* ::f_abs (-1: disabled) */
+  double initial_stepsize_rel; /* ::initial_stepsize_rel (0.1); <= 0 means 0.1 */
 } mtg_time_params;
 
 int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
@@ -228,9 +242,10 @@ int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
 /* Batched segment-time optimisation.  Replaces optimizeTime
  * (nonlinear_impl:332-397): bounds [0.1, 2 T0] per segment (:350-358,
  * 375-378), `max_evals` objective evaluations per trajectory (NLopt maxeval,
- * :101).  NLopt's SBPLX is not available; the optimiser is a projected
- * gradient method with backtracking on the grad_mode 2 gradient, run entirely
- * on the device (one workgroup per trajectory, no host round trips).
+ * :101).  params->optimizer 0: a projected gradient method with
+ * backtracking on the grad_mode 2 gradient; 1: LN_SBPLX (the reference's
+ * default, restated: NLopt itself is absent).  Both run entirely on the
+ * device (one workgroup per trajectory, no host round trips).
  *   times_io   B x S  in: initial times T0, out: optimised times
  *   cost       B      final objective
  *   evals      B      objective evaluations used (nullable)
@@ -241,6 +256,17 @@ int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                       double* times_io, const mtg_time_params* params,
                       int max_evals, double* cost, int32_t* evals,
                       int32_t* solves, int32_t* status, void* stream);
+/* The same with the optimiser's stopping reason per trajectory (result, B,
+ * nullable): NLopt's nlopt_result codes, as optimizeTime returns them
+ * (nlopt::opt::optimize, nonlinear_impl:386): 3 FTOL_REACHED, 4 XTOL_REACHED
+ * (the Subplex / Nelder-Mead simplex collapsed), 5 MAXEVAL_REACHED.  With
+ * optimizer 0 the descent reports 5 when it used max_evals and 4 when its
+ * step vanished.  times_io is the best point and cost its objective (NLopt's
+ * x and opt_f). */
+int mtg_time_optimize_ex(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                         double* times_io, const mtg_time_params* params, int max_evals,
+                         double* cost, int32_t* evals, int32_t* solves, int32_t* result,
+                         int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * Free-derivative objectives of PolynomialOptimizationNonLinear (the NLopt

@@ -95,16 +95,24 @@ class TimeParams(ctypes.Structure):
                 ("grad_mode", ctypes.c_int), ("n_soft", ctypes.c_int),
                 ("soft_derivative", ctypes.c_int * 8), ("soft_limit", ctypes.c_double * 8),
                 ("soft_weight", ctypes.c_double), ("soft_maximum_cost", ctypes.c_double),
-                ("hard_constraints", ctypes.c_int), ("hard_tolerance", ctypes.c_double)]
+                ("hard_constraints", ctypes.c_int), ("hard_tolerance", ctypes.c_double),
+                ("optimizer", ctypes.c_int), ("f_rel", ctypes.c_double),
+                ("f_abs", ctypes.c_double), ("initial_stepsize_rel", ctypes.c_double)]
+
+OPTIMIZERS = {"fd": 0, "descent": 0, "sbplx": 1}
 
 
 def make_time_params(time_penalty=500.0, increment=0.1, w_d=0.1, w_t=1.0, grad_mode=0,
                      soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12, hard=False,
-                     hard_tolerance=0.1):
+                     hard_tolerance=0.1, optimizer="fd", f_rel=0.05, f_abs=-1.0,
+                     initial_stepsize_rel=0.1):
     """soft: list of (derivative, maximum_value) magnitude constraints
     (addMaximumMagnitudeConstraint), evaluated as soft costs, or with
     hard=True as hard inequalities max - value <= hard_tolerance
-    (use_soft_constraints = false)."""
+    (use_soft_constraints = false).  optimizer: "fd" (projected
+    central-difference descent) or "sbplx" (LN_SBPLX, the reference's
+    default) with NLopt's f_rel / f_abs and initial_stepsize_rel
+    (NonlinearOptimizationParameters defaults)."""
     p = TimeParams(time_penalty, increment, w_d, w_t, grad_mode)
     soft = list(soft or [])
     if len(soft) > 8:
@@ -117,6 +125,12 @@ def make_time_params(time_penalty=500.0, increment=0.1, w_d=0.1, w_t=1.0, grad_m
     p.soft_maximum_cost = soft_maximum_cost
     p.hard_constraints = 1 if hard else 0
     p.hard_tolerance = hard_tolerance
+    if optimizer not in OPTIMIZERS:
+        raise MTGError(f"optimizer must be one of {sorted(OPTIMIZERS)}")
+    p.optimizer = OPTIMIZERS[optimizer]
+    p.f_rel = f_rel
+    p.f_abs = f_abs
+    p.initial_stepsize_rel = initial_stepsize_rel
     return p
 
 
@@ -184,6 +198,9 @@ SIGNATURES = {
     "mtg_time_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp,
                                          ctypes.POINTER(TimeParams), ctypes.c_int, _vp, _vp,
                                          _vp, _vp, _vp]),
+    "mtg_time_optimize_ex": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp,
+                                            ctypes.POINTER(TimeParams), ctypes.c_int, _vp, _vp,
+                                            _vp, _vp, _vp, _vp]),
     "mtg_tube_num_constraints": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "mtg_tube_residuals": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -218,10 +218,15 @@ class LinearPlan:
 
     def time_optimize(self, fixed_vals, times, max_evals=50, time_penalty=500.0, increment=0.1,
                       w_d=0.1, w_t=1.0, soft=None, soft_weight=100.0, hard=False,
-                      hard_tolerance=0.1):
+                      hard_tolerance=0.1, optimizer="fd", f_rel=0.05, f_abs=-1.0,
+                      initial_stepsize_rel=0.1):
         """Optimise segment times in place on a copy; returns dict(times, cost,
-        evals, solves, status); solves = inner solves run (gradient points
-        included)."""
+        evals, solves, result, status); solves = inner solves run (gradient
+        points included), result = the nlopt_result stopping code
+        (mtg_time_optimize_ex).  optimizer "fd" (projected central-difference
+        descent) or "sbplx" (LN_SBPLX, the reference's default algorithm,
+        with f_rel / f_abs / initial_stepsize_rel as
+        NonlinearOptimizationParameters)."""
         import torch
         B = times.shape[0]
         _require(times, (B, self.S), "times")
@@ -231,13 +236,17 @@ class LinearPlan:
         cost = torch.empty(B, dtype=torch.float64, device=dev)
         evals = torch.empty(B, dtype=torch.int32, device=dev)
         solves = torch.empty(B, dtype=torch.int32, device=dev)
+        result = torch.empty(B, dtype=torch.int32, device=dev)
         status = torch.empty(B, dtype=torch.int32, device=dev)
         p = make_time_params(time_penalty, increment, w_d, w_t, 2, soft, soft_weight,
-                             hard=hard, hard_tolerance=hard_tolerance)
-        check(lib().mtg_time_optimize(self._h, B, _ptr(fixed_vals), _ptr(t), ctypes.byref(p),
-                                      max_evals, _ptr(cost), _ptr(evals), _ptr(solves),
-                                      _ptr(status), _stream(dev)), "mtg_time_optimize")
-        return dict(times=t, cost=cost, evals=evals, solves=solves, status=status)
+                             hard=hard, hard_tolerance=hard_tolerance, optimizer=optimizer,
+                             f_rel=f_rel, f_abs=f_abs, initial_stepsize_rel=initial_stepsize_rel)
+        check(lib().mtg_time_optimize_ex(self._h, B, _ptr(fixed_vals), _ptr(t), ctypes.byref(p),
+                                         max_evals, _ptr(cost), _ptr(evals), _ptr(solves),
+                                         _ptr(result), _ptr(status), _stream(dev)),
+              "mtg_time_optimize_ex")
+        return dict(times=t, cost=cost, evals=evals, solves=solves, result=result,
+                    status=status)
 
     def free_cost(self, fixed_vals, free_vals, times, mode=0, time_penalty=500.0, soft=None,
                   soft_weight=100.0, grad=True):

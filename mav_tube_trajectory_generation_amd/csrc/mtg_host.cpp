@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "mtg_internal.h"
+#include "mtg_sbplx_device.h"
 #include "mav_tube_trajectory_generation_amd/vertex.h"
 
 struct mtg_ctx {
@@ -765,19 +766,33 @@ int mtg_time_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                                         status, static_cast<hipStream_t>(stream)));
 }
 
-int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
-                      double* times_io, const mtg_time_params* params, int max_evals,
-                      double* cost, int32_t* evals, int32_t* solves, int32_t* status,
-                      void* stream) {
+int mtg_time_optimize_ex(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                         double* times_io, const mtg_time_params* params, int max_evals,
+                         double* cost, int32_t* evals, int32_t* solves, int32_t* result,
+                         int32_t* status, void* stream) {
   clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
   if (!valid_soft(plan, params, true)) return MTG_ERR_INVALID_ARG;
+  if (params->optimizer != 0 && params->optimizer != 1) return MTG_ERR_INVALID_ARG;
+  // LN_SBPLX takes no inequality constraints (NLopt rejects them), and its
+  // LDS state holds at most kMaxN segments
+  if (params->optimizer == 1 &&
+      ((params->hard_constraints && params->n_soft > 0) || plan->dev.S > mtg::sbplx::kMaxN))
+    return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   return from_hip(mtg::launch_time_optimize(plan->dev, B, fixed_vals, times_io, *params,
-                                            max_evals, cost, evals, solves, status,
+                                            max_evals, cost, evals, solves, result, status,
                                             static_cast<hipStream_t>(stream)));
+}
+
+int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                      double* times_io, const mtg_time_params* params, int max_evals,
+                      double* cost, int32_t* evals, int32_t* solves, int32_t* status,
+                      void* stream) {
+  return mtg_time_optimize_ex(plan, B, fixed_vals, times_io, params, max_evals, cost, evals,
+                              solves, nullptr, status, stream);
 }
 
 int mtg_tube_num_constraints(int N, int S) {
@@ -890,6 +905,8 @@ int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                            int32_t* evals, int32_t* status, void* workspace,
                            size_t workspace_bytes, void* stream) {
   clear_stale_error();
+  // the QCQP-inner-solve optimiser is the projected descent only
+  if (params && params->optimizer != 0) return MTG_ERR_UNSUPPORTED;
   mtg::TubeArgs a;
   // times_cp = the initial times (read before the first write of times_io).
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_io, times_io, radii, &a);

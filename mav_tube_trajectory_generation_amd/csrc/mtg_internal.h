@@ -86,8 +86,7 @@ hipError_t launch_time_cost_std(const PlanDev& pl, int64_t B, const double* df,
 hipError_t launch_time_optimize_std(const PlanDev& pl, int64_t B, const double* df,
                                     double* times, const mtg_time_params& p, int max_evals,
                                     double* cost, int32_t* evals, int32_t* solves,
-                                    int32_t* status,
-                                    hipStream_t st);
+                                    int32_t* result, int32_t* status, hipStream_t st);
 size_t time_std_lds_bytes(int N, int S, int D, bool soft);
 
 // Free-derivative objectives and optimiser (mtg_free.hip).
@@ -122,8 +121,7 @@ hipError_t launch_time_cost(const PlanDev& pl, int64_t B, const double* df,
 hipError_t launch_time_optimize(const PlanDev& pl, int64_t B, const double* df,
                                 double* times, const mtg_time_params& p, int max_evals,
                                 double* cost, int32_t* evals, int32_t* solves,
-                                    int32_t* status,
-                                hipStream_t st);
+                                int32_t* result, int32_t* status, hipStream_t st);
 hipError_t launch_segment_matrices(int N, int r, int64_t n, const double* tab,
                                    const double* times, double* Q, double* A,
                                    double* Ainv, double* H, hipStream_t st);

@@ -8,6 +8,7 @@
 #include "mtg_device.h"
 #include "mtg_extrema_device.h"
 #include "mtg_internal.h"
+#include "mtg_sbplx_device.h"
 
 namespace mtg {
 
@@ -197,6 +198,12 @@ __device__ double objective_at(Traj<N>& t, const double* __restrict__ tab,
 __host__ __device__ inline size_t soft_cbuf_offset(const Layout& lay) {
   return (lay.bytes() + 15) / 16 * 16;
 }
+// The optimiser's LN_SBPLX state (mtg_sbplx_device.h) after everything else.
+__host__ __device__ inline size_t sbplx_state_offset(const Layout& lay, int S, int D, int N,
+                                                     bool soft) {
+  const size_t end = soft ? soft_cbuf_offset(lay) + sizeof(double) * S * D * N : lay.bytes();
+  return (end + 15) / 16 * 16;
+}
 
 // The reference's getCostAndGradientTime (grad_mode 1): with d held at the
 // base solution (dv), J_d(T') differs from J_d(T) only in segment n's block
@@ -292,7 +299,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
     PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ times_io,
     mtg_time_params p, int max_evals, double* __restrict__ cost,
     int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ result_out, int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int S = pl.S, D = pl.D, nf = pl.nf;
   const double* tab = pl.tab;
@@ -313,14 +320,34 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   }
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
-  int phase = kBase, gi = 0, evals = 0, nsolve = 0;
+  int phase = kBase, gi = 0, evals = 0, nsolve = 0, res = 0;
   double f = 0.0, fv = 0.0, Jlo = 0.0, vlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   int fl = 0;
+  // LN_SBPLX (optimizer 1): the machine picks every point, lane 0 advances it
+  const bool sb = p.optimizer == 1;
+  auto* sbs = reinterpret_cast<sbplx::State*>(reinterpret_cast<char*>(smem) +
+                                              sbplx_state_offset(lay, S, D, N, kSoft));
+  sbplx::Machine mach{sbs};
+  if (sb) {
+    __syncthreads();
+    if (t.lane == 0)
+      mach.init(S, t.T(), p.initial_stepsize_rel > 0.0 ? p.initial_stepsize_rel : 0.1,
+                max_evals, p.f_rel, p.f_abs);
+    __syncthreads();
+  }
   while (phase != kDone) {
     double viol;
     const double J = objective_at<N, kSoft>(t, tab, p, cbuf, &viol);  // at T()
     ++nsolve;
+    if (sb) {
+      if (t.flag()[0] & 1) break;
+      __syncthreads();
+      if (t.lane == 0) mach.resume(J, t.T());
+      __syncthreads();
+      if (sbs->done) break;
+      continue;
+    }
     if (phase == kBase) {
       f = J;
       fv = viol;
@@ -382,11 +409,21 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   }
   fl = t.flag()[0];
   __syncthreads();
+  if (sb) {  // NLopt's x and opt_f: the best point and its value
+    for (int i = t.lane; i < S; i += kWave) Tcur[i] = sbs->x[i];
+    f = sbs->minf;
+    evals = sbs->nevals;
+    res = sbs->result;
+    __syncthreads();
+  } else {
+    res = evals >= max_evals ? sbplx::kMaxEval : sbplx::kXtol;
+  }
   for (int i = t.lane; i < S; i += kWave) times_io[b * S + i] = Tcur[i];
   if (t.lane == 0) {
     if (cost) cost[b] = (fl & 1) ? NAN : f;
     if (evals_out) evals_out[b] = evals;
     if (solves_out) solves_out[b] = nsolve;
+    if (result_out) result_out[b] = res;
     if (status)
       status[b] = (fl & 1) ? MTG_TRAJ_BAD_TIME
                            : ((fl & 2) ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
@@ -456,22 +493,23 @@ template <int N>
 static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* df,
                                     double* times, const mtg_time_params& p,
                                     int max_evals, double* cost, int32_t* evals,
-                                    int32_t* solves, int32_t* status, hipStream_t st) {
+                                    int32_t* solves, int32_t* result, int32_t* status,
+                                    hipStream_t st) {
   const Layout lay = make_layout(N, pl.S, pl.D);
   if (p.n_soft > 0) {
-    const size_t bytes = soft_cbuf_offset(lay) + sizeof(double) * pl.S * pl.D * N;
+    const size_t bytes = sbplx_state_offset(lay, pl.S, pl.D, N, true) + sbplx::kStateBytes;
     hipError_t e = prepare_lds(time_optimize_kernel<N, true>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_kernel<N, true>), dim3(static_cast<unsigned>(B)),
                        dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, solves,
-                       status);
+                       result, status);
   } else {
-    const size_t bytes = lay.bytes();
+    const size_t bytes = sbplx_state_offset(lay, pl.S, pl.D, N, false) + sbplx::kStateBytes;
     hipError_t e = prepare_lds(time_optimize_kernel<N, false>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_kernel<N, false>), dim3(static_cast<unsigned>(B)),
                        dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, solves,
-                       status);
+                       result, status);
   }
   return hipGetLastError();
 }
@@ -563,12 +601,12 @@ hipError_t launch_time_cost(const PlanDev& pl, int64_t B, const double* df,
 hipError_t launch_time_optimize(const PlanDev& pl, int64_t B, const double* df,
                                 double* times, const mtg_time_params& p, int max_evals,
                                 double* cost, int32_t* evals, int32_t* solves,
-                                int32_t* status, hipStream_t st) {
+                                int32_t* result, int32_t* status, hipStream_t st) {
   if (has_time_std(pl))
-    return launch_time_optimize_std(pl, B, df, times, p, max_evals, cost, evals, solves, status,
-                                    st);
+    return launch_time_optimize_std(pl, B, df, times, p, max_evals, cost, evals, solves, result,
+                                    status, st);
 #define CALL(n) \
-  launch_time_opt_n<n>(pl, B, df, times, p, max_evals, cost, evals, solves, status, st)
+  launch_time_opt_n<n>(pl, B, df, times, p, max_evals, cost, evals, solves, result, status, st)
   MTG_DISPATCH_N(pl.N, CALL)
 #undef CALL
 }

@@ -12,6 +12,7 @@
 #include <cstdlib>
 
 #include "mtg_extrema_device.h"
+#include "mtg_sbplx_device.h"
 #include "mtg_std_device.h"
 #include "mtg_wave_device.h"
 
@@ -143,13 +144,18 @@ __device__ inline void std_set_fd_point(double* T, const double* Tb, int S, int 
 
 }  // namespace
 
-size_t time_std_lds_bytes(int N, int S, int D, bool soft) {
+__host__ __device__ inline size_t time_std_bytes(int N, int S, int D, bool soft) {
   const size_t base = sizeof(double) * static_cast<size_t>(stdp::layout(N, S, D).n);
   // soft: the coefficients (S x D x N), then the soft searches' scratch and
   // maxima (ext_soft_maxima_wave).
   return soft ? (base + 15) / 16 * 16 +
                     sizeof(double) * (S * D * N + kMaxSoftConstraints * (N + 2))
               : base;
+}
+size_t time_std_lds_bytes(int N, int S, int D, bool soft) { return time_std_bytes(N, S, D, soft); }
+// The optimiser kernels add the LN_SBPLX machine's state after that.
+static size_t time_std_opt_lds_bytes(int N, int S, int D, bool soft) {
+  return (time_std_bytes(N, S, D, soft) + 15) / 16 * 16 + sbplx::kStateBytes;
 }
 
 // objectiveFunctionTime / getCostAndGradientTime on one trajectory per
@@ -248,7 +254,8 @@ __device__ __attribute__((always_inline)) void time_optimize_body(
     SV& sv, int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     double* __restrict__ times_io, const mtg_time_params& p, int max_evals,
     double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
-    int32_t* __restrict__ status, double* cbuf) {
+    int32_t* __restrict__ result_out, int32_t* __restrict__ status, double* cbuf,
+    sbplx::State* sbs) {
   const int64_t b = blockIdx.x;
   const int lane = sv.lane;
   const int nf = N + S - 1;
@@ -261,15 +268,33 @@ __device__ __attribute__((always_inline)) void time_optimize_body(
   for (int i = lane; i < S; i += kWave) T[i] = Tcur[i] = T0[i] = times_io[b * S + i];
   constexpr double kLower = 0.1;  // kOptimizationTimeLowerBound (:370)
   enum { kBase, kGrad, kTrial, kDone };
-  int phase = kBase, gi = 0, evals = 0, nsolve = 0;
+  int phase = kBase, gi = 0, evals = 0, nsolve = 0, res = 0;
   double f = 0.0, fv = 0.0, Jlo = 0.0, vlo = 0.0;
   double alpha = 0.1;  // initial_stepsize_rel (polynomial_optimization_nonlinear.h:55)
   bool bad = false, not_spd = false;
+  // LN_SBPLX (optimizer 1): the machine picks every point, lane 0 advances it
+  const bool sb = p.optimizer == 1;
+  sbplx::Machine mach{sbs};
+  if (sb) {
+    __syncthreads();
+    if (lane == 0)
+      mach.init(S, T, p.initial_stepsize_rel > 0.0 ? p.initial_stepsize_rel : 0.1, max_evals,
+                p.f_rel, p.f_abs);
+    __syncthreads();
+  }
   MTG_STAMP(460);
   while (phase != kDone) {
     double viol;
     const double J = std_objective<N, D, kSoft>(sv, tab, T, S, p, cbuf, &bad, &not_spd, &viol);
     ++nsolve;
+    if (sb) {
+      if (bad) break;
+      __syncthreads();
+      if (lane == 0) mach.resume(J, T);
+      __syncthreads();
+      if (sbs->done) break;
+      continue;
+    }
     if (phase == kBase) {
       f = J;
       fv = viol;
@@ -329,11 +354,21 @@ __device__ __attribute__((always_inline)) void time_optimize_body(
   }
   __syncthreads();
   MTG_STAMP(461);
+  if (sb) {  // NLopt's x and opt_f: the best point and its value
+    for (int i = lane; i < S; i += kWave) Tcur[i] = sbs->x[i];
+    f = sbs->minf;
+    evals = sbs->nevals;
+    res = sbs->result;
+    __syncthreads();
+  } else {
+    res = evals >= max_evals ? sbplx::kMaxEval : sbplx::kXtol;
+  }
   for (int i = lane; i < S; i += kWave) times_io[b * S + i] = Tcur[i];
   if (lane == 0) {
     if (cost) cost[b] = bad ? NAN : f;
     if (evals_out) evals_out[b] = evals;
     if (solves_out) solves_out[b] = nsolve;
+    if (result_out) result_out[b] = res;
     if (status)
       status[b] = bad ? MTG_TRAJ_BAD_TIME : (not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
   }
@@ -344,12 +379,15 @@ __global__ __launch_bounds__(kWave) void time_optimize_std_kernel(
     int S, const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     double* __restrict__ times_io, mtg_time_params p, int max_evals,
     double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ result_out, int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   StdSv<N, R, D> sv;
   sv.init(S, smem, tab);
+  auto* sbs = reinterpret_cast<sbplx::State*>(
+      reinterpret_cast<char*>(smem) + (time_std_bytes(N, S, D, kSoft) + 15) / 16 * 16);
   time_optimize_body<N, D, kSoft>(sv, S, tab, fixed_vals, times_io, p, max_evals, cost,
-                                  evals_out, solves_out, status, smem + (sv.L.n + 1) / 2 * 2);
+                                  evals_out, solves_out, result_out, status,
+                                  smem + (sv.L.n + 1) / 2 * 2, sbs);
 }
 
 // The same on the compile-time-S solver (N = 10, r = 4, D = 3, S = 2..16).
@@ -358,14 +396,16 @@ __global__ __launch_bounds__(kWave) void time_optimize_wave_kernel(
     const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     double* __restrict__ times_io, mtg_time_params p, int max_evals,
     double* __restrict__ cost, int32_t* __restrict__ evals_out, int32_t* __restrict__ solves_out,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ result_out, int32_t* __restrict__ status) {
   using G = wave::Geo<N, R, D, S>;
   constexpr int CB = kSoft ? S * D * N + kMaxSoftConstraints * (N + 2) : 0;
-  __shared__ __attribute__((aligned(16))) double sm[G::L_N + CB];
+  constexpr int SB = static_cast<int>(sbplx::kStateBytes / sizeof(double));
+  __shared__ __attribute__((aligned(16))) double sm[(G::L_N + CB + 1) / 2 * 2 + SB];
   wave::Solver<N, R, D, S> sv;
   sv.init(sm);
   time_optimize_body<N, D, kSoft>(sv, S, tab, fixed_vals, times_io, p, max_evals, cost,
-                                  evals_out, solves_out, status, sm + G::L_N);
+                                  evals_out, solves_out, result_out, status, sm + G::L_N,
+                                  reinterpret_cast<sbplx::State*>(sm + (G::L_N + CB + 1) / 2 * 2));
 }
 
 namespace {
@@ -401,21 +441,21 @@ hipError_t time_cost_nrd(const PlanDev& pl, int64_t B, const double* df, const d
 template <int N, int R, int D>
 hipError_t time_opt_nrd(const PlanDev& pl, int64_t B, const double* df, double* times,
                         const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
-                        int32_t* solves, int32_t* status, hipStream_t st) {
+                        int32_t* solves, int32_t* result, int32_t* status, hipStream_t st) {
   const bool soft = p.n_soft > 0;
-  const size_t bytes = time_std_lds_bytes(N, pl.S, D, soft);
+  const size_t bytes = time_std_opt_lds_bytes(N, pl.S, D, soft);
   if (soft) {
     hipError_t e = prepare_lds_std(time_optimize_std_kernel<N, R, D, true>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_std_kernel<N, R, D, true>),
                        dim3(static_cast<unsigned>(B)), dim3(kWave), bytes, st, pl.S, pl.tab,
-                       df, times, p, max_evals, cost, evals, solves, status);
+                       df, times, p, max_evals, cost, evals, solves, result, status);
   } else {
     hipError_t e = prepare_lds_std(time_optimize_std_kernel<N, R, D, false>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_std_kernel<N, R, D, false>),
                        dim3(static_cast<unsigned>(B)), dim3(kWave), bytes, st, pl.S, pl.tab,
-                       df, times, p, max_evals, cost, evals, solves, status);
+                       df, times, p, max_evals, cost, evals, solves, result, status);
   }
   return hipGetLastError();
 }
@@ -436,15 +476,15 @@ hipError_t time_cost_wave_s(const PlanDev& pl, int64_t B, const double* df, cons
 template <int S>
 hipError_t time_opt_wave_s(const PlanDev& pl, int64_t B, const double* df, double* times,
                            const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
-                           int32_t* solves, int32_t* status, hipStream_t st) {
+                           int32_t* solves, int32_t* result, int32_t* status, hipStream_t st) {
   if (p.n_soft > 0)
     hipLaunchKernelGGL((time_optimize_wave_kernel<10, 4, 3, S, true>),
                        dim3(static_cast<unsigned>(B)), dim3(kWave), 0, st, pl.tab, df, times, p,
-                       max_evals, cost, evals, solves, status);
+                       max_evals, cost, evals, solves, result, status);
   else
     hipLaunchKernelGGL((time_optimize_wave_kernel<10, 4, 3, S, false>),
                        dim3(static_cast<unsigned>(B)), dim3(kWave), 0, st, pl.tab, df, times, p,
-                       max_evals, cost, evals, solves, status);
+                       max_evals, cost, evals, solves, result, status);
   return hipGetLastError();
 }
 
@@ -503,13 +543,13 @@ hipError_t launch_time_cost_std(const PlanDev& pl, int64_t B, const double* df,
 hipError_t launch_time_optimize_std(const PlanDev& pl, int64_t B, const double* df,
                                     double* times, const mtg_time_params& p, int max_evals,
                                     double* cost, int32_t* evals, int32_t* solves,
-                                    int32_t* status, hipStream_t st) {
+                                    int32_t* result, int32_t* status, hipStream_t st) {
   if (!has_time_std(pl)) return hipErrorInvalidValue;
   if (use_time_wave(pl))
     MTG_TIME_WAVE_DISPATCH(time_opt_wave_s, pl, B, df, times, p, max_evals, cost, evals, solves,
-                           status, st)
-  MTG_TIME_STD_DISPATCH(time_opt_nrd, pl, B, df, times, p, max_evals, cost, evals, solves, status,
-                        st)
+                           result, status, st)
+  MTG_TIME_STD_DISPATCH(time_opt_nrd, pl, B, df, times, p, max_evals, cost, evals, solves, result,
+                        status, st)
 }
 
 }  // namespace mtg

@@ -7,6 +7,7 @@
 // standing in for Eigen::SparseQR<COLAMD>, per-segment coefficient recovery),
 // without the reference's unconditional stdout prints.
 #include "mtg_oracle.h"
+#include "orc_sbplx.h"
 
 #include <algorithm>
 #include <array>
@@ -1868,6 +1869,56 @@ static int timeOptimizeImpl(int N, int D, int r, int S, int K, const uint8_t* ma
   return 0;
 }
 
+// optimizeTime (nonlinear_impl:332-397) with the reference's default
+// algorithm: LN_SBPLX (orc_sbplx.cpp) on objectiveFunctionTime with the
+// linear inner solve, bounds [0.1, 2 T0] (:350-358, 375-378), initial step
+// initial_stepsize_rel T0 (:343-346), maxeval = max_iterations (:101),
+// ftol_rel = f_rel, ftol_abs = f_abs (:97-98).  times_io: in T0, out the
+// best point (NLopt's x); *cost its objective; history (nullable, max_evals
+// x S) the evaluated points in order.
+int orc_time_optimize_sbplx(int N, int D, int r, int S, int K, const uint8_t* mask,
+                            const double* vals, double* times_io, double time_penalty,
+                            int max_evals, double f_rel, double f_abs, double step_rel,
+                            int n_soft, const int* soft_derivatives, const double* soft_limits,
+                            double soft_weight, double soft_maximum_cost, double* cost,
+                            int* evals, int* result, double* history) {
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times_io, &lp);
+  if (rc) return rc;
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  int k = 0;
+  auto objective = [&](const double* tp) {
+    std::vector<double> t(tp, tp + S);
+    if (history && k < max_evals) std::memcpy(history + static_cast<size_t>(k) * S, tp, sizeof(double) * S);
+    ++k;
+    lp.updateSegmentTimes(t);
+    lp.solveLinear();
+    double total = 0.0;
+    for (double v : t) total += v;  // nonlinear_impl:2768-2774
+    double J = lp.computeCost() + total * total * time_penalty;
+    if (n_soft > 0) {
+      double c = 0.0;
+      orc_soft_constraint_cost(N, D, S, lp.coeffs.data(), t.data(), soft.n, soft.derivatives,
+                               soft.limits, soft.weight, soft.maximum_cost, nullptr, &c);
+      J += c;
+    }
+    return J;
+  };
+  std::vector<double> lb(S, 0.1), ub(S), step(S);
+  for (int i = 0; i < S; ++i) {
+    ub[i] = 2.0 * times_io[i];
+    step[i] = step_rel * times_io[i];
+  }
+  double minf = 0.0;
+  int nev = 0;
+  const int res = orc_sbplx_run(S, objective, lb.data(), ub.data(), times_io, &minf, step.data(),
+                                max_evals, f_rel, f_abs, &nev);
+  if (cost) *cost = minf;
+  if (evals) *evals = nev;
+  if (result) *result = res;
+  return 0;
+}
+
 int orc_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
                       const double* vals, double* times_io, double time_penalty,
                       double increment, int max_evals, double* cost, int* evals) {
@@ -2015,7 +2066,7 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                        const uint8_t* masks, const double* vals, const double* times,
                        const double* radii, int param_i, double param_d, int threads,
                        double min_seconds, int64_t* units, double* seconds) {
-  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 5) return -1;
+  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 6) return -1;
   if ((kind == 2 || kind == 5) && !radii) return -1;
   if (kind == 3 && !(param_d > 0.0)) return -1;
   const size_t mstride = static_cast<size_t>(S + 1) * K;
@@ -2050,6 +2101,17 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
         double c = 0.0;
         int ev = 0;
         if (orc_time_optimize(N, D, r, S, K, mk, vl, t.data(), 500.0, 0.1, param_i, &c, &ev))
+          failed = 1;
+        acc += c;
+        ++n;
+      } else if (kind == 6) {
+        // optimizeTime with LN_SBPLX (orc_time_optimize_sbplx), maxeval param_i
+        std::vector<double> t(tb, tb + S);
+        double c = 0.0;
+        int ev = 0, res = 0;
+        if (orc_time_optimize_sbplx(N, D, r, S, K, mk, vl, t.data(), 500.0, param_i, 0.05, -1.0,
+                                    0.1, 0, nullptr, nullptr, 100.0, 1.0e12, &c, &ev, &res,
+                                    nullptr))
           failed = 1;
         acc += c;
         ++n;

@@ -220,6 +220,20 @@ int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mas
                            const int* soft_derivatives, const double* soft_limits,
                            double soft_weight, double soft_maximum_cost, double* cost,
                            int* evals);
+// optimizeTime with the reference's default LN_SBPLX (orc_sbplx.cpp, NLopt
+// restated; impl/polynomial_optimization_nonlinear_impl.h:95-101, 332-397,
+// 877-945): bounds [0.1, 2 T0], initial step step_rel T0, maxeval
+// max_evals, ftol_rel f_rel, ftol_abs f_abs.  result: the nlopt_result code.
+int orc_time_optimize_sbplx(int N, int D, int r, int S, int K, const uint8_t* mask,
+                            const double* vals, double* times_io, double time_penalty,
+                            int max_evals, double f_rel, double f_abs, double step_rel,
+                            int n_soft, const int* soft_derivatives, const double* soft_limits,
+                            double soft_weight, double soft_maximum_cost, double* cost,
+                            int* evals, int* result, double* history);
+// The LN_SBPLX restatement on a fixed test objective (tests/test_sbplx.py).
+int orc_sbplx_test(int n, const double* lb, const double* ub, double* x, const double* xstep,
+                   int maxeval, double ftol_rel, double ftol_abs, double* minf, int* nevals,
+                   double* history);
 
 // CPU baseline for the other bench workloads, same cycling/threads/timing
 // rules as orc_bench_linear.  kind 1: orc_time_optimize with max_evals =
@@ -229,7 +243,8 @@ int orc_time_optimize_soft(int N, int D, int r, int S, int K, const uint8_t* mas
 // the clock starts; kind 4: the soft-constraint cost of max |v| <= 3,
 // max |a| <= 5 (two computeMaximumOfMagnitude searches) on coefficients
 // solved before the clock starts; kind 5: orc_tube_time_cost with the
-// grad_mode 2 gradient (2S + 1 QCQP solves, times_cp = times).  *units =
+// grad_mode 2 gradient (2S + 1 QCQP solves, times_cp = times); kind 6:
+// orc_time_optimize_sbplx with max_evals = param_i (f_rel 0.05, step 0.1).  *units =
 // optimisations (1), solves (2), samples (3, one sample = all derivatives of
 // all dimensions at one time), trajectories (4) or evaluations (5).
 int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,

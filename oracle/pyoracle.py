@@ -228,6 +228,53 @@ def time_optimize(N, r, vertices, times, max_evals, time_penalty=500.0, incremen
     return t, float(cost[0]), evals.value
 
 
+def sbplx_test(lb, ub, x0, xstep, maxeval, ftol_rel=0.05, ftol_abs=-1.0):
+    """orc_sbplx_test: the LN_SBPLX restatement (orc_sbplx.cpp) on its fixed
+    test objective.  Returns (code, x, minf, nevals, history [nevals, n])."""
+    n = len(x0)
+    x = np.array(x0, dtype=np.float64)
+    lb = np.ascontiguousarray(lb, dtype=np.float64)
+    ub = np.ascontiguousarray(ub, dtype=np.float64)
+    st = np.ascontiguousarray(xstep, dtype=np.float64)
+    hist = np.zeros((maxeval, n))
+    minf = np.zeros(1)
+    nev = ctypes.c_int()
+    L = lib()
+    L.orc_sbplx_test.argtypes = [ctypes.c_int, _dp, _dp, _dp, _dp, ctypes.c_int,
+                                 ctypes.c_double, ctypes.c_double, _dp, _ip, _dp]
+    code = L.orc_sbplx_test(n, _d(lb), _d(ub), _d(x), _d(st), maxeval, ftol_rel, ftol_abs,
+                            _d(minf), ctypes.byref(nev), _d(hist))
+    return code, x, float(minf[0]), nev.value, hist[:nev.value]
+
+
+def time_optimize_sbplx(N, r, vertices, times, max_evals, time_penalty=500.0, f_rel=0.05,
+                        f_abs=-1.0, step_rel=0.1, soft=None, soft_weight=100.0,
+                        soft_maximum_cost=1.0e12):
+    """orc_time_optimize_sbplx: optimizeTime (nonlinear_impl:332-397) with
+    the LN_SBPLX restatement on objectiveFunctionTime (linear inner solve):
+    bounds [0.1, 2 T0], initial step step_rel T0, maxeval max_evals.
+    Returns (times, cost, evals, result, history [evals, S])."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    t = np.array(times, dtype=np.float64)
+    cost = np.zeros(1)
+    evals, result = ctypes.c_int(), ctypes.c_int()
+    hist = np.zeros((max_evals, S))
+    der = np.ascontiguousarray([d for d, _ in (soft or [])] or [0], dtype=np.int32)
+    lim = np.ascontiguousarray([v for _, v in (soft or [])] or [1.0], dtype=np.float64)
+    L = lib()
+    L.orc_time_optimize_sbplx.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+        ctypes.c_double, ctypes.c_int, _ip, _dp, ctypes.c_double, ctypes.c_double, _dp, _ip,
+        _ip, _dp]
+    _check(L.orc_time_optimize_sbplx(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                     _d(vertices.vals), _d(t), time_penalty, max_evals, f_rel,
+                                     f_abs, step_rel, len(soft or []), der.ctypes.data_as(_ip),
+                                     _d(lim), soft_weight, soft_maximum_cost, _d(cost),
+                                     ctypes.byref(evals), ctypes.byref(result), _d(hist)),
+           "time_optimize_sbplx")
+    return t, float(cost[0]), evals.value, result.value, hist[:evals.value]
+
+
 def bench_workload(kind, N, D, r, S, K, masks, vals, times, radii=None, param_i=0,
                    param_d=0.0, threads=1, seconds=10.0):
     """orc_bench_workload (kind 1 time optimisation, 2 tube, 3 sampling).
