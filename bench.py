@@ -523,7 +523,7 @@ def main():
     metric_base = "trajectories/sec (10-seg, N=10, 3D minimum-snap) at 1/2/4/8 MI355X"
     coll = None  # collision workload inputs (also the CPU baseline's)
     extra_cfg = {}
-    pipe = None  # linear: the selection pipeline (its side stream joins in end_steps)
+    pipe = None  # linear: the selection pipeline (its open bucket closes in end_steps)
 
     def end_steps():
         if pipe is not None:
@@ -533,15 +533,16 @@ def main():
         out = plan.solve(fixed_d, times_d, free=False)
         shard_start = shard_range(global_batch, world, rank)[0]
         # The selection step (shard argmin, RCCL all-gather of the triples,
-        # global argmin) runs on a side stream, off the solve's critical path:
-        # step k + 1's solve overlaps step k's selection, two output sets
-        # alternate (shard.SelectionPipeline).  On one GPU without a process
-        # group the all-gather and the global argmin of one triple are the
-        # identity.
-        pipe = SelectionPipeline(
-            lambda o: plan.solve(fixed_d, times_d, free=False, out=o),
-            [out, plan.solve(fixed_d, times_d, free=False)], global_batch, shard_start, rank,
-            dev, use_dist=select)
+        # global argmin) is pipelined (shard.SelectionPipeline): step k's
+        # launch also reduces step k - 1's costs in one extra workgroup, and
+        # the triples of a bucket of steps (here: all K steps of the timed
+        # graph) are all-gathered in one collective with every step's winner
+        # taken at once.  On one GPU without a process group the all-gather
+        # and the global argmin are the identity.
+        pipe = SelectionPipeline(plan, fixed_d, times_d,
+                                 [out, plan.solve(fixed_d, times_d, free=False)], global_batch,
+                                 shard_start, rank, dev, use_dist=select,
+                                 bucket=max(args.steps, args.warmup, 1))
 
         def step_selected():
             return pipe.step()
@@ -913,9 +914,11 @@ def main():
                             "frac": ex_tf / FP64_PEAK_TFLOPS,
                             "flop_per_trajectory": ex_flop, "source": ex_src}
     if select and wl == "linear":
-        roof["kernel_timing"] += ("; per-step device time includes the selection (shard "
-                                  "argmin, RCCL all-gather, global argmin) on a side stream "
-                                  "overlapping the next step's solve")
+        roof["kernel_timing"] += ("; per-step device time includes the selection: each "
+                                  "launch reduces the previous step's costs in one extra "
+                                  "workgroup, and the K steps' triples are all-gathered "
+                                  "(RCCL) in one collective with every step's winner taken at "
+                                  "once")
 
     if rank == 0:
         cpu = None
@@ -933,6 +936,8 @@ def main():
                "batch_per_gpu": B, "segments": S, "N": N, "D": D, "r": r,
                "parallelism": f"shard{world}",
                "selection": bool(select and wl == "linear")}
+        if wl == "linear":
+            cfg["selection_bucket"] = pipe.bucket
         cfg.update(extra_cfg)
         if useful_per_step is not None:
             cfg["converged_per_step"] = useful_per_step

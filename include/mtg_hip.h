@@ -717,6 +717,26 @@ int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed
                             void* stream);
 int mtg_select_global(const double* triples, int world, double* out, void* stream);
 
+/* The pipelined step (round 5): this step's solve (mtg_linear_solve) with
+ * the PREVIOUS step's shard selection -- mtg_select_local of prev_cost
+ * (device, prev_count costs, global indices prev_start ..) into prev_triple
+ * (device, 3 doubles) -- in the same launch: the wave and lane-pair kernels
+ * run it in one extra workgroup beside the solves, the others as a launch of
+ * their own first.  prev_cost NULL: the plain solve.  prev_cost must not
+ * alias this step's cost (alternate two output sets).  The selection never
+ * feeds a solve, so it costs no launch on the step's critical path
+ * (mav_tube_trajectory_generation_amd/shard.py SelectionPipeline). */
+int mtg_linear_solve_select_prev(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                                 const double* times, double* coeffs, double* cost,
+                                 double* free_vals, int32_t* status, const double* prev_cost,
+                                 int64_t prev_count, int64_t prev_start, int rank,
+                                 double* prev_triple, void* stream);
+/* The per-step winners of G steps at once: triples = the all-gather of every
+ * rank's G triples (world x G x 3, rank-major), out = n x 3 (device), step
+ * g's winner by mtg_select_global's rule, for g < n <= G. */
+int mtg_select_global_steps(const double* triples, int world, int G, int n, double* out,
+                            void* stream);
+
 /* ------------------------------------------------------------------------
  * Host-side input generation (vertex.cpp:27-82, 228-269) for batches:
  * trajectory b uses createRandomVertices(max_derivative = M-1, S, +/-pos_bound,

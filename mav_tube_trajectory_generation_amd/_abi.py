@@ -230,6 +230,11 @@ SIGNATURES = {
                                                ctypes.c_size_t, _vp]),
     "mtg_select_global": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.c_void_p]),
+    "mtg_linear_solve_select_prev": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp,
+                                                     _vp, _vp, ctypes.c_int64, ctypes.c_int64,
+                                                     ctypes.c_int, _vp, _vp]),
+    "mtg_select_global_steps": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                _vp, _vp]),
     "mtg_sample_trajectories": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int64, _vp, _vp, ctypes.c_double,
                                                ctypes.c_double, ctypes.c_double, ctypes.c_int,

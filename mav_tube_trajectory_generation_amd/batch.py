@@ -177,6 +177,23 @@ class LinearPlan:
             _ptr(workspace), workspace.numel(), _stream(dev)), "mtg_linear_solve_select")
         return o
 
+    def solve_select_prev(self, fixed_vals, times, out, prev_cost=None, prev_start=0, rank=0,
+                          prev_triple=None):
+        """solve() into the output set `out` (coeffs, cost, status) with the
+        previous step's shard selection in the same launch
+        (mtg_linear_solve_select_prev): prev_cost [n] (another output set's
+        costs) reduced to prev_triple [3] = (cost, prev_start + index, rank).
+        prev_cost None: the plain solve."""
+        B = times.shape[0]
+        _require(times, (B, self.S), "times")
+        _require(fixed_vals, (B, self.D, self.n_fixed), "fixed_vals")
+        n = 0 if prev_cost is None else prev_cost.numel()
+        check(lib().mtg_linear_solve_select_prev(
+            self._h, B, _ptr(fixed_vals), _ptr(times), _ptr(out["coeffs"]), _ptr(out.get("cost")),
+            _ptr(out.get("free")), _ptr(out.get("status")), _ptr(prev_cost), n, int(prev_start),
+            int(rank), _ptr(prev_triple), _stream(times.device)), "mtg_linear_solve_select_prev")
+        return out
+
     def coefficients(self, fixed_vals, free_vals, times):
         """Coefficients and cost from given d_f and d_p, no solve
         (setFreeConstraints, linear_impl:497-506).  Returns (coeffs, cost,

@@ -656,6 +656,44 @@ int mtg_linear_solve_select(const mtg_plan* plan, int64_t B, const double* fixed
                                            free_vals, status, st, sel));
 }
 
+int mtg_linear_solve_select_prev(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                                 const double* times, double* coeffs, double* cost,
+                                 double* free_vals, int32_t* status, const double* prev_cost,
+                                 int64_t prev_count, int64_t prev_start, int rank,
+                                 double* prev_triple, void* stream) {
+  clear_stale_error();
+  if (!plan || B < 0 || B > 0x7fffffff || rank < 0 || prev_count < 0 || prev_start < 0)
+    return MTG_ERR_INVALID_ARG;
+  if (prev_cost && !prev_triple) return MTG_ERR_INVALID_ARG;
+  if (prev_cost && cost && prev_cost == cost) return MTG_ERR_INVALID_ARG;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  if (B == 0) {  // no solve launch to ride on
+    if (!prev_cost) return MTG_OK;
+    return from_hip(mtg::launch_select_local(prev_cost, prev_count, prev_start, rank,
+                                             prev_triple, st));
+  }
+  if (!times || !coeffs || (plan->dev.nf > 0 && !fixed_vals)) return MTG_ERR_INVALID_ARG;
+  mtg::SelectArgs sel;
+  sel.rank = rank;
+  if (prev_cost) {
+    sel.prev_cost = prev_cost;
+    sel.prev_count = prev_count;
+    sel.prev_start = prev_start;
+    sel.prev_out = prev_triple;
+  }
+  return from_hip(mtg::launch_linear_solve(plan->dev, B, fixed_vals, times, coeffs, cost,
+                                           free_vals, status, st, sel));
+}
+
+int mtg_select_global_steps(const double* triples, int world, int G, int n, double* out,
+                            void* stream) {
+  clear_stale_error();
+  if (world < 1 || G < 1 || n < 0 || n > G || (n > 0 && (!triples || !out)))
+    return MTG_ERR_INVALID_ARG;
+  return from_hip(mtg::launch_select_global_steps(triples, world, G, n, out,
+                                                  static_cast<hipStream_t>(stream)));
+}
+
 int mtg_select_global(const double* triples, int world, double* out, void* stream) {
   clear_stale_error();
   if (world < 1 || !triples || !out) return MTG_ERR_INVALID_ARG;

@@ -36,6 +36,14 @@ struct SelectArgs {
   double* out = nullptr;
   double* part_cost = nullptr;
   int64_t* part_idx = nullptr;
+  // Deferred selection (mtg_linear_solve_select_prev): the PREVIOUS step's
+  // costs prev_cost[0 .. prev_count) (global indices prev_start ..) reduced
+  // to the triple prev_out by one extra workgroup of this solve launch
+  // (wave and lane-pair kernels; a separate launch before the others).
+  const double* prev_cost = nullptr;
+  int64_t prev_count = 0;
+  int64_t prev_start = 0;
+  double* prev_out = nullptr;
 };
 // Workgroups of the fused solve (the partial slots the workspace needs).
 int64_t select_partials(const PlanDev& pl, int64_t B);
@@ -43,7 +51,8 @@ int64_t select_partials(const PlanDev& pl, int64_t B);
 // Standard-pattern linear solve at compile-time S (mtg_linear_wave.hip):
 // N = 10, r = 4, D = 3, 2 <= S <= 16, the kernel behind "standard" there.
 bool has_linear_wave(const PlanDev& pl);
-hipError_t launch_linear_solve_wave(const PlanDev& pl, int64_t B, const double* df,
+hipError_t launch_linear_solve_wave(const PlanDev& pl, int64_t B, const SelectArgs& sel,
+                                    const double* df,
                                     const double* times, double* coeffs, double* cost,
                                     double* free_vals, int32_t* status, hipStream_t st);
 // Standard-pattern linear solve (mtg_linear_std.hip).
@@ -76,7 +85,8 @@ int64_t lane2_blocks(int64_t B);
 int linear_kernel_for_batch(const PlanDev& pl, int64_t B);
 hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
                                    const double* times, double* coeffs, double* cost,
-                                   double* free_vals, int32_t* status, hipStream_t st);
+                                   double* free_vals, int32_t* status, hipStream_t st,
+                                   const SelectArgs& sel = SelectArgs{});
 size_t linear_std_lds_bytes(int N, int S, int D);
 // Standard-pattern time kernels (mtg_time_std.hip): N = 10, r = 2..4, D = 1..3.
 bool has_time_std(const PlanDev& pl);
@@ -106,6 +116,8 @@ inline bool use_std_kernel(const PlanDev& pl) {
   return pl.std_pattern && pl.kernel != MTG_KERNEL_GENERIC;
 }
 
+hipError_t launch_select_global_steps(const double* triples, int world, int G, int n,
+                                      double* out, hipStream_t st);
 hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                const double* times, double* coeffs, double* cost,
                                double* free_vals, int32_t* status, hipStream_t st,

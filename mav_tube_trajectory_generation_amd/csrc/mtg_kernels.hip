@@ -545,15 +545,26 @@ hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
                                double* free_vals, int32_t* status, hipStream_t st,
                                const SelectArgs& sel) {
   const int k = linear_kernel_for_batch(pl, B);
+  // A deferred selection (the previous step's costs, SelectArgs::prev_*):
+  // an extra workgroup of the wave and lane-pair launches; a launch of its
+  // own before the other kernels.
+  SelectArgs own = sel;
+  const bool prev_inside = k == MTG_KERNEL_LANE_PAIR || (k == MTG_KERNEL_STANDARD);
+  if (sel.prev_out && !prev_inside) {
+    const hipError_t e = launch_select_local(sel.prev_cost, sel.prev_count, sel.prev_start,
+                                             sel.rank, sel.prev_out, st);
+    if (e != hipSuccess) return e;
+    own.prev_out = nullptr;
+  }
   // Lane kernels: per-workgroup partials in the epilogue, then one small
   // reduction launch.  Wavefront kernels (one trajectory per workgroup): the
   // reduction reads the costs.
   if (k == MTG_KERNEL_LANE || k == MTG_KERNEL_LANE_PAIR) {
     const hipError_t e =
         k == MTG_KERNEL_LANE
-            ? launch_linear_solve_lane(pl, B, df, times, coeffs, cost, free_vals, status, st, sel)
+            ? launch_linear_solve_lane(pl, B, df, times, coeffs, cost, free_vals, status, st, own)
             : launch_linear_solve_lane2(pl, B, df, times, coeffs, cost, free_vals, status, st,
-                                        sel);
+                                        own);
     if (e != hipSuccess || !sel.out) return e;
     const int64_t n = k == MTG_KERNEL_LANE ? lane_blocks(B) : lane2_blocks(B);
     return launch_select_reduce(sel.part_cost, sel.part_idx, n, B, sel.start, sel.rank, sel.out,
@@ -561,7 +572,7 @@ hipError_t launch_linear_solve(const PlanDev& pl, int64_t B, const double* df,
   }
   hipError_t e;
   if (use_std_kernel(pl)) {
-    e = launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st);
+    e = launch_linear_solve_std(pl, B, df, times, coeffs, cost, free_vals, status, st, own);
     if (e != hipSuccess || !sel.out) return e;
     return launch_select_local(cost, B, sel.start, sel.rank, sel.out, st);
   }

@@ -444,7 +444,7 @@ struct Half {
 // status to wave 0, which forms the per-trajectory cost and status.
 template <int N, int R, int D, int S, bool BW>
 __device__ __attribute__((always_inline)) inline void lane2_half(
-    int64_t B, const double* __restrict__ fixed_vals, const double* __restrict__ times,
+    int64_t B, int blk, const double* __restrict__ fixed_vals, const double* __restrict__ times,
     double* __restrict__ coeffs, double* __restrict__ cost, double* __restrict__ free_vals,
     int32_t* __restrict__ status, const SelectArgs& sel, double* xch, double* cxch, int* sxch,
     double* stage) {
@@ -453,7 +453,7 @@ __device__ __attribute__((always_inline)) inline void lane2_half(
   constexpr int TPW = kWave / D;
   const int lane = threadIdx.x & (kWave - 1);
   const int tl = lane / D, d = lane - tl * D;
-  const int64_t b = static_cast<int64_t>(blockIdx.x) * TPW + tl;
+  const int64_t b = static_cast<int64_t>(blk) * TPW + tl;
   const bool act = tl < TPW && b < B;
   // Inactive lanes run trajectory 0 with no outputs: every lane reaches the
   // barriers with defined data.
@@ -509,7 +509,7 @@ __device__ __attribute__((always_inline)) inline void lane2_half(
     // of the output: both waves copy it out in 16-byte pieces, consecutive
     // lanes on consecutive addresses (the per-lane stores touch 64 cache
     // lines per instruction: B = 8192 13.0 -> 10.9 us).
-    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * TPW;
+    const int64_t b0 = static_cast<int64_t>(blk) * TPW;
     const int nt = B - b0 < TPW ? static_cast<int>(B - b0) : TPW;
     const int nch = nt * (PER / 2);
     const double2* src = reinterpret_cast<const double2*>(stage);
@@ -536,7 +536,7 @@ __device__ __attribute__((always_inline)) inline void lane2_half(
     if (status)
       status[b] = stt == 1 ? MTG_TRAJ_BAD_TIME : (stt == 2 ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK);
   }
-  if (sel.out) select_partial(sel, tot, act && d == 0 ? b : -1, blockIdx.x);
+  if (sel.out) select_partial(sel, tot, act && d == 0 ? b : -1, blk);
 }
 
 }  // namespace lane2
@@ -552,13 +552,22 @@ __global__ __launch_bounds__(2 * kWave) void linear_lane2_kernel(
   __shared__ double xch[2 * (H::NT + H::MF) * kWave];
   __shared__ double cxch[kWave];
   __shared__ int sxch[kWave];
+  // The deferred selection (the previous step's costs, SelectArgs::prev_*)
+  // in one extra workgroup, dispatched first (block 0) so that it ends well
+  // before the solves' (8192 costs: four rounds of loads by 128 threads).
+  const int blk = static_cast<int>(blockIdx.x) - (sel.prev_out ? 1 : 0);
+  if (blk < 0) {
+    select_reduce_block<2 * kWave>(sel.prev_cost, sel.prev_count, sel.prev_start, sel.rank,
+                                   sel.prev_out, cxch, reinterpret_cast<int64_t*>(xch));
+    return;
+  }
   __shared__ __attribute__((aligned(16))) double stage[(kWave / D) * S * D * N];
   if (threadIdx.x < kWave)
-    lane2::lane2_half<N, R, D, S, false>(B, fixed_vals, times, coeffs, cost, free_vals, status,
-                                         sel, xch, cxch, sxch, stage);
+    lane2::lane2_half<N, R, D, S, false>(B, blk, fixed_vals, times, coeffs, cost, free_vals,
+                                         status, sel, xch, cxch, sxch, stage);
   else
-    lane2::lane2_half<N, R, D, S, true>(B, fixed_vals, times, coeffs, cost, free_vals, status,
-                                        sel, xch, cxch, sxch, stage);
+    lane2::lane2_half<N, R, D, S, true>(B, blk, fixed_vals, times, coeffs, cost, free_vals,
+                                        status, sel, xch, cxch, sxch, stage);
 }
 
 namespace {
@@ -568,7 +577,7 @@ hipError_t launch_lane2(int64_t B, const double* df, const double* times, double
                         double* cost, double* free_vals, int32_t* status, hipStream_t st,
                         const SelectArgs& sel) {
   constexpr int TPW = kWave / D;
-  const int64_t blocks = (B + TPW - 1) / TPW;
+  const int64_t blocks = (B + TPW - 1) / TPW + (sel.prev_out ? 1 : 0);
   hipLaunchKernelGGL((linear_lane2_kernel<N, R, D, S>), dim3(static_cast<unsigned>(blocks)),
                      dim3(2 * kWave), 0, st, B, df, times, coeffs, cost, free_vals, status, sel);
   return hipGetLastError();

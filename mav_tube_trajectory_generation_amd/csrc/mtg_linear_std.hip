@@ -140,9 +140,17 @@ static bool runtime_s_forced() {
 
 hipError_t launch_linear_solve_std(const PlanDev& pl, int64_t B, const double* df,
                                    const double* times, double* coeffs, double* cost,
-                                   double* free_vals, int32_t* status, hipStream_t st) {
+                                   double* free_vals, int32_t* status, hipStream_t st,
+                                   const SelectArgs& sel) {
+  // the wave kernel reduces a deferred selection in an extra workgroup; the
+  // runtime-S kernel takes it as a launch of its own first
   if (has_linear_wave(pl) && !runtime_s_forced())
-    return launch_linear_solve_wave(pl, B, df, times, coeffs, cost, free_vals, status, st);
+    return launch_linear_solve_wave(pl, B, sel, df, times, coeffs, cost, free_vals, status, st);
+  if (sel.prev_out) {
+    const hipError_t e = launch_select_local(sel.prev_cost, sel.prev_count, sel.prev_start,
+                                             sel.rank, sel.prev_out, st);
+    if (e != hipSuccess) return e;
+  }
   switch (pl.N) {
     case 4: return launch_std_n<4>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
     case 6: return launch_std_n<6>(pl.r, pl.D, pl.S, B, pl.tab, df, times, coeffs, cost, free_vals, status, st);

@@ -9,6 +9,7 @@
 
 #include <cmath>
 
+#include "mtg_select_device.h"
 #include "mtg_wave_device.h"
 
 namespace mtg {
@@ -18,15 +19,24 @@ template <int N, int R, int D, int S>
 __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     const double* __restrict__ times, double* __restrict__ coeffs, double* __restrict__ cost,
-    double* __restrict__ free_vals, int32_t* __restrict__ status) {
+    double* __restrict__ free_vals, int32_t* __restrict__ status, SelectArgs sel) {
   using Sv = Solver<N, R, D, S>;
   using G = typename Sv::G;
   constexpr int MF = G::MF, MP = G::MP, NFIX = G::NFIX;
   __shared__ __attribute__((aligned(16))) double sm[G::L_N];
+  // The deferred selection (the previous step's costs) in one extra
+  // workgroup after the solves: it runs beside them (about 1 us at
+  // B = 1024 against a 3.4 us solve), so it costs no launch of its own.
+  const int64_t nb = gridDim.x - (sel.prev_out ? 1 : 0);
+  if (sel.prev_out && blockIdx.x == nb) {
+    select_reduce_block<kWave>(sel.prev_cost, sel.prev_count, sel.prev_start, sel.rank,
+                               sel.prev_out, nullptr, nullptr);
+    return;
+  }
   Sv sv;
   sv.init(sm);
   const int lane = sv.lane;
-  const int64_t b = xcd_problem(blockIdx.x, gridDim.x);
+  const int64_t b = xcd_problem(blockIdx.x, nb);
   const double* fb = fixed_vals + b * D * NFIX;
   const double* tb = times + b * S;
   MTG_STAMP(0);
@@ -62,12 +72,16 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   // 80 bytes at an 80-byte stride).
   static_assert(2 * G::NSL * G::SLOT >= per, "coefficients fit the slots");
   double* stage = sv.slots;
+#ifndef MTG_ABL_NOCOEF  // diagnostic ablation builds only (tools/gpu_r05_abl.sh)
   const double J = sv.coeff_cost(T, stage);
   lds_order();
   {
     copy_out16<kWave, per / 2>(reinterpret_cast<const double2*>(stage),
                                reinterpret_cast<double2*>(coeffs + b * per), lane);
   }
+#else
+  const double J = sv.dv[lane];
+#endif
   if (lane == 0) {
     if (cost) cost[b] = J;
     if (status) status[b] = not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK;
@@ -83,11 +97,13 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
 }
 
 template <int S>
-static hipError_t launch_wave_s(int64_t B, const double* tab, const double* df,
-                                const double* times, double* coeffs, double* cost,
-                                double* free_vals, int32_t* status, hipStream_t st) {
-  hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S>), dim3(static_cast<unsigned>(B)),
-                     dim3(kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status);
+static hipError_t launch_wave_s(int64_t B, const SelectArgs& sel, const double* tab,
+                                const double* df, const double* times, double* coeffs,
+                                double* cost, double* free_vals, int32_t* status,
+                                hipStream_t st) {
+  const int64_t blocks = B + (sel.prev_out ? 1 : 0);
+  hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status, sel);
   return hipGetLastError();
 }
 
@@ -97,12 +113,13 @@ bool has_linear_wave(const PlanDev& pl) {
   return pl.std_pattern && pl.N == 10 && pl.r == 4 && pl.D == 3 && pl.S >= 2 && pl.S <= 16;
 }
 
-hipError_t launch_linear_solve_wave(const PlanDev& pl, int64_t B, const double* df,
+hipError_t launch_linear_solve_wave(const PlanDev& pl, int64_t B, const SelectArgs& sel,
+                                    const double* df,
                                     const double* times, double* coeffs, double* cost,
                                     double* free_vals, int32_t* status, hipStream_t st) {
   switch (pl.S) {
 #define MTG_WAVE_S(SS) \
-  case SS: return wave::launch_wave_s<SS>(B, pl.tab, df, times, coeffs, cost, free_vals, status, st);
+  case SS: return wave::launch_wave_s<SS>(B, sel, pl.tab, df, times, coeffs, cost, free_vals, status, st);
     MTG_WAVE_S(2) MTG_WAVE_S(3) MTG_WAVE_S(4) MTG_WAVE_S(5) MTG_WAVE_S(6) MTG_WAVE_S(7)
     MTG_WAVE_S(8) MTG_WAVE_S(9) MTG_WAVE_S(10) MTG_WAVE_S(11) MTG_WAVE_S(12) MTG_WAVE_S(13)
     MTG_WAVE_S(14) MTG_WAVE_S(15) MTG_WAVE_S(16)

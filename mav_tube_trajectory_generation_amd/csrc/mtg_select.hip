@@ -92,6 +92,38 @@ __global__ void select_global_kernel(const double* __restrict__ triples, int wor
   out[2] = triples[3 * w + 2];
 }
 
+// Per-step global argmin of G steps' triples gathered from every rank
+// (triples: world x G x 3, rank-major as all_gather_into_tensor lays them
+// out): out[g] for g < n, the select_global rule per step.
+__global__ void select_global_steps_kernel(const double* __restrict__ triples, int world, int G,
+                                           int n, double* __restrict__ out) {
+  const int g = threadIdx.x + blockIdx.x * blockDim.x;
+  if (g >= n) return;
+  int w = 0;
+  double best = HUGE_VAL;
+  for (int r = 0; r < world; ++r) {
+    const double* t = triples + (static_cast<int64_t>(r) * G + g) * 3;
+    double key = t[0];
+    if (t[1] < 0.0 || key != key) key = HUGE_VAL;
+    if (key < best) {
+      best = key;
+      w = r;
+    }
+  }
+  const double* t = triples + (static_cast<int64_t>(w) * G + g) * 3;
+  out[3 * g] = t[0];
+  out[3 * g + 1] = t[1];
+  out[3 * g + 2] = t[2];
+}
+
+hipError_t launch_select_global_steps(const double* triples, int world, int G, int n,
+                                      double* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(select_global_steps_kernel, dim3((n + 63) / 64), dim3(64), 0, st, triples,
+                     world, G, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_select_local(const double* costs, int64_t count, int64_t start, int rank,
                                double* out, hipStream_t st) {
   return launch_select_reduce(costs, nullptr, count, count, start, rank, out, st);

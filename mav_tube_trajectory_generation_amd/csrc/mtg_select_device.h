@@ -56,4 +56,57 @@ __device__ inline void select_partial(const SelectArgs& sel, double c, int64_t i
   }
 }
 
+// The shard's triple of costs c[0 .. count) (global indices start ..) by
+// the NT threads of one workgroup: the deferred selection's extra workgroup
+// (SelectArgs::prev_*), the rule of select_reduce_kernel.  Sixteen loads in
+// flight per thread (a reduction of 8192 costs is four rounds of L2 latency
+// at NT = 128); the waves combine through ws_c / ws_i (LDS, NT / 64 each).
+template <int NT>
+__device__ inline void select_reduce_block(const double* __restrict__ c, int64_t count,
+                                           int64_t start, int rank, double* __restrict__ out,
+                                           double* ws_c, int64_t* ws_i) {
+  const int t = threadIdx.x;
+  double bc = HUGE_VAL;
+  int64_t bi = INT64_MAX;
+  constexpr int kU = 16;
+  for (int64_t k0 = t; k0 < count; k0 += NT * kU) {
+    double pc[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t k = k0 + u * NT;
+      pc[u] = k < count ? c[k] : HUGE_VAL;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t k = k0 + u * NT;
+      const double v = pc[u] != pc[u] ? HUGE_VAL : pc[u];  // NaN never wins
+      if (k < count && sel_better(v, k, bc, bi)) {
+        bc = v;
+        bi = k;
+      }
+    }
+  }
+  sel_wave_min(bc, bi);
+  if constexpr (NT > 64) {
+    if ((t & 63) == 0) {
+      ws_c[t / 64] = bc;
+      ws_i[t / 64] = bi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NT / 64; ++q)
+      if (sel_better(ws_c[q], ws_i[q], bc, bi)) {
+        bc = ws_c[q];
+        bi = ws_i[q];
+      }
+  }
+  if (t == 0) {
+    const bool empty = count <= 0;
+    const int64_t at = (bi >= count || bi < 0) ? 0 : bi;  // all +inf: the first index
+    out[0] = empty ? HUGE_VAL : bc;
+    out[1] = empty ? -1.0 : static_cast<double>(at + start);
+    out[2] = static_cast<double>(rank);
+  }
+}
+
 }  // namespace mtg

@@ -250,6 +250,7 @@ struct Solver {
       const double cnext = hk[M] * qr[0];                      // p_{v+1}
       MTG_STAMP(1);
       double* sl = slot_of(av);
+#ifndef MTG_ABL_NOB  // diagnostic ablation builds only (tools/gpu_r05_abl.sh)
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         double s = cpos * pos[1][d];
@@ -257,6 +258,7 @@ struct Solver {
         s = fma(cnext, pos[2][d], s);
         sl[O_R + d * MF + ai] = -s;
       }
+#endif
       // lower triangle of row i (entries j > i go to the slot's Z area,
       // written again by the sweep before it is read)
       const int rbase = O_S + tri(ai, 0);
@@ -271,13 +273,16 @@ struct Solver {
       const bool fw = av < MID, bk = av >= MID && av < S - 1;
       double* pc = fw ? sl + O_P + ai : (bk ? slot_of(av + 1) + O_P + ai * MF : junk);
       const int ps = fw ? MF : 1;
+#ifndef MTG_ABL_NOC
 #pragma unroll
       for (int j = 0; j < MF; ++j) pc[j * ps] = Cr[j];
+#endif
     }
     lds_order();
     MTG_STAMP(12);
     // The fully fixed end vertices' part of b_1 (segment 0) and b_(S-1)
     // (segment S-1): lane (e, d, i) adds -sum_l H_seg(k, l) d_f(l) for its row.
+#ifndef MTG_ABL_NOEND
     {
       double qe[M];
       row_powers<M, R>(te, i1, i2, i3, qe);
@@ -287,6 +292,7 @@ struct Solver {
       // lanes past the 2 D MF end lanes repeat one and add nothing
       atomicAdd(slot_of(ee ? S - 1 : 1) + O_R + ed * MF + ai, lane < 2 * D * MF ? -s : 0.0);
     }
+#endif
     lds_order();
     MTG_STAMP(2);
 

@@ -119,76 +119,117 @@ def select_best_device(local_costs, global_batch, group=None, local_triple=None)
     return allv[w]
 
 
+def select_steps(ring, n, group=None, out=None, use_dist=True):
+    """Per-step global winners of a bucket of n steps: ring [G, 3] holds this
+    rank's triple of each step (rows >= n unused).  The ranks all-gather
+    their whole rings (world x G x 3 doubles, one collective per bucket) and
+    step g's winner is the select_global rule over the ranks' row g.
+    Returns out [G, 3] (rows < n set).  use_dist=False (one process): the
+    rank's own triples are the winners."""
+    G = ring.shape[0]
+    if out is None:
+        out = torch.full_like(ring, float("nan"))
+    if n == 0:
+        return out
+    if not use_dist:
+        out[:n].copy_(ring[:n])
+        return out
+    world = dist.get_world_size(group)
+    flat = torch.empty(world * G * 3, dtype=torch.float64, device=ring.device)
+    dist.all_gather_into_tensor(flat, ring.reshape(-1), group=group)
+    if flat.is_cuda:  # one HIP launch (mtg_select_global_steps)
+        lib, check, ptr, stream = _hip()
+        check(lib.mtg_select_global_steps(ptr(flat), world, G, n, ptr(out),
+                                          stream(flat.device)), "mtg_select_global_steps")
+        return out
+    allv = flat.view(world, G, 3)[:, :n]
+    key = torch.where(allv[..., 1] < 0, torch.full_like(allv[..., 0], float("nan")),
+                      allv[..., 0])
+    key = torch.where(torch.isnan(key), torch.full_like(key, float("inf")), key)
+    w = torch.argmin(key, dim=0)  # the first rank holding the minimum
+    out[:n] = allv[w, torch.arange(n)]
+    return out
+
+
 class SelectionPipeline:
     """The multi-GPU step with the selection off the solve's critical path.
 
-    Step k solves into output set k % depth on the current stream; a side
-    stream then reduces that set's costs to the shard's triple
-    (mtg_select_local), all-gathers the triples (RCCL) and takes the global
-    argmin (mtg_select_global), while the current stream already runs step
-    k + 1's solve.  The selection never feeds a later solve; the only
-    ordering is that solve k + depth, which overwrites output set k % depth,
-    waits for selection k to have read it.  Every call sequence ends with
-    drain() (the side stream joins the current one), so a captured graph or
-    an eager batch of steps is closed and `best` is final after it.
+    Step k solves into output set k % 2 and, in the SAME launch, reduces
+    step k - 1's costs (the other set) to the shard's triple
+    (mtg_linear_solve_select_prev: one extra workgroup of the wave /
+    lane-pair kernels, running beside the solves).  The triples of a bucket
+    of up to `bucket` steps collect in a device ring; at the end of the
+    bucket (or drain()) the last step's costs are reduced, the ranks
+    all-gather their rings in ONE collective (RCCL over xGMI) and every
+    step's global winner is taken at once (mtg_select_global_steps).  So a
+    step costs the solve launch alone, and the collective's fixed latency
+    is paid once per bucket, not per step.  Everything is stream-ordered on
+    the current stream, so a captured graph holds it without cross-stream
+    edges (a side-stream fork and join per step measured 6.4 us of graph
+    overhead per step).  The selection never feeds a later solve.
 
-    solve_into(out): enqueue one solve writing out["cost"] (and the rest of
-    the output set) on the current stream.  use_dist=False (one process, no
-    process group): the all-gather and the global argmin of one triple are
-    the identity, so the shard's triple is the winner."""
+    best [bucket, 3]: the winners (cost, global index, owner rank) of the
+    last closed bucket, rows < n_done valid.  use_dist=False (one process,
+    no process group): the shard's triples are the winners."""
 
-    def __init__(self, solve_into, outs, global_batch, start, rank, device, use_dist=True,
-                 group=None):
-        self.solve_into = solve_into
+    def __init__(self, plan, fixed_vals, times, outs, global_batch, start, rank, device,
+                 use_dist=True, bucket=32, group=None):
+        self.plan = plan
+        self.fixed_vals = fixed_vals
+        self.times = times
         self.outs = list(outs)
+        if len(self.outs) != 2:
+            raise ValueError("two output sets alternate")
         self.global_batch = int(global_batch)
         self.start = int(start)
         self.rank = int(rank)
         self.use_dist = use_dist
         self.group = group
-        self.side = torch.cuda.Stream(device)
-        self.triples = [torch.empty(3, dtype=torch.float64, device=device) for _ in self.outs]
-        self.best = torch.empty(3, dtype=torch.float64, device=device)
+        self.bucket = int(bucket)
+        self.ring = torch.full((self.bucket, 3), float("nan"), dtype=torch.float64,
+                               device=device)
+        self.best = torch.full((self.bucket, 3), float("nan"), dtype=torch.float64,
+                               device=device)
         self.k = 0
-        self._read = [None] * len(self.outs)  # event: selection done reading set i
-        self._pending = False  # side stream forked from the current one since drain()
+        self.n = 0          # steps in the open bucket
+        self.n_done = 0     # steps of the last closed bucket
+        self.last = None    # output set of the last solve (costs not yet reduced)
 
     def step(self):
-        lib, check, ptr, stream = _hip()
-        main = torch.cuda.current_stream()
-        i = self.k % len(self.outs)
-        if self._read[i] is not None:
-            main.wait_event(self._read[i])
+        if self.n == self.bucket:
+            self._flush()
+        i = self.k % 2
         o = self.outs[i]
-        self.solve_into(o)
-        solved = torch.cuda.Event()
-        solved.record(main)
-        self.side.wait_event(solved)
-        with torch.cuda.stream(self.side):
-            cost = o["cost"]
-            t = self.triples[i]
-            check(lib.mtg_select_local(ptr(cost), cost.numel(), self.start, self.rank, ptr(t),
-                                       stream(cost.device)), "mtg_select_local")
-            if self.use_dist:
-                self.best = select_best_device(None, self.global_batch, self.group,
-                                               local_triple=t)
-            else:
-                self.best = t
-            done = torch.cuda.Event()
-            done.record(self.side)
-        self._read[i] = done
-        self._pending = True
+        if self.last is None:
+            self.plan.solve_select_prev(self.fixed_vals, self.times, o)
+        else:
+            self.plan.solve_select_prev(self.fixed_vals, self.times, o,
+                                        prev_cost=self.outs[self.last]["cost"],
+                                        prev_start=self.start, rank=self.rank,
+                                        prev_triple=self.ring[self.n - 1])
+        self.last = i
+        self.n += 1
         self.k += 1
         return self.best
 
+    def _flush(self):
+        if self.n == 0:
+            return
+        lib, check, ptr, stream = _hip()
+        c = self.outs[self.last]["cost"]
+        t = self.ring[self.n - 1]
+        check(lib.mtg_select_local(ptr(c), c.numel(), self.start, self.rank, ptr(t),
+                                   stream(c.device)), "mtg_select_local")
+        select_steps(self.ring, self.n, self.group, out=self.best, use_dist=self.use_dist)
+        self.last = None
+        self.n_done = self.n
+        self.n = 0
+
     def drain(self):
-        """Join the side stream into the current one (end of a captured
-        sequence or of an eager batch of steps)."""
-        if self._pending:
-            torch.cuda.current_stream().wait_stream(self.side)
-        self._pending = False
-        self._read = [None] * len(self.outs)
-        return self.best
+        """Close the open bucket (end of a captured sequence or of an eager
+        batch of steps); returns the winners of its steps [n_done, 3]."""
+        self._flush()
+        return self.best[:self.n_done]
 
 
 def select_best(local_costs, global_batch, group=None):

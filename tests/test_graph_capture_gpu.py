@@ -6,9 +6,9 @@ something else, must fail here rather than in the bench).
 Also: a stale error left in the HIP runtime's per-thread last-error slot by
 an unrelated failed call must not be reported as the next entry point's
 MTG_ERR_HIP (the cause of round 4's failed captures), and the
-selection pipeline (shard.SelectionPipeline: the selection on a side
-stream, overlapping the next solve) must give the eager selection's winner
-inside a graph.
+selection pipeline (shard.SelectionPipeline: each launch reduces the
+previous step's costs, a bucket of steps closes with one selection) must
+give every step's winner inside a graph.
 """
 import ctypes
 
@@ -91,31 +91,43 @@ def test_tube_step_captures(ctx, dev):
         assert torch.equal(got[k], eager[k]), k
 
 
-def test_selection_pipeline_in_graph(ctx, dev):
+@pytest.mark.parametrize("B,kernel", [(1024, "auto"), (8192, "auto"), (300, "generic"),
+                                      (2000, "lane")])
+def test_selection_pipeline_in_graph(ctx, dev, B, kernel):
+    """shard.SelectionPipeline: each launch reduces the previous step's costs
+    in an extra workgroup (or a launch of its own for the other kernels),
+    buckets of steps close with one selection; every step's winner is the
+    argmin of its costs (select_local's rule), eagerly and replayed from a
+    graph, across bucket boundaries."""
     import mav_tube_trajectory_generation_amd as mtg
     from mav_tube_trajectory_generation_amd.shard import SelectionPipeline
-    S, B, start = 10, 1024, 4096
+    S, start = 10, 4096
     mask, fixed, times, _ = _problems(S, B)
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
     fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
-    ref = plan.solve(fd, td)["cost"].cpu().numpy()
-    i = int(np.argmin(ref))
+    base = plan.solve(fd, td)["cost"].cpu().numpy()
+    j = int(np.argmin(base))
+    want = torch.tensor([base[j], start + j, 1.0], dtype=torch.float64)
     outs = [plan.solve(fd, td), plan.solve(fd, td)]
-    pipe = SelectionPipeline(lambda o: plan.solve(fd, td, out=o), outs, 2 * B, start, 1, dev,
-                             use_dist=False)
-    for _ in range(3):
+    for o in outs:
+        o["cost"].fill_(float("nan"))
+    pipe = SelectionPipeline(plan, fd, td, outs, 2 * B, start, 1, dev, use_dist=False, bucket=3)
+    for _ in range(5):  # a bucket of 3, then 2 closed by drain()
         pipe.step()
     eager = pipe.drain().clone()
     torch.cuda.synchronize()
+    assert eager.shape == (2, 3)
+    for r in eager.cpu():
+        assert torch.equal(r, want)
 
     def steps():
-        for _ in range(4):
+        for _ in range(3):
             pipe.step()
         return pipe.drain()
     got = _capture(steps, reps=1)
-    want = torch.tensor([ref[i], start + i, 1.0], dtype=torch.float64)
-    assert torch.equal(eager.cpu(), want)
-    assert torch.equal(got.cpu(), want)
+    assert got.shape == (3, 3)
+    for r in got.cpu():
+        assert torch.equal(r, want)
 
 
 def _hip_runtime():

@@ -99,3 +99,47 @@ def test_sharded_selection_matches_single_process(world, global_batch):
         assert all_nan[1:] == [0.0, 0.0]
         assert ties == [7.0, 0.0, 0.0]
         assert tiny == [3.0, 0.0, 0.0]
+
+
+def _steps_worker(rank, world, port, G, n, result_q):
+    """select_steps over gloo: each rank's ring of per-step triples, one
+    all-gather per bucket, every step's winner by the select_global rule."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, REPO)
+    import torch.distributed as dist
+    from mav_tube_trajectory_generation_amd.shard import select_steps
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(7)  # the same on every rank: all rings known
+    rings = rng.uniform(1.0, 2.0, (world, G, 3))
+    rings[:, :, 1] = np.arange(world)[:, None] * 100 + np.arange(G)[None, :]
+    rings[:, :, 2] = np.arange(world)[:, None]
+    rings[:, 1, 0] = 1.5              # step 1: a tie across every rank
+    rings[world - 1, 2, 0] = np.nan   # NaN never wins
+    rings[0, 3, 1] = -1.0             # an empty shard never wins
+    out = select_steps(torch.from_numpy(rings[rank].copy()), n)
+    result_q.put((rank, out[:n].numpy(), rings))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_select_steps_bucket_gloo(world):
+    G, n = 6, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_steps_worker, args=(r, world, port, G, n, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rings = res[0][2]
+    for g in range(n):
+        keys = [np.inf if (rings[w, g, 1] < 0 or np.isnan(rings[w, g, 0])) else rings[w, g, 0]
+                for w in range(world)]
+        w = int(np.argmin(keys))
+        for rank, got, _ in res:
+            assert np.array_equal(got[g], rings[w, g]), (rank, g)

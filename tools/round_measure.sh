@@ -9,6 +9,21 @@ set -e -o pipefail
 mkdir -p gpurun_out
 B() { timeout -k 10 300 python bench.py "$@"; }
 case "${1:-benches}" in
+  tests)  # bash tools/round_measure.sh tests <test files / pytest args>
+    shift
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread "$@" \
+      > gpurun_out/tests.log 2>&1
+    ;;
+  bench)  # bash tools/round_measure.sh bench <name> <bench args>
+    name=$2; shift 2
+    B "$@" > gpurun_out/bench_$name.json 2> gpurun_out/bench_$name.err
+    ;;
+  quick)  # the verdict's C2 / selection / SBPLX lines
+    B --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_c2_driver.json 2> gpurun_out/bench_c2_driver.err
+    B --steps 20 --warmup 5 --select --no-cpu-baseline > gpurun_out/bench_c2_select.json 2> gpurun_out/bench_c2_select.err
+    B --steps 20 --warmup 5 --batch 8192 --select --no-cpu-baseline > gpurun_out/bench_8192_select.json 2> gpurun_out/bench_8192_select.err
+    B --workload time --steps 5 --warmup 2 --optimizer sbplx > gpurun_out/bench_time_sbplx.json 2> gpurun_out/bench_time_sbplx.err
+    ;;
   benches)
     B > gpurun_out/bench_linear.json 2> gpurun_out/bench_linear.err
     B --batch 8192 --no-cpu-baseline > gpurun_out/bench_linear_8192.json 2> gpurun_out/bench_linear_8192.err
