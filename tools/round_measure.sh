@@ -1,24 +1,46 @@
 #!/bin/bash
-# Whole measurement pass of a round, in two gpurun calls from the repo root:
-#   bash tools/round_measure.sh benches    -- every bench line
-#   bash tools/round_measure.sh profiles   -- rocprofv3 kernel stats, HBM PMC
-#                                             passes, SQ counters, batch sweep
-# Then, in the container: tools/pmc_summary.py / tools/sq_summary.py per tag
-#  and copy the bench lines to profiles/<round>_bench_*.json.
+# Every GPU measurement of a round, as modes of one script (run from the repo
+# root through gpurun; outputs under gpurun_out/, copied to profiles/ by the
+# builder, indexed in profiles/INDEX.md):
+#
+#   tests <pytest args>      the -m gpu suite or a subset       -> tests.log
+#   bench <name> <args>      one bench.py line                  -> bench_<name>.json
+#   quick                    the driver's C2 line, C2 / 8192 with the
+#                            selection pipeline, C5 in LN_SBPLX mode
+#   benches                  every workload's bench line
+#   profiles                 rocprofv3 kernel stats + HBM PMC passes (profile.sh),
+#                            SQ instruction-mix passes (pmc_sq.sh), batch sweep
+#   ablation                 C2 kernel ablations (build_variant.sh libraries
+#                            libmtg_hip_<v>.so must be built first), K = 200
+#   ab <ENV> <args>          A/B of an environment switch of the library
+#                            (e.g. MTG_WAVE2, MTG_STD_RUNTIME_S) on one bench
+#                            line, alternating 3 times         -> ab_<ENV>.txt
+#   stamps                   s_memtime phase stamps of the C2 kernels
+#                            (make STAMPS=1 build first)
+#   ubench                   tools/ubench microbenchmarks (built in-tree)
+#
+# Helpers: tools/profile.sh, tools/pmc_sq.sh, tools/pmc_lds.sh,
+# tools/build_variant.sh; summaries: tools/pmc_summary.py,
+# tools/sq_summary.py, tools/sq_executed.py, tools/stamps_std.py.
 set -e -o pipefail
 mkdir -p gpurun_out
+export TMPDIR=/tmp
 B() { timeout -k 10 300 python bench.py "$@"; }
-case "${1:-benches}" in
-  tests)  # bash tools/round_measure.sh tests <test files / pytest args>
-    shift
+kline() {  # <json> <tag>: kernel_ms and ms_per_step of a bench line
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'kernel', round(d['roofline']['kernel_ms']*1e3,3), 'us  step', round(d['ms_per_step']*1e3,3), 'us')" "$1" "$2"
+}
+mode=${1:-benches}
+shift || true
+case "$mode" in
+  tests)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread "$@" \
       > gpurun_out/tests.log 2>&1
     ;;
-  bench)  # bash tools/round_measure.sh bench <name> <bench args>
-    name=$2; shift 2
+  bench)
+    name=$1; shift
     B "$@" > gpurun_out/bench_$name.json 2> gpurun_out/bench_$name.err
     ;;
-  quick)  # the verdict's C2 / selection / SBPLX lines
+  quick)
     B --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_c2_driver.json 2> gpurun_out/bench_c2_driver.err
     B --steps 20 --warmup 5 --select --no-cpu-baseline > gpurun_out/bench_c2_select.json 2> gpurun_out/bench_c2_select.err
     B --steps 20 --warmup 5 --batch 8192 --select --no-cpu-baseline > gpurun_out/bench_8192_select.json 2> gpurun_out/bench_8192_select.err
@@ -26,26 +48,68 @@ case "${1:-benches}" in
     ;;
   benches)
     B > gpurun_out/bench_linear.json 2> gpurun_out/bench_linear.err
+    B --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_c2_driver.json 2> gpurun_out/bench_c2_driver.err
     B --batch 8192 --no-cpu-baseline > gpurun_out/bench_linear_8192.json 2> gpurun_out/bench_linear_8192.err
+    B --batch 8192 --select --no-cpu-baseline > gpurun_out/bench_8192_select.json 2> gpurun_out/bench_8192_select.err
     B --batch 65536 --no-cpu-baseline --steps 50 --warmup 5 > gpurun_out/bench_linear_65536.json 2> gpurun_out/bench_linear_65536.err
     B --workload tube --steps 20 --warmup 3 > gpurun_out/bench_tube.json 2> gpurun_out/bench_tube.err
     B --workload time --steps 20 --warmup 3 > gpurun_out/bench_time.json 2> gpurun_out/bench_time.err
+    B --workload time --optimizer sbplx --steps 20 --warmup 3 > gpurun_out/bench_time_sbplx.json 2> gpurun_out/bench_time_sbplx.err
     B --workload time --soft --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_time_soft.json 2> gpurun_out/bench_time_soft.err
     B --workload time-qcqp --steps 5 --warmup 1 > gpurun_out/bench_time_qcqp.json 2> gpurun_out/bench_time_qcqp.err
     B --workload extrema > gpurun_out/bench_extrema.json 2> gpurun_out/bench_extrema.err
     B --workload sample > gpurun_out/bench_sample.json 2> gpurun_out/bench_sample.err
     B --workload collision --steps 5 --warmup 1 > gpurun_out/bench_collision.json 2> gpurun_out/bench_collision.err
-    B --batch 8192 --kernel lane --no-cpu-baseline > gpurun_out/bench_linear_8192_lane.json 2> gpurun_out/bench_linear_8192_lane.err
     ;;
   profiles)
     bash tools/profile.sh linear
+    bash tools/profile.sh linear_8192 --batch 8192 --steps 20 --warmup 2
     bash tools/profile.sh linear_65536 --batch 65536 --steps 20 --warmup 2
     bash tools/profile.sh tube --workload tube --steps 5 --warmup 1
     bash tools/profile.sh time --workload time --steps 5 --warmup 1
-    bash tools/pmc_sq.sh tube --workload tube --steps 5 --warmup 1
-    bash tools/pmc_sq.sh linear_65536 --batch 65536 --steps 20 --warmup 2
+    bash tools/profile.sh time_sbplx --workload time --optimizer sbplx --steps 5 --warmup 1
     bash tools/pmc_sq.sh linear
+    bash tools/pmc_sq.sh linear_8192 --batch 8192 --steps 20 --warmup 2
+    bash tools/pmc_sq.sh linear_65536 --batch 65536 --steps 20 --warmup 2
+    bash tools/pmc_sq.sh tube --workload tube --steps 5 --warmup 1
+    bash tools/pmc_sq.sh time --workload time --steps 5 --warmup 1
     timeout -k 10 300 python tools/sweep.py > gpurun_out/sweep_linear.jsonl 2>&1
+    ;;
+  ablation)
+    mkdir -p gpurun_out/abl
+    P=mav_tube_trajectory_generation_amd
+    for rep in 1 2 3; do
+      for lib in $P/libmtg_hip.so $P/libmtg_hip_*.so; do
+        v=$(basename $lib .so); v=${v#libmtg_hip}; v=${v#_}; v=${v:-base}
+        MTG_LIB_PATH=$lib B --no-cpu-baseline --steps 200 --warmup 20 \
+          > gpurun_out/abl/${v}_$rep.json 2> gpurun_out/abl/${v}_$rep.err
+        kline gpurun_out/abl/${v}_$rep.json ${v}_$rep
+      done
+    done | tee gpurun_out/ablation.txt
+    ;;
+  ab)
+    env=$1; shift
+    mkdir -p gpurun_out/ab
+    for rep in 1 2 3; do
+      for v in 0 1; do
+        env $env=$v timeout -k 10 300 python bench.py --no-cpu-baseline "$@" \
+          > gpurun_out/ab/${env}_${v}_$rep.json 2> gpurun_out/ab/${env}_${v}_$rep.err
+        kline gpurun_out/ab/${env}_${v}_$rep.json ${env}=${v}_$rep
+      done
+    done | tee -a gpurun_out/ab_$env.txt
+    ;;
+  stamps)
+    MTG_LIB_PATH=mav_tube_trajectory_generation_amd/libmtg_hip_stamps.so \
+      timeout -k 10 120 python tools/stamps_std.py 1024 > gpurun_out/stamps_c2.txt 2>&1
+    ;;
+  ubench)
+    for u in launch_floor fp64_latency store_tail graph_fixed last_arriver fetch_calib; do
+      [ -x tools/ubench/$u ] && timeout -k 10 120 tools/ubench/$u > gpurun_out/ubench_$u.txt 2>&1
+    done
+    ;;
+  *)
+    echo "unknown mode $mode" >&2
+    exit 2
     ;;
 esac
 echo ALLDONE
