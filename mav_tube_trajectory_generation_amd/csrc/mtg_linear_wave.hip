@@ -8,7 +8,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
-#include <cstdlib>
 
 #include "mtg_select_device.h"
 #include "mtg_wave_device.h"
@@ -97,143 +96,6 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   MTG_STAMP(6);
 }
 
-// The same solve on two waves per trajectory (round 5).  Wave 0 runs the
-// solver (assembly, twisted sweep, middle block, back substitution); wave 1
-// works beside it on what the solver does not wait for:
-//   * the end vertices' share of b_1 and b_(S-1) (end_terms) during wave 0's
-//     assembly, added by the sweep's first step (one barrier);
-//   * the coefficients and cost of the inner segments, as soon as the back
-//     substitution has produced their vertices (a barrier after half of its
-//     steps), stored while wave 0 finishes the outer vertices;
-//   * after the last barrier both waves take one outer range each.
-// So the end-term pass and most of the coefficient phase and its output
-// stores leave the solver's critical path (ablations at C2, K = 200:
-// without the end terms 4.98 -> 4.80 us, without the coefficient phase
-// 4.14 us; tools/gpu_r05_abl.sh).
-template <int N, int R, int D, int S>
-__global__ __launch_bounds__(2 * kWave) void linear_wave2_kernel(
-    const double* __restrict__ tab, const double* __restrict__ fixed_vals,
-    const double* __restrict__ times, double* __restrict__ coeffs, double* __restrict__ cost,
-    double* __restrict__ free_vals, int32_t* __restrict__ status, SelectArgs sel) {
-  using Sv = Solver<N, R, D, S>;
-  using G = typename Sv::G;
-  constexpr int MF = G::MF, MP = G::MP, NFIX = G::NFIX, MID = G::MID;
-  constexpr int NFW = G::NFW, NBW = G::NBW, NK = G::NK;
-  constexpr int PER = S * D * N;
-  // Back-substitution steps before the split barrier, and the vertices
-  // known then: MID, MID - 1 .. LO0 and MID + 1 .. HI0 (plus the fixed ends).
-  constexpr int kSplit = NK / 2;
-  constexpr int LO0 = MID - (kSplit < NFW ? kSplit : NFW);
-  constexpr int HI0 = MID + (kSplit < NBW ? kSplit : NBW);
-  constexpr int LO = LO0 == 1 ? 0 : LO0, HI = HI0 == S - 1 ? S : HI0;
-  __shared__ __attribute__((aligned(16))) double sm[G::L_N];
-  __shared__ __attribute__((aligned(16))) double ex[2 * D * MF];
-  __shared__ __attribute__((aligned(16))) double stage[PER];
-  __shared__ double cpart[2];
-  __shared__ int64_t ipart[2];
-  const int64_t nb = gridDim.x - (sel.prev_out ? 1 : 0);
-  if (sel.prev_out && blockIdx.x == nb) {  // the deferred selection (mtg_linear_wave.hip above)
-    select_reduce_block<2 * kWave>(sel.prev_cost, sel.prev_count, sel.prev_start, sel.rank,
-                                   sel.prev_out, cpart, ipart);
-    return;
-  }
-  const int w = static_cast<int>(threadIdx.x) / kWave;
-  Sv sv;
-  sv.init(sm);
-  const int lane = sv.lane;
-  const int64_t b = xcd_problem(blockIdx.x, nb);
-  const double* fb = fixed_vals + b * D * NFIX;
-  const double* tb = times + b * S;
-  double* T = sv.aux();
-  // Inputs, one load per lane: wave 0 d_f and the times, wave 1 H(1).
-  if (w == 0) {
-    const double f0 = fb[lane < D * NFIX ? lane : D * NFIX - 1];
-    double f1 = 0.0;
-    if constexpr (D * NFIX > kWave)
-      f1 = fb[lane + kWave < D * NFIX ? lane + kWave : D * NFIX - 1];
-    const double t_own = tb[lane < S ? lane : S - 1];
-    if (lane < D * NFIX) sv.put_fixed(lane, f0);
-    if constexpr (D * NFIX > kWave)
-      if (lane + kWave < D * NFIX) sv.put_fixed(lane + kWave, f1);
-    if (lane < S) T[lane] = t_own;
-  } else {
-    const double2 h_own =
-        *reinterpret_cast<const double2*>(tab + 2 * (lane < N * N / 2 ? lane : 0));
-    if (lane < N * N / 2) *reinterpret_cast<double2*>(sv.hh + 2 * lane) = h_own;
-  }
-  __syncthreads();
-  const double t_l = T[lane < S ? lane : S - 1];
-  const bool bad = __any(lane < S && (!(t_l > 0.0) || !(t_l < 1e300)));
-  constexpr int NP = (S - 1) * MF;
-  if (bad) {  // both waves leave here; wave 0 writes the outputs
-    if (w == 0) {
-      for (int i = lane; i < PER; i += kWave) coeffs[b * PER + i] = NAN;
-      if (free_vals)
-        for (int i = lane; i < D * NP; i += kWave) free_vals[b * D * NP + i] = NAN;
-      if (cost && lane == 0) cost[b] = NAN;
-      if (status && lane == 0) status[b] = MTG_TRAJ_BAD_TIME;
-    }
-    return;
-  }
-  double* out = coeffs + b * PER;
-  if (w == 0) {
-    const bool not_spd = sv.template solve_t<false, kSplit>(T, ex);  // barriers 1 and 2 inside
-    __syncthreads();  // 3: every vertex is in dv
-    double J = 0.0;
-    if constexpr (LO > 0) {
-      J = sv.template coeff_range<0, LO>(T, stage);
-      lds_order();
-      copy_out16<kWave, LO * D * N / 2>(reinterpret_cast<const double2*>(stage),
-                                         reinterpret_cast<double2*>(out), lane);
-    }
-    if (free_vals) {
-      for (int i = lane; i < D * NP; i += kWave) {
-        const int d = i / NP, p = i % NP;
-        const int v = p / MF + 1, kk = p % MF + 1;
-        free_vals[b * D * NP + i] = sv.dv[(v * D + d) * MP + kk];
-      }
-    }
-    __syncthreads();  // 4: wave 1's cost share
-    if (lane == 0) {
-      if (cost) cost[b] = J + cpart[1];
-      if (status) status[b] = not_spd ? MTG_TRAJ_NOT_SPD : MTG_TRAJ_OK;
-    }
-  } else {
-    sv.end_terms(T, ex);
-    __syncthreads();  // 1: E for the sweep
-    __syncthreads();  // 2: the inner vertices are in dv
-    double J = 0.0;
-    if constexpr (HI > LO) {
-      J = sv.template coeff_range<LO, HI - LO>(T, stage);
-      lds_order();
-      copy_out16<kWave, (HI - LO) * D * N / 2>(
-          reinterpret_cast<const double2*>(stage + LO * D * N),
-          reinterpret_cast<double2*>(out + LO * D * N), lane);
-    }
-    __syncthreads();  // 3: every vertex is in dv
-    if constexpr (HI < S) {
-      J += sv.template coeff_range<HI, S - HI>(T, stage);
-      lds_order();
-      copy_out16<kWave, (S - HI) * D * N / 2>(
-          reinterpret_cast<const double2*>(stage + HI * D * N),
-          reinterpret_cast<double2*>(out + HI * D * N), lane);
-    }
-    if (lane == 0) cpart[1] = J;
-    __syncthreads();  // 4
-  }
-}
-
-template <int S>
-static hipError_t launch_wave2_s(int64_t B, const SelectArgs& sel, const double* tab,
-                                 const double* df, const double* times, double* coeffs,
-                                 double* cost, double* free_vals, int32_t* status,
-                                 hipStream_t st) {
-  const int64_t blocks = B + (sel.prev_out ? 1 : 0);
-  hipLaunchKernelGGL((linear_wave2_kernel<10, 4, 3, S>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(2 * kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status, sel);
-  return hipGetLastError();
-}
-
 template <int S>
 static hipError_t launch_wave_s(int64_t B, const SelectArgs& sel, const double* tab,
                                 const double* df, const double* times, double* coeffs,
@@ -255,22 +117,6 @@ hipError_t launch_linear_solve_wave(const PlanDev& pl, int64_t B, const SelectAr
                                     const double* df,
                                     const double* times, double* coeffs, double* cost,
                                     double* free_vals, int32_t* status, hipStream_t st) {
-  // MTG_WAVE2=1 (A/B runs): the two-wave kernel
-  static const bool two = [] {
-    const char* e = std::getenv("MTG_WAVE2");
-    return e && e[0] == '1';
-  }();
-  if (two) {
-    switch (pl.S) {
-#define MTG_WAVE2_S(SS) \
-  case SS: return wave::launch_wave2_s<SS>(B, sel, pl.tab, df, times, coeffs, cost, free_vals, status, st);
-      MTG_WAVE2_S(2) MTG_WAVE2_S(3) MTG_WAVE2_S(4) MTG_WAVE2_S(5) MTG_WAVE2_S(6) MTG_WAVE2_S(7)
-      MTG_WAVE2_S(8) MTG_WAVE2_S(9) MTG_WAVE2_S(10) MTG_WAVE2_S(11) MTG_WAVE2_S(12) MTG_WAVE2_S(13)
-      MTG_WAVE2_S(14) MTG_WAVE2_S(15) MTG_WAVE2_S(16)
-#undef MTG_WAVE2_S
-      default: return hipErrorInvalidValue;
-    }
-  }
   switch (pl.S) {
 #define MTG_WAVE_S(SS) \
   case SS: return wave::launch_wave_s<SS>(B, sel, pl.tab, df, times, coeffs, cost, free_vals, status, st);

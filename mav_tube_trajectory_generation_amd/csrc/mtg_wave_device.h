@@ -154,7 +154,7 @@ struct Solver {
     slots = sm + G::L_SL;
     hh = sm + G::L_H;
     junk = sm + G::L_JUNK;
-    lane = threadIdx.x & (kWave - 1);
+    lane = threadIdx.x;
     ai = lane % MF;
     av = lane / MF + 1 < S - 1 ? lane / MF + 1 : S - 1;
     const int sd = lane < S * D ? lane : S * D - 1;
@@ -204,43 +204,10 @@ struct Solver {
     if (lane < N * N / 2) *reinterpret_cast<double2*>(hh + 2 * lane) = h_own;
   }
 
-  // The fixed end vertices' share of b_1 (segment 0) and b_(S-1) (segment
-  // S-1) on its own (the two-wave C2 kernel's second wave, beside the first
-  // wave's assembly): lane (e, d, i) < 2 D MF writes -sum_l H_seg(k, l) d_f(l)
-  // for its row to E[(e D + d) MF + i].  All lanes of the wave call.
-  __device__ void end_terms(const double* T, double* E) const {
-    const double te = T[ee ? S - 1 : 0];
-    double h[M];
-    {
-      double hr[N];
-      lds_ld(hh + ((ee ? 0 : M) + ai + 1) * N, hr);  // row k (e = 1) or M + k (e = 0)
-#pragma unroll
-      for (int l = 1; l < M; ++l) h[l] = ee ? hr[M + l] : hr[l];
-    }
-    double endd[M - 1];
-    const double* de = dv + ((ee ? S : 0) * D + ed) * MP;
-#pragma unroll
-    for (int l = 1; l < M; ++l) endd[l - 1] = de[l];
-    double qe[M];
-    row_powers<M, R>(te, i1, i2, i3, qe);
-    double s = 0.0;
-#pragma unroll
-    for (int l = 1; l < M; ++l) s = fma(h[l] * qe[l], endd[l - 1], s);
-    if (lane < 2 * D * MF) E[lane] = -s;
-  }
-
   // A solve at the segment times T (LDS, S valid values): dv receives every
   // vertex derivative.  Returns true if a pivot was not positive
   // (wave-uniform).  All lanes call.
-  __device__ bool solve(const double* T) { return solve_t<true, -1>(T, nullptr); }
-
-  // kEnd = false (the two-wave kernel): the end vertices' share of b comes
-  // from E (end_terms, the other wave) instead: the workgroup barrier after
-  // the assembly orders E, the sweep's first step and the middle block add
-  // it.  kSplit >= 0: a workgroup barrier after kSplit back-substitution
-  // steps (the other wave then computes the segments already known).
-  template <bool kEnd, int kSplit>
-  __device__ bool solve_t(const double* T, const double* E) {
+  __device__ bool solve(const double* T) {
     // With no backward step (S = 2) the middle vertex reads the backward
     // chain's terminal slot as zero; otherwise its last step writes it.
     if constexpr (NBW == 0) {
@@ -315,9 +282,6 @@ struct Solver {
     MTG_STAMP(12);
     // The fully fixed end vertices' part of b_1 (segment 0) and b_(S-1)
     // (segment S-1): lane (e, d, i) adds -sum_l H_seg(k, l) d_f(l) for its row.
-    if constexpr (!kEnd) {
-      __syncthreads();  // E written by the other wave
-    } else {
 #ifndef MTG_ABL_NOEND
     {
       double qe[M];
@@ -329,7 +293,6 @@ struct Solver {
       atomicAdd(slot_of(ee ? S - 1 : 1) + O_R + ed * MF + ai, lane < 2 * D * MF ? -s : 0.0);
     }
 #endif
-    }
     lds_order();
     MTG_STAMP(2);
 
@@ -377,14 +340,6 @@ struct Solver {
                 for (int c = 0; c <= r; ++c) Sv[r][c] = t[tri(r, c)];
             }
             lds_ld(Up + k * SLOT, u);
-            if constexpr (!kEnd) {
-              if (k == 0) {  // b_1 / b_(S-1): the end vertices' share from E
-                double e4[MF];
-                lds_ld(E + (g * D + (colj ? 0 : dd)) * MF, e4);
-#pragma unroll
-                for (int m = 0; m < MF; ++m) u[m] = colj ? u[m] : u[m] + e4[m];
-              }
-            }
             double pcn[MF], an = 0.0;
             if (k + 1 < NK) {  // next step's coupling row and Schur / rhs entry
               lds_ld(Pp + (k + 1) * SLOT, pcn);
@@ -442,16 +397,6 @@ struct Solver {
         lds_ld(mb + O_R + dc * MF, r1);
 #pragma unroll
         for (int r = 0; r < MF; ++r) rr[r] = r0[r] + r1[r];
-        if constexpr (!kEnd && (NFW == 0 || NBW == 0)) {  // the middle is vertex 1 or S-1
-          double e0[MF], e1[MF];
-          lds_ld(E + dc * MF, e0);
-          lds_ld(E + (D + dc) * MF, e1);
-#pragma unroll
-          for (int r = 0; r < MF; ++r) {
-            if (NFW == 0) rr[r] += e0[r];
-            if (NBW == 0) rr[r] += e1[r];
-          }
-        }
       }
       // every back-substitution operand in flight before the middle solve
       const int nst = g ? NBW : NFW;
@@ -471,12 +416,6 @@ struct Solver {
       *(p_act && g == 0 ? dv + (MID * D + d) * MP + 1 + ii : junk + ii) = xi;
 #pragma unroll
       for (int t = 0; t < NK; ++t) {
-        if constexpr (kSplit >= 0) {
-          if (t == kSplit) {
-            lds_order();
-            __syncthreads();  // the vertices so far are in dv (the other wave reads them)
-          }
-        }
         if (NFW == NBW || t < nst) {
           const double xb0 = quad_bcast<0>(xi), xb1 = quad_bcast<1>(xi);
           const double xb2 = quad_bcast<2>(xi), xb3 = quad_bcast<3>(xi);
@@ -488,10 +427,6 @@ struct Solver {
           const int v = g ? S - 1 - sidx : 1 + sidx;
           *(p_act ? dv + (v * D + d) * MP + 1 + ii : junk + 4 + ii) = xi;
         }
-      }
-      if constexpr (kSplit >= 0 && kSplit >= NK) {  // the split barrier exactly once
-        lds_order();
-        __syncthreads();
       }
     }
     const bool not_spd = __any(!(pmin > 0.0));
@@ -549,59 +484,6 @@ struct Solver {
 #pragma unroll
         for (int i = 0; i < N / 2; ++i) o2[i] = make_double2(cc[2 * i], cc[2 * i + 1]);
       }
-      acc = stdp::Solver<N, R, D>::q_form(h) * ipow<1 - 2 * R>(ts, inv);
-    }
-    return wave_sum_dpp(acc);
-  }
-
-  // coeff_cost for the segments S0 .. S0+NS-1 only (the two-wave kernel's
-  // passes): lane (S0 + lane / D, lane % D) < NS D; the coefficients go to
-  // out + (s D + d) N (the output layout, LDS); returns the range's cost
-  // share (wave-uniform).
-  template <int S0, int NS>
-  __device__ double coeff_range(const double* T, double* out) const {
-    double acc = 0.0;
-    if (lane < NS * D) {
-      constexpr AInvTab<N> kA{};
-      const int s = S0 + lane / D, d = lane % D;
-      const double ts = T[s];
-      double e[N], f[N], h[N];
-      {
-        double e0[MP], e1[MP];
-        lds_ld(dv + (s * D + d) * MP, e0);
-        lds_ld(dv + ((s + 1) * D + d) * MP, e1);
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-          e[j] = e0[j];
-          e[M + j] = e1[j];
-        }
-      }
-      const double inv = rcp64_1(ts);
-      double tp[M], tn[N];
-      tp[0] = 1.0;
-      tn[0] = 1.0;
-#pragma unroll
-      for (int j = 1; j < M; ++j) tp[j] = (j & 1) ? tp[j - 1] * ts : tp[j / 2] * tp[j / 2];
-#pragma unroll
-      for (int j = 1; j < N; ++j) tn[j] = (j & 1) ? tn[j - 1] * inv : tn[j / 2] * tn[j / 2];
-#pragma unroll
-      for (int j = 0; j < N; ++j) f[j] = e[j] * tp[j % M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) h[i] = kA.v[i * N + i] * f[i];
-#pragma unroll
-      for (int i = M; i < N; ++i) {
-        double t = 0.0;
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-          if (kA.v[i * N + j] != 0.0) t = fma(kA.v[i * N + j], f[j], t);
-        h[i] = t;
-      }
-      double cc[N];
-#pragma unroll
-      for (int i = 0; i < N; ++i) cc[i] = h[i] * tn[i];
-      double2* o2 = reinterpret_cast<double2*>(out + static_cast<int64_t>(s * D + d) * N);
-#pragma unroll
-      for (int i = 0; i < N / 2; ++i) o2[i] = make_double2(cc[2 * i], cc[2 * i + 1]);
       acc = stdp::Solver<N, R, D>::q_form(h) * ipow<1 - 2 * R>(ts, inv);
     }
     return wave_sum_dpp(acc);

@@ -10,8 +10,11 @@
 #   benches                  every workload's bench line
 #   profiles                 rocprofv3 kernel stats + HBM PMC passes (profile.sh),
 #                            SQ instruction-mix passes (pmc_sq.sh), batch sweep
-#   ablation                 C2 kernel ablations (build_variant.sh libraries
-#                            libmtg_hip_<v>.so must be built first), K = 200
+#   ablation [bench args]    every libmtg_hip_<v>.so variant (build_variant.sh)
+#                            against the product library, alternating 3 times;
+#                            default the C2 line at K = 200   -> ablation.txt
+#   tube                     the tube parity tests, the config-3 line and the
+#                            400-seed status agreement with the oracle
 #   ab <ENV> <args>          A/B of an environment switch of the library
 #                            (e.g. MTG_WAVE2, MTG_STD_RUNTIME_S) on one bench
 #                            line, alternating 3 times         -> ab_<ENV>.txt
@@ -75,17 +78,27 @@ case "$mode" in
     bash tools/pmc_sq.sh time --workload time --steps 5 --warmup 1
     timeout -k 10 300 python tools/sweep.py > gpurun_out/sweep_linear.jsonl 2>&1
     ;;
-  ablation)
+  ablation)  # [bench args]: default the C2 line at K = 200
     mkdir -p gpurun_out/abl
     P=mav_tube_trajectory_generation_amd
+    args=("$@"); [ ${#args[@]} -eq 0 ] && args=(--steps 200 --warmup 20)
     for rep in 1 2 3; do
       for lib in $P/libmtg_hip.so $P/libmtg_hip_*.so; do
         v=$(basename $lib .so); v=${v#libmtg_hip}; v=${v#_}; v=${v:-base}
-        MTG_LIB_PATH=$lib B --no-cpu-baseline --steps 200 --warmup 20 \
+        MTG_LIB_PATH=$lib B --no-cpu-baseline "${args[@]}" \
           > gpurun_out/abl/${v}_$rep.json 2> gpurun_out/abl/${v}_$rep.err
         kline gpurun_out/abl/${v}_$rep.json ${v}_$rep
       done
     done | tee gpurun_out/ablation.txt
+    ;;
+  tube)
+    mkdir -p gpurun_out/tube
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread \
+      tests/test_tube_gpu.py tests/test_tube_time_gpu.py tests/test_configs_gpu.py -k "tube or config3" \
+      > gpurun_out/tube/tests.log 2>&1
+    B --workload tube --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/tube/bench.json 2> gpurun_out/tube/bench.err
+    kline gpurun_out/tube/bench.json tube
+    timeout -k 10 300 python tools/tube_status_agreement.py r05 > gpurun_out/tube/agreement.txt 2>&1
     ;;
   ab)
     env=$1; shift
