@@ -542,8 +542,10 @@ __device__ __attribute__((always_inline)) inline void lane2_half(
 }  // namespace lane2
 
 // Workgroup = 2 waves (forward, backward) over 21 trajectories x 3
-// dimensions; the direction is wave-uniform.
-template <int N, int R, int D, int S>
+// dimensions; the direction is wave-uniform.  kPrev: the launch carries the
+// deferred selection's workgroup (a template parameter so that the solves do
+// not wait on the kernel arguments past the preloaded ones; mtg_linear_wave.hip).
+template <int N, int R, int D, int S, bool kPrev>
 __global__ __launch_bounds__(2 * kWave) void linear_lane2_kernel(
     int64_t B, const double* __restrict__ fixed_vals, const double* __restrict__ times,
     double* __restrict__ coeffs, double* __restrict__ cost, double* __restrict__ free_vals,
@@ -555,12 +557,20 @@ __global__ __launch_bounds__(2 * kWave) void linear_lane2_kernel(
   // The deferred selection (the previous step's costs, SelectArgs::prev_*)
   // in one extra workgroup, dispatched first (block 0) so that it ends well
   // before the solves' (8192 costs: four rounds of loads by 128 threads).
-  const int blk = static_cast<int>(blockIdx.x) - (sel.prev_out ? 1 : 0);
-  if (blk < 0) {
+  const int blk = static_cast<int>(blockIdx.x) - (kPrev ? 1 : 0);
+  if (kPrev && blk < 0) {
     select_reduce_block<2 * kWave>(sel.prev_cost, sel.prev_count, sel.prev_start, sel.rank,
                                    sel.prev_out, cxch, reinterpret_cast<int64_t*>(xch));
     return;
   }
+  // The staging area is static LDS on every launch (it is not used below
+  // kLane2StageMinBatch): 50 KB at S = 10, 75 KB at S = 12 with the exchange
+  // buffers.  Above 64 KB per workgroup this builds for gfx950 (160 KB LDS
+  // per CU) only, the one target of this library; two workgroups per CU is
+  // the occupancy one wave per SIMD allows anyway.
+  static_assert(sizeof(double) * ((kWave / D) * S * D * N + 2 * (H::NT + H::MF) * kWave +
+                                  kWave) + sizeof(int) * kWave <= 160 * 1024 / 2,
+                "lane-pair LDS must leave room for two workgroups per gfx950 CU");
   __shared__ __attribute__((aligned(16))) double stage[(kWave / D) * S * D * N];
   if (threadIdx.x < kWave)
     lane2::lane2_half<N, R, D, S, false>(B, blk, fixed_vals, times, coeffs, cost, free_vals,
@@ -577,9 +587,13 @@ hipError_t launch_lane2(int64_t B, const double* df, const double* times, double
                         double* cost, double* free_vals, int32_t* status, hipStream_t st,
                         const SelectArgs& sel) {
   constexpr int TPW = kWave / D;
-  const int64_t blocks = (B + TPW - 1) / TPW + (sel.prev_out ? 1 : 0);
-  hipLaunchKernelGGL((linear_lane2_kernel<N, R, D, S>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(2 * kWave), 0, st, B, df, times, coeffs, cost, free_vals, status, sel);
+  const int64_t blocks = (B + TPW - 1) / TPW;
+  if (sel.prev_out)
+    hipLaunchKernelGGL((linear_lane2_kernel<N, R, D, S, true>), dim3(static_cast<unsigned>(blocks + 1)),
+                       dim3(2 * kWave), 0, st, B, df, times, coeffs, cost, free_vals, status, sel);
+  else
+    hipLaunchKernelGGL((linear_lane2_kernel<N, R, D, S, false>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(2 * kWave), 0, st, B, df, times, coeffs, cost, free_vals, status, sel);
   return hipGetLastError();
 }
 

@@ -15,11 +15,20 @@
 namespace mtg {
 namespace wave {
 
-template <int N, int R, int D, int S>
+// The problem count nb is an argument in the first 64 bytes (the first 56
+// are preloaded into SGPRs; nb is the one scalar load before the first
+// global load, as gridDim.x was in round 4), and kPrev (this launch carries
+// the deferred selection's workgroup) a template parameter.  With the
+// selection arguments appended, reading gridDim.x (a hidden argument after
+// them, byte 128) and testing sel.prev_out in every workgroup measured
+// 4.62 -> 4.99 us at C2, K = 200 (profiles/r05_kernarg_abl_c2.txt); moving nb
+// into the preloaded bytes as well (free_vals after it) gave no gain
+// (4.65 - 4.71 us, profiles/r05_kernarg_abl_c2_v2.txt).
+template <int N, int R, int D, int S, bool kPrev>
 __global__ __launch_bounds__(kWave) void linear_wave_kernel(
     const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     const double* __restrict__ times, double* __restrict__ coeffs, double* __restrict__ cost,
-    double* __restrict__ free_vals, int32_t* __restrict__ status, SelectArgs sel) {
+    double* __restrict__ free_vals, int32_t* __restrict__ status, int nb, SelectArgs sel) {
   using Sv = Solver<N, R, D, S>;
   using G = typename Sv::G;
   constexpr int MF = G::MF, MP = G::MP, NFIX = G::NFIX;
@@ -27,8 +36,7 @@ __global__ __launch_bounds__(kWave) void linear_wave_kernel(
   // The deferred selection (the previous step's costs) in one extra
   // workgroup after the solves: it runs beside them (about 1 us at
   // B = 1024 against a 3.4 us solve), so it costs no launch of its own.
-  const int64_t nb = gridDim.x - (sel.prev_out ? 1 : 0);
-  if (sel.prev_out && blockIdx.x == nb) {
+  if (kPrev && static_cast<int>(blockIdx.x) == nb) {
     select_reduce_block<kWave>(sel.prev_cost, sel.prev_count, sel.prev_start, sel.rank,
                                sel.prev_out, nullptr, nullptr);
     return;
@@ -101,9 +109,12 @@ static hipError_t launch_wave_s(int64_t B, const SelectArgs& sel, const double* 
                                 const double* df, const double* times, double* coeffs,
                                 double* cost, double* free_vals, int32_t* status,
                                 hipStream_t st) {
-  const int64_t blocks = B + (sel.prev_out ? 1 : 0);
-  hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status, sel);
+  if (sel.prev_out)
+    hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S, true>), dim3(static_cast<unsigned>(B + 1)),
+                       dim3(kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status, static_cast<int>(B), sel);
+  else
+    hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status, static_cast<int>(B), sel);
   return hipGetLastError();
 }
 
