@@ -390,6 +390,55 @@ struct Tube {
     return type == 2 ? (G[16] - nc) : (nc - G[17]);
   }
 
+  // Every constraint on control point (i, j) at control points `cpo`, in
+  // con_at's slots: slot 0 the tube (1 <= j <= N-2) or the sphere (j = N-1,
+  // i < S-1), slots 1 and 2 the end caps (1 <= j <= N-2); k[t] = -1 marks an
+  // absent slot.  con_eval's arithmetic without its per-constraint decode and
+  // type branches (round 5): the tube, sphere and cap formulas run on every
+  // lane and slot 0 selects, so a wave whose lanes hold different j does not
+  // serialise the types.  h0 = 1 selects slot 0's Hessian factor 2 I
+  // (sphere) over 2 LL (tube); the caps' is 0.
+  __device__ void cp_cons(int i, int j, int cpo, int (&k)[3], double (&g)[3],
+                          double (&w)[3][3], bool& sph) const {
+    const double* cv = sm + cpo + (i * N + j) * 3;
+    const double* G = sm + L->geo + i * kGeo;
+    const bool mid = j >= 1 && j <= N - 2;
+    sph = j == N - 1 && i < S - 1;
+    const int eb = seg_base(i) + (i < S - 1 ? 1 : 0);
+    k[0] = mid ? eb + (j - 1) : (sph ? seg_base(i) : -1);
+    k[1] = mid ? eb + (N - 2) + 2 * (j - 1) : -1;
+    k[2] = mid ? eb + (N - 2) + 2 * (j - 1) + 1 : -1;
+    const double c[3] = {cv[0], cv[1], cv[2]};
+    double gt = G[15], wt[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {  // tube (qcqp_impl:369-429)
+      double llc = 0.0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) llc += G[3 + a * 3 + e] * c[e];
+      gt += c[a] * llc + G[12 + a] * c[a];
+      wt[a] = 2.0 * llc + G[12 + a];
+    }
+    const double* p = sm + L->pos + (i + 1) * 3;  // sphere (qcqp_impl:357-365)
+    double gs = -G[18], ws[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const double e = c[d] - p[d];
+      gs += e * e;
+      ws[d] = 2.0 * e;
+    }
+    g[0] = sph ? gs : gt;
+    double nc = 0.0;  // end caps (qcqp_impl:431-474)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      w[0][d] = sph ? ws[d] : wt[d];
+      nc += G[d] * c[d];
+      w[1][d] = -1.0 * G[d];
+      w[2][d] = 1.0 * G[d];
+    }
+    g[1] = G[16] - nc;
+    g[2] = nc - G[17];
+  }
+
   // Hessian factor of constraint type (w.r.t. the control point): 2 I, 2 LL, 0.
   __device__ double con_hess(int type, int i, int a, int e) const {
     if (type == 0) return a == e ? 2.0 : 0.0;
@@ -431,35 +480,9 @@ struct Tube {
 
   // --------------------------------------------------------- KKT assembly
   // Per control point: G = sum_k lam_k Hess_k + (lam_k / s_k) w_k w_k^T over
-  // the (at most 3) constraints acting on it.  The diagonal KKT block of
-  // vertex a is K_a = I_3 (x) Pd_a + sum_cp G_cp (x) beta_cp beta_cp^T; its
-  // columns are built in registers by factor().
-  __device__ void assemble_g() {
-    double* Gcp = sm + L->Gc;
-    for (int cpi = tid; cpi < S * N; cpi += nthr) {
-      const int i = cpi / N, j = cpi % N;
-      double G[9];
-#pragma unroll
-      for (int e = 0; e < 9; ++e) G[e] = 0.0;
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int k = con_at(i, j, t);
-        if (k < 0) continue;
-        double w[3];
-        con_eval(k, L->cp, w);
-        int ii, jj, type;
-        con_of(k, &ii, &jj, &type);
-        const double lam = sm[L->lam + k], s = sm[L->s + k];
-        const double ws = lam / s;
-          for (int a = 0; a < 3; ++a)
-          for (int e = 0; e < 3; ++e)
-            G[a * 3 + e] += lam * con_hess(type, i, a, e) + ws * w[a] * w[e];
-      }
-      for (int a = 0; a < 3; ++a)
-        for (int e = a; e < 3; ++e) Gcp[cpi * 6 + gsym(a, e)] = G[a * 3 + e];
-    }
-    __syncthreads();
-  }
+  // the (at most 3) constraints acting on it (ipm's residual pass).  The
+  // diagonal KKT block of vertex a is K_a = I_3 (x) Pd_a + sum_cp G_cp (x)
+  // beta_cp beta_cp^T; its columns are built in registers by factor().
 
   // 1 if x == 0 else 0 (integer arithmetic, see is_zero).
   __device__ static int izero(int x) { return ((x | -x) >> 31) + 1; }
@@ -891,16 +914,18 @@ struct Tube {
     for (int cpi = tid; cpi < S * N; cpi += nthr) {
       const int i = cpi / N, j = cpi % N;
       double P3[3] = {0.0, 0.0, 0.0};
+      int kk[3];
+      double gg[3], ww[3][3];
+      bool sph;
+      cp_cons(i, j, L->cp, kk, gg, ww, sph);
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const int k = con_at(i, j, t);
+        const int k = kk[t];
         if (k < 0) continue;
-        double w[3];
-        const double g = con_eval(k, L->cp, w);
         const double lam = sm[L->lam + k], s = sm[L->s + k];
-        const double rp = g + s;
+        const double rp = gg[t] + s;
         const double coef = (lam * rp - rc_of<kCorr>(k, smu)) / s;
-        for (int d = 0; d < 3; ++d) P3[d] += w[d] * coef;
+        for (int d = 0; d < 3; ++d) P3[d] += ww[t][d] * coef;
       }
       for (int d = 0; d < 3; ++d) sm[L->acc + cpi * 3 + d] = P3[d];
     }
@@ -916,19 +941,26 @@ struct Tube {
     MTG_TACC(210, tl);
     control_point_steps(sm + L->dx, L->acc);
     __syncthreads();
-    for (int k = tid; k < nc; k += nthr) {
-      double w[3];
-      const double g = con_eval(k, L->cp, w);
-      int i, j, type;
-      con_of(k, &i, &j, &type);
-      const double* dc = sm + L->acc + (i * N + j) * 3;
-      const double adx = w[0] * dc[0] + w[1] * dc[1] + w[2] * dc[2];
-      const double lam = sm[L->lam + k], s = sm[L->s + k];
-      const double rp = g + s;
-      const double rc = rc_of<kCorr>(k, smu);
-      const double dl = (lam / s) * (adx + rp) - rc / s;
-      sm[L->dl + k] = dl;
-      sm[L->ds + k] = (-rc - s * dl) / lam;
+    // dl, ds per control point (its constraints' (g, w) evaluated once).
+    for (int cpi = tid; cpi < S * N; cpi += nthr) {
+      const int i = cpi / N, j = cpi % N;
+      int kk[3];
+      double gg[3], ww[3][3];
+      bool sph;
+      cp_cons(i, j, L->cp, kk, gg, ww, sph);
+      const double* dc = sm + L->acc + cpi * 3;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int k = kk[t];
+        if (k < 0) continue;
+        const double adx = ww[t][0] * dc[0] + ww[t][1] * dc[1] + ww[t][2] * dc[2];
+        const double lam = sm[L->lam + k], s = sm[L->s + k];
+        const double rp = gg[t] + s;
+        const double rc = rc_of<kCorr>(k, smu);
+        const double dl = (lam / s) * (adx + rp) - rc / s;
+        sm[L->dl + k] = dl;
+        sm[L->ds + k] = (-rc - s * dl) / lam;
+      }
     }
     __syncthreads();
   }
@@ -1000,22 +1032,28 @@ struct Tube {
         double G[9];
 #pragma unroll
         for (int e = 0; e < 9; ++e) G[e] = 0.0;
+        int kk[3];
+        double gg[3], ww[3][3];
+        bool sph;
+        cp_cons(i, j, L->cp, kk, gg, ww, sph);
+        const double* LL = sm + L->geo + i * kGeo + 3;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-          const int k = con_at(i, j, t);
+          const int k = kk[t];
           if (k < 0) continue;
-          double w[3];
-          const double g = con_eval(k, L->cp, w);
-          int ii, jj, type;
-          con_of(k, &ii, &jj, &type);
           const double s = sm[L->s + k], lam = sm[L->lam + k];
-          rpn = fmax(rpn, fabs(g + s));
+          rpn = fmax(rpn, fabs(gg[t] + s));
           mu += s * lam;
-          for (int d = 0; d < 3; ++d) O3[d] += lam * w[d];
+          for (int d = 0; d < 3; ++d) O3[d] += lam * ww[t][d];
           const double ws = lam / s;
+#pragma unroll
           for (int a = 0; a < 3; ++a)
-            for (int e = 0; e < 3; ++e)
-              G[a * 3 + e] += lam * con_hess(type, i, a, e) + ws * w[a] * w[e];
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+              // con_hess: 2 I (sphere), 2 LL (tube), 0 (caps)
+              const double h = t > 0 ? 0.0 : (sph ? (a == e ? 2.0 : 0.0) : 2.0 * LL[a * 3 + e]);
+              G[a * 3 + e] += lam * h + ws * ww[t][a] * ww[t][e];
+            }
         }
         for (int d = 0; d < 3; ++d) sm[L->acc + cpi * 3 + d] = O3[d];
         for (int a = 0; a < 3; ++a)
