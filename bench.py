@@ -265,19 +265,33 @@ def device_kernel(wl, plan, B, N, D, r, S):
     return {"sample": "sample_kernel", "collision": "coll_walk_kernel"}[wl]
 
 
+# rocprofv3's kernel trace adds a per-dispatch cost of its own: the C2
+# kernel (4.6 us unprofiled) averages 5.2-5.7 us in the trace passes and its
+# event-timed launches 5.2-7.6 us in the same runs (round 5), so a profiled
+# average may exceed this run's time by that much on the same build.
+PROFILER_SLACK_MS = 0.0012
+
+
+def same_build_time(profiled_ms, kernel_ms):
+    """A profiled kernel time (avg_ns of a committed rocprofv3 pass) that can
+    come from this build: within 15 % of this run's kernel time, plus the
+    profiler's per-dispatch cost above it."""
+    return 0.85 * kernel_ms <= profiled_ms <= 1.15 * kernel_ms + PROFILER_SLACK_MS
+
+
 def load_pmc_traffic(key, kernel_ms):
     """HBM bytes per launch of this workload's kernel from the committed
     rocprofv3 PMC passes (profiles/pmc_traffic.json, keyed
     workload:batch:segments:kernel), or None.  An entry whose kernel time
-    differs from this run's by more than 15 % was measured on another build
-    and is not used."""
+    differs from this run's by more than 15 % (plus, above, the profiler's own
+    per-dispatch cost, PROFILER_SLACK_MS) was measured on another build and
+    is not used."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             entry = json.load(f).get(key)
         if entry and entry.get("avg_ns"):
-            ratio = entry["avg_ns"] * 1e-6 / kernel_ms
-            if 0.85 <= ratio <= 1.15:
+            if same_build_time(entry["avg_ns"] * 1e-6, kernel_ms):
                 return entry.get("bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -295,8 +309,7 @@ def load_sq_executed(config_key, kernel_ms):
         with open(path) as f:
             entry = json.load(f).get(config_key)
         if entry and entry.get("avg_ns"):
-            ratio = entry["avg_ns"] * 1e-6 / kernel_ms
-            if 0.85 <= ratio <= 1.15:
+            if same_build_time(entry["avg_ns"] * 1e-6, kernel_ms):
                 return entry["executed_f64_flop_per_trajectory"], entry["source"]
     except (OSError, ValueError, KeyError):
         pass
@@ -879,7 +892,8 @@ def main():
     value = total_units / elapsed
     alg_bytes = bytes_per_traj * B
     gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    config_key = f"{wl}:B{B}:S{S}" + (":soft" if getattr(args, "soft", False) else "")
+    config_key = (f"{wl}:B{B}:S{S}" + (":soft" if getattr(args, "soft", False) else "")
+                  + (":sbplx" if wl == "time" and args.optimizer == "sbplx" else ""))
     dev_kernel = device_kernel(wl, plan, B, N, D, r, S)
     traffic = load_pmc_traffic(f"{config_key}:{dev_kernel}", kernel_ms)
     timing = ("HIP events around one graph replay of the K steps, / K" if use_graph else

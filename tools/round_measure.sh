@@ -18,8 +18,8 @@
 #   ab <ENV> <args>          A/B of an environment switch of the library
 #                            (e.g. MTG_WAVE2, MTG_STD_RUNTIME_S) on one bench
 #                            line, alternating 3 times         -> ab_<ENV>.txt
-#   stamps                   s_memtime phase stamps of the C2 kernels
-#                            (make STAMPS=1 build first)
+#   stamps                   s_memtime phase stamps of the C2 kernel and the
+#                            tube IPM (make STAMPS=1 build first)
 #   ubench                   tools/ubench microbenchmarks (built in-tree)
 #
 # Helpers: tools/profile.sh, tools/pmc_sq.sh, tools/pmc_lds.sh,
@@ -112,8 +112,10 @@ case "$mode" in
     done | tee -a gpurun_out/ab_$env.txt
     ;;
   stamps)
-    MTG_LIB_PATH=mav_tube_trajectory_generation_amd/libmtg_hip_stamps.so \
+    STAMPS_SYM=wave MTG_LIB_PATH=mav_tube_trajectory_generation_amd/libmtg_hip_stamps.so \
       timeout -k 10 120 python tools/stamps_std.py 1024 > gpurun_out/stamps_c2.txt 2>&1
+    MTG_LIB_PATH=mav_tube_trajectory_generation_amd/libmtg_hip_stamps.so \
+      timeout -k 10 120 python tools/tube_stamps.py 4096 > gpurun_out/stamps_tube.txt 2>&1
     ;;
   ubench)
     for u in launch_floor fp64_latency store_tail graph_fixed last_arriver fetch_calib; do
