@@ -65,6 +65,12 @@ def parse():
     p.add_argument("--sync", choices=["spin", "auto"], default=os.environ.get("MTG_BENCH_SYNC", "auto"),
                    help="host wait mode of the HIP runtime (hipSetDeviceFlags): spin polls for "
                         "completion, auto is the runtime's default")
+    p.add_argument("--events", choices=["device", "system"],
+                   default=os.environ.get("MTG_BENCH_EVENTS", "system"),
+                   help="release scope of the two timing events around the timed replay: "
+                        "device (hipEventDisableSystemFence, HIP's flag for events used only "
+                        "to time) or system (hipEventRecord's default, with a system-scope "
+                        "cache writeback and invalidation at each event)")
     return p.parse_args()
 
 
@@ -270,6 +276,69 @@ def device_kernel(wl, plan, B, N, D, r, S):
 # event-timed launches 5.2-7.6 us in the same runs (round 5), so a profiled
 # average may exceed this run's time by that much on the same build.
 PROFILER_SLACK_MS = 0.0012
+
+
+class TimingEvents:
+    """The two events around the timed replay, recorded on the launch stream
+    through the HIP runtime torch loaded.  scope "device" creates them with
+    hipEventDisableSystemFence: HIP documents it for events used only to
+    time, "avoiding the cost of cache writeback and invalidation" that a
+    default event's system-scope fence adds when it is recorded (a fixed
+    cost per replay that the K launches would otherwise share).  The host
+    still waits for the work with torch.cuda.synchronize, so the wall-clock
+    ms_per_step is unaffected.  scope "system": torch's default events."""
+
+    def __init__(self, scope):
+        import ctypes
+        import torch
+        self.scope = scope
+        if scope == "system":
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            return
+        path = None
+        with open("/proc/self/maps") as f:  # the runtime torch has mapped
+            for line in f:
+                if "libamdhip64.so" in line:
+                    path = line.split()[-1]
+                    break
+        self.hip = hip = ctypes.CDLL(path or "libamdhip64.so")
+        hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+        hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                            ctypes.c_void_p]
+        hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.ev = (ctypes.c_void_p(), ctypes.c_void_p())
+        for e in self.ev:
+            rc = hip.hipEventCreateWithFlags(ctypes.byref(e), 0x20000000)  # DisableSystemFence
+            if rc != 0:
+                raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
+
+    def record(self, i, stream):
+        if self.scope == "system":
+            self.ev[i].record(stream)
+            return
+        rc = self.hip.hipEventRecord(self.ev[i], ctypes_stream(stream))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed ({rc})")
+
+    def elapsed_ms(self):
+        if self.scope == "system":
+            return self.ev[0].elapsed_time(self.ev[1])
+        import ctypes
+        ms = ctypes.c_float()
+        rc = self.hip.hipEventSynchronize(self.ev[1])
+        rc = rc or self.hip.hipEventElapsedTime(ctypes.byref(ms), self.ev[0], self.ev[1])
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
+        for e in self.ev:
+            self.hip.hipEventDestroy(e)
+        return float(ms.value)
+
+
+def ctypes_stream(stream):
+    import ctypes
+    return ctypes.c_void_p(stream.cuda_stream)
 
 
 def same_build_time(profiled_ms, kernel_ms):
@@ -818,18 +887,18 @@ def main():
     torch.cuda.synchronize(dev)
 
     if use_graph:
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tev = TimingEvents(args.events)
         t0 = time.perf_counter()
-        ev0.record(stream)
+        tev.record(0, stream)
         for g in graphs["timed"]:
             g.replay()
-        ev1.record(stream)
+        tev.record(1, stream)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
-        kernel_ms = ev0.elapsed_time(ev1) / args.steps
+        kernel_ms = tev.elapsed_ms() / args.steps
     else:
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
@@ -859,7 +928,7 @@ def main():
             step_selected()
         end_steps()
         torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        sev = TimingEvents(args.events)
         if use_graph:
             try:
                 gs = torch.cuda.CUDAGraph()
@@ -873,17 +942,17 @@ def main():
                 sys.exit(3)
             gs.replay()  # warm replay, then the timed one
             torch.cuda.synchronize(dev)
-            e0.record(stream)
+            sev.record(0, stream)
             gs.replay()
-            e1.record(stream)
+            sev.record(1, stream)
         else:
-            e0.record(stream)
+            sev.record(0, stream)
             for _ in range(args.steps):
                 step_selected()
             end_steps()
-            e1.record(stream)
+            sev.record(1, stream)
         torch.cuda.synchronize(dev)
-        selection_ms = e0.elapsed_time(e1) / args.steps
+        selection_ms = sev.elapsed_ms() / args.steps
 
     if useful_per_step is not None:
         total_units = useful_per_step * args.steps * world
@@ -896,7 +965,8 @@ def main():
                   + (":sbplx" if wl == "time" and args.optimizer == "sbplx" else ""))
     dev_kernel = device_kernel(wl, plan, B, N, D, r, S)
     traffic = load_pmc_traffic(f"{config_key}:{dev_kernel}", kernel_ms)
-    timing = ("HIP events around one graph replay of the K steps, / K" if use_graph else
+    timing = (f"HIP events ({args.events}-scope release) around one graph replay of the K "
+              "steps, / K" if use_graph else
               "HIP event pair per step, mean (--no-graph)")
     hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
            "alg_bytes_per_launch": alg_bytes, "traffic": traffic}

@@ -35,3 +35,23 @@ def test_world_size_mismatch_fails_loudly():
                        env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
     assert p.returncode != 0
     assert "WORLD_SIZE" in p.stderr
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_profiled_entry_guard():
+    """Committed PMC / SQ entries are used only when their profiled kernel
+    time can come from this build: within 15 % of the run's, plus the
+    profiler's per-dispatch cost above it."""
+    b = _bench_module()
+    assert b.same_build_time(0.0057, 0.0046)       # C2 under the kernel trace
+    assert not b.same_build_time(0.0080, 0.0046)   # another build
+    assert not b.same_build_time(0.0030, 0.0046)
+    assert b.same_build_time(7.63, 7.47)           # tube: the slack is negligible
+    assert not b.same_build_time(9.0, 7.47)

@@ -153,3 +153,37 @@ def test_stale_error_not_reported(ctx, dev):
     out = plan.solve(fd, td)  # raises MTGError if the stale error leaked
     torch.cuda.synchronize()
     assert (out["status"].cpu().numpy() == 0).all()
+
+
+def test_bench_timing_events(ctx, dev):
+    """bench.py's timing events: device scope (hipEventDisableSystemFence,
+    recorded through the HIP runtime torch mapped) and torch's system-scope
+    events both time a replayed graph of solves."""
+    import importlib.util
+    import os
+    import mav_tube_trajectory_generation_amd as mtg
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+    spec = importlib.util.spec_from_file_location("bench_mod", path)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    S, B = 10, 1024
+    mask, fixed, times, _ = _problems(S, B)
+    plan = mtg.LinearPlan(ctx, N, D, R, S, mask)
+    fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
+    out = plan.solve(fd, td)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(20):
+            plan.solve(fd, td, out=out)
+    g.replay()
+    torch.cuda.synchronize()
+    for scope in ("device", "system"):
+        ev = bench.TimingEvents(scope)
+        ev.record(0, stream)
+        g.replay()
+        ev.record(1, stream)
+        torch.cuda.synchronize()
+        ms = ev.elapsed_ms()
+        assert 0.0 < ms < 50.0, (scope, ms)

@@ -18,6 +18,9 @@
 #   ab <ENV> <args>          A/B of an environment switch of the library
 #                            (e.g. MTG_WAVE2, MTG_STD_RUNTIME_S) on one bench
 #                            line, alternating 3 times         -> ab_<ENV>.txt
+#   events                   bench.py --events device vs system (timing-event
+#                            release scope) on C2 at K = 20 / 200 and B = 8192,
+#                            alternating 3 times                -> events.txt
 #   stamps                   s_memtime phase stamps of the C2 kernel and the
 #                            tube IPM (make STAMPS=1 build first)
 #   ubench                   tools/ubench microbenchmarks (built in-tree)
@@ -110,6 +113,30 @@ case "$mode" in
         kline gpurun_out/ab/${env}_${v}_$rep.json ${env}=${v}_$rep
       done
     done | tee -a gpurun_out/ab_$env.txt
+    ;;
+  events)
+    mkdir -p gpurun_out/ev
+    for rep in 1 2 3; do
+      for ev in system device; do
+        for cfg in "k20:--steps 20 --warmup 5" "k200:--steps 200 --warmup 20" "b8192:--batch 8192 --steps 20 --warmup 5"; do
+          tag=${cfg%%:*}; a=${cfg#*:}
+          B --no-cpu-baseline --events $ev $a > gpurun_out/ev/${tag}_${ev}_$rep.json 2> gpurun_out/ev/${tag}_${ev}_$rep.err
+          kline gpurun_out/ev/${tag}_${ev}_$rep.json ${tag}_${ev}_$rep
+        done
+      done
+    done | tee gpurun_out/events.txt
+    ;;
+  envs)  # HIP runtime switches on the C2 line at K = 20 (one run each, twice)
+    mkdir -p gpurun_out/envs
+    for rep in 1 2; do
+      for e in NONE=1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 \
+               HIP_FORCE_DEV_KERNARG=0 HIP_FORCE_DEV_KERNARG=1 DEBUG_CLR_KERNARG_HDP_FLUSH_WA=0 \
+               DEBUG_HIP_KERNARG_COPY_OPT=0 DEBUG_HIP_KERNARG_COPY_OPT=1 ROC_USE_FGS_KERNARG=0; do
+        env $e timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --warmup 5 \
+          > gpurun_out/envs/${e}_$rep.json 2> gpurun_out/envs/${e}_$rep.err || { echo "$e failed"; exit 1; }
+        kline gpurun_out/envs/${e}_$rep.json ${e}_$rep
+      done
+    done | tee gpurun_out/envs.txt
     ;;
   stamps)
     STAMPS_SYM=wave MTG_LIB_PATH=mav_tube_trajectory_generation_amd/libmtg_hip_stamps.so \

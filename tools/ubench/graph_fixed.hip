@@ -3,7 +3,10 @@
 // captured in one graph, timed by events around hipGraphLaunch, for K = 20
 // and 200, with and without hipGraphUpload before the timed launch, and with
 // a 50 us busy kernel queued just before the start event (so the graph's
-// submission overlaps it).
+// submission overlaps it); round 5: with the timing events created with
+// hipEventDisableSystemFence / hipEventReleaseToDevice (no system-scope
+// cache writeback and invalidation when an event is recorded), and the K
+// launches eager (not captured) behind the busy kernel.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench/graph_fixed tools/ubench/graph_fixed.hip
 #include <hip/hip_runtime.h>
 
@@ -37,7 +40,7 @@ int main() {
   hipStream_t st;
   CHECK(hipStreamCreate(&st));
   for (int K : {20, 200}) {
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 6; ++mode) {
       hipGraph_t g;
       hipGraphExec_t ge;
       CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
@@ -46,15 +49,23 @@ int main() {
       CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
       if (mode == 1) CHECK(hipGraphUpload(ge, st));
       hipEvent_t e0, e1;
-      CHECK(hipEventCreate(&e0));
-      CHECK(hipEventCreate(&e1));
+      const unsigned ef = mode == 3 ? hipEventDisableSystemFence
+                          : mode == 4 ? hipEventReleaseToDevice : hipEventDefault;
+      CHECK(hipEventCreateWithFlags(&e0, ef));
+      CHECK(hipEventCreateWithFlags(&e1, ef));
       for (int w = 0; w < 3; ++w) CHECK(hipGraphLaunch(ge, st));
       CHECK(hipStreamSynchronize(st));
       float best = 1e9f, sum = 0.0f;
       for (int r = 0; r < 10; ++r) {
-        if (mode == 2) hipLaunchKernelGGL(busy_kernel, dim3(1), dim3(64), 0, st, 50LL * 2400);
+        if (mode == 2 || mode == 5)
+          hipLaunchKernelGGL(busy_kernel, dim3(1), dim3(64), 0, st, (mode == 5 ? 400LL : 50LL) * 2400);
         CHECK(hipEventRecord(e0, st));
-        CHECK(hipGraphLaunch(ge, st));
+        if (mode == 5) {
+          for (int k = 0; k < K; ++k)
+            hipLaunchKernelGGL(work_kernel, dim3(1024), dim3(64), 0, st, out);
+        } else {
+          CHECK(hipGraphLaunch(ge, st));
+        }
         CHECK(hipEventRecord(e1, st));
         CHECK(hipEventSynchronize(e1));
         float ms = 0;
@@ -63,7 +74,13 @@ int main() {
         sum += ms;
       }
       std::printf("K=%3d mode=%s: best %.3f us/launch, mean %.3f us/launch\n", K,
-                  mode == 0 ? "plain " : (mode == 1 ? "upload" : "busy  "), 1000.0 * best / K,
+                  mode == 0   ? "plain "
+                  : mode == 1 ? "upload"
+                  : mode == 2 ? "busy  "
+                  : mode == 3 ? "nofence"
+                  : mode == 4 ? "reldev"
+                              : "eager ",
+                  1000.0 * best / K,
                   1000.0 * sum / 10 / K);
       CHECK(hipGraphExecDestroy(ge));
       CHECK(hipGraphDestroy(g));
