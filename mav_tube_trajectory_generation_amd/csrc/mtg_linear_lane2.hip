@@ -133,7 +133,10 @@ struct Half {
 
   double T[S], x0[M], xS[M], pos[S + 1];
   double Lf[NSTc][NL > 0 ? NL : 1], If[NSTc][MF], z[NSTc][MF];
-  double Zp[MF][MF], Gp[MF][MF], zp[MF];
+  // The last step's Y = L^-1 G, D^-1 Y, its coupling G and z = S^-1 r: the
+  // next step's (or the middle's) Schur terms are G^T S^-1 G = Y^T D^-1 Y
+  // and G^T z.
+  double Yp[MF][MF], DYp[MF][MF], Gp[MF][MF], zp[MF];
   double pmin;
   bool bad;
 
@@ -234,27 +237,31 @@ struct Half {
 
   // Elimination over the half.  Kept per step: the LDL^T factors of the
   // Schur complement and z = S^-1 r; the coupling is recomputed in the back
-  // pass.  Leaves the last step's Z = S^-1 G, G and z for the middle.
+  // pass.  Leaves the last step's Y = L^-1 G, D^-1 Y, G and z for the middle.
+  // Consecutive steps share a segment (forward: step k's right segment is
+  // step k+1's left one; backward the reverse), so its powers are formed
+  // once.
   __device__ void eliminate() {
     pmin = 1.0;
+    Pw<N, R> Ps;  // the shared segment's powers from the previous step
 #pragma unroll
     for (int k = 0; k < NST; ++k) {
       const int v = vert(k);
       Pw<N, R> Pl, Pr;
-      Pl.set(T[v - 1]);
-      Pr.set(T[v]);
+      if (k == 0 || BW) Pl.set(T[v - 1]); else Pl = Ps;
+      if (k == 0 || !BW) Pr.set(T[v]); else Pr = Ps;
       double A[MF][MF], rr[MF], G[MF][MF];
       assemble(Pl, Pr, v, !BW && k == 0, BW && k == 0, A, rr);
       coupling(BW ? Pl : Pr, G);
       if (k > 0) {
-        // S_v = A_v - Gp^T Zp;  r_v = b_v - Gp^T z_prev
+        // S_v = A_v - Y^T D^-1 Y;  r_v = b_v - Gp^T z_prev
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
 #pragma unroll
           for (int j = 0; j <= i; ++j) {
             double s = A[i][j];
 #pragma unroll
-            for (int m = 0; m < MF; ++m) s = fma(-Gp[m][i], Zp[m][j], s);
+            for (int m = 0; m < MF; ++m) s = fma(-Yp[m][i], DYp[m][j], s);
             A[i][j] = s;
           }
           double s = rr[i];
@@ -263,6 +270,7 @@ struct Half {
           rr[i] = s;
         }
       }
+      Ps = BW ? Pl : Pr;
       double l[MF][MF];
       ldlt<MF>(A, l, If[k], pmin);
       {
@@ -273,14 +281,17 @@ struct Half {
           for (int j = 0; j < i; ++j) Lf[k][q++] = l[i][j];
       }
       ldlt_apply<MF>(l, If[k], rr, z[k]);
+      // Y = L^-1 G (unit lower triangular), D^-1 Y
 #pragma unroll
       for (int c = 0; c < MF; ++c) {
-        double col[MF], xc[MF];
 #pragma unroll
-        for (int i = 0; i < MF; ++i) col[i] = G[i][c];
-        ldlt_apply<MF>(l, If[k], col, xc);
+        for (int i = 0; i < MF; ++i) {
+          double s = G[i][c];
 #pragma unroll
-        for (int i = 0; i < MF; ++i) Zp[i][c] = xc[i];
+          for (int m = 0; m < i; ++m) s = fma(-l[i][m], Yp[m][c], s);
+          Yp[i][c] = s;
+          DYp[i][c] = s * If[k][i];
+        }
       }
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
@@ -291,8 +302,8 @@ struct Half {
     }
   }
 
-  // This half's Schur terms at the middle vertex: Gp^T Zp (lower
-  // triangle, row-major) and Gp^T z.
+  // This half's Schur terms at the middle vertex: Y^T D^-1 Y = Gp^T S^-1 Gp
+  // (lower triangle, row-major) and Gp^T z.
   __device__ void terms(double (&tm)[NT], double (&rm)[MF]) const {
     int q = 0;
 #pragma unroll
@@ -301,7 +312,7 @@ struct Half {
       for (int j = 0; j <= i; ++j) {
         double s = 0.0;
 #pragma unroll
-        for (int m = 0; m < MF; ++m) s = fma(Gp[m][i], Zp[m][j], s);
+        for (int m = 0; m < MF; ++m) s = fma(Yp[m][i], DYp[m][j], s);
         tm[q++] = NST > 0 ? s : 0.0;
       }
       double s = 0.0;
