@@ -576,6 +576,9 @@ struct Tube {
     const int m = mid(), nb = nv - 1 - m;
     const bool bw = wv == 1;  // wave-uniform
     for (int st = 0; st <= m; ++st) {
+      // The middle step reads wave 1's last V and L^-1 block: the one
+      // barrier of the sweep (workgroup-uniform condition).
+      if (st == m) __syncthreads();
       // This wave's block: wave 0 a = st (the middle at st = m), wave 1
       // a = nv - 1 - st while st < nb.
       const bool act = bw ? st < nb : true;
@@ -702,7 +705,10 @@ struct Tube {
       // V_a (replacing the previous block's, which every lane of the wave has
       // read by the barrier).  Offsets are selected per lane with integer
       // masks (no branches), unused stores go to a per-lane dummy slot.
-      __syncthreads();
+      // No barrier: a wave's blocks are its own until the middle step (its
+      // W / V reads of this step are issued before these stores, and LDS
+      // operations of a wave complete in issue order).
+      asm volatile("" ::: "memory");
       if (act) {
         const int li = L->Li + a * kTri;
         const int wo = bw ? L->Wb : L->W;
@@ -716,7 +722,7 @@ struct Tube {
           sm[o] = col[i];
         }
       }
-      __syncthreads();
+      asm volatile("" ::: "memory");
       MTG_TACC(224, tf);
     }
     if (bad && lane == 0) *fail = 1;
