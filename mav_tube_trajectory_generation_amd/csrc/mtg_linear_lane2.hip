@@ -112,6 +112,29 @@ __device__ inline void ldlt_apply(const double (&l)[MF][MF], const double (&inv)
   }
 }
 
+// ldlt_apply that also returns w = D^-1 L^-1 r (the back substitution's
+// start), with which G^T S^-1 r = (L^-1 G)^T w.
+template <int MF>
+__device__ inline void ldlt_apply_w(const double (&l)[MF][MF], const double (&inv)[MF],
+                                    const double (&r)[MF], double (&x)[MF], double (&w)[MF]) {
+  double y[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    double s = r[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s = fma(-l[i][k], y[k], s);
+    y[i] = s;
+    w[i] = s * inv[i];
+  }
+#pragma unroll
+  for (int i = MF - 1; i >= 0; --i) {
+    double s = w[i];
+#pragma unroll
+    for (int k = i + 1; k < MF; ++k) s = fma(-l[k][i], x[k], s);
+    x[i] = s;
+  }
+}
+
 // One half of the twisted elimination for one (trajectory, dimension):
 // BW = false eliminates forward over v = 1 .. MID-1 (step k: v = 1 + k),
 // BW = true backward over v = S-1 .. MID+1 (step k: v = S - 1 - k).  The
@@ -133,10 +156,10 @@ struct Half {
 
   double T[S], x0[M], xS[M], pos[S + 1];
   double Lf[NSTc][NL > 0 ? NL : 1], If[NSTc][MF], z[NSTc][MF];
-  // The last step's Y = L^-1 G, D^-1 Y, its coupling G and z = S^-1 r: the
-  // next step's (or the middle's) Schur terms are G^T S^-1 G = Y^T D^-1 Y
-  // and G^T z.
-  double Yp[MF][MF], DYp[MF][MF], Gp[MF][MF], zp[MF];
+  // The last step's Y = L^-1 G, D^-1 Y and w = D^-1 L^-1 r: the next
+  // step's (or the middle's) Schur terms are G^T S^-1 G = Y^T D^-1 Y and
+  // G^T S^-1 r = Y^T w.
+  double Yp[MF][MF], DYp[MF][MF], wp[MF];
   double pmin;
   bool bad;
 
@@ -237,7 +260,7 @@ struct Half {
 
   // Elimination over the half.  Kept per step: the LDL^T factors of the
   // Schur complement and z = S^-1 r; the coupling is recomputed in the back
-  // pass.  Leaves the last step's Y = L^-1 G, D^-1 Y, G and z for the middle.
+  // pass.  Leaves the last step's Y = L^-1 G, D^-1 Y and w for the middle.
   // Consecutive steps share a segment (forward: step k's right segment is
   // step k+1's left one; backward the reverse), so its powers are formed
   // once.
@@ -254,7 +277,7 @@ struct Half {
       assemble(Pl, Pr, v, !BW && k == 0, BW && k == 0, A, rr);
       coupling(BW ? Pl : Pr, G);
       if (k > 0) {
-        // S_v = A_v - Y^T D^-1 Y;  r_v = b_v - Gp^T z_prev
+        // S_v = A_v - Y^T D^-1 Y;  r_v = b_v - Y^T w
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
 #pragma unroll
@@ -266,7 +289,7 @@ struct Half {
           }
           double s = rr[i];
 #pragma unroll
-          for (int m = 0; m < MF; ++m) s = fma(-Gp[m][i], zp[m], s);
+          for (int m = 0; m < MF; ++m) s = fma(-Yp[m][i], wp[m], s);
           rr[i] = s;
         }
       }
@@ -280,7 +303,7 @@ struct Half {
 #pragma unroll
           for (int j = 0; j < i; ++j) Lf[k][q++] = l[i][j];
       }
-      ldlt_apply<MF>(l, If[k], rr, z[k]);
+      ldlt_apply_w<MF>(l, If[k], rr, z[k], wp);
       // Y = L^-1 G (unit lower triangular), D^-1 Y
 #pragma unroll
       for (int c = 0; c < MF; ++c) {
@@ -293,17 +316,11 @@ struct Half {
           DYp[i][c] = s * If[k][i];
         }
       }
-#pragma unroll
-      for (int i = 0; i < MF; ++i) {
-        zp[i] = z[k][i];
-#pragma unroll
-        for (int j = 0; j < MF; ++j) Gp[i][j] = G[i][j];
-      }
     }
   }
 
-  // This half's Schur terms at the middle vertex: Y^T D^-1 Y = Gp^T S^-1 Gp
-  // (lower triangle, row-major) and Gp^T z.
+  // This half's Schur terms at the middle vertex: Y^T D^-1 Y = G^T S^-1 G
+  // (lower triangle, row-major) and Y^T w = G^T z.
   __device__ void terms(double (&tm)[NT], double (&rm)[MF]) const {
     int q = 0;
 #pragma unroll
@@ -317,7 +334,7 @@ struct Half {
       }
       double s = 0.0;
 #pragma unroll
-      for (int m = 0; m < MF; ++m) s = fma(Gp[m][i], zp[m], s);
+      for (int m = 0; m < MF; ++m) s = fma(Yp[m][i], wp[m], s);
       rm[i] = NST > 0 ? s : 0.0;
     }
   }
@@ -382,21 +399,28 @@ struct Half {
         // The step's coupling lives on segment s as well: forward C_v with
         // v = s + 1 - 1 ... = the far vertex's right segment (s), backward
         // C_(v-1)^T with v - 1 = s.
-        double G[MF][MF];
-        coupling(P, G);
+        // G x_near with G[i][m] = K[i][m] T^(ex(i+1, m+1)) split as
+        // T^(1-2r+i+1) sum_m K[i][m] (T^(m+1) x_m): the constant K as
+        // literals, 8 multiplications instead of coupling()'s 16.
+        constexpr HTab<N, R> kH{};
         double l[MF][MF];
         int q = 0;
 #pragma unroll
         for (int i = 1; i < MF; ++i)
 #pragma unroll
           for (int jj = 0; jj < i; ++jj) l[i][jj] = Lf[k >= 0 ? k : 0][q++];
-        double gx[MF], w[MF];
+        double gx[MF], w[MF], u[MF];
+#pragma unroll
+        for (int m = 0; m < MF; ++m) u[m] = xn[m] * P[m + 1];
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
           double t = 0.0;
 #pragma unroll
-          for (int m = 0; m < MF; ++m) t = fma(G[i][m], xn[m], t);
-          gx[i] = t;
+          for (int m = 0; m < MF; ++m) {
+            const double kim = BW ? kH.v[(m + 1) * N + M + i + 1] : kH.v[(i + 1) * N + M + m + 1];
+            t = fma(kim, u[m], t);
+          }
+          gx[i] = t * P[1 - 2 * R + i + 1];
         }
         ldlt_apply<MF>(l, If[k >= 0 ? k : 0], gx, w);
 #pragma unroll
