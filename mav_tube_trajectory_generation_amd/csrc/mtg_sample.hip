@@ -21,6 +21,7 @@ namespace mtg {
 constexpr int kSampleBlock = 256;
 constexpr int kSamplesPerLane = 4;  // amortises the per-workgroup staging
 constexpr int kScaledMax = 4096;    // doubles of pre-scaled coefficients in LDS
+typedef double v2d __attribute__((ext_vector_type(2)));  // 16-byte non-temporal stores
 
 // base(n, i) = i! / (i-n)! (polynomial.cpp:145-161), i >= n.
 __device__ inline double falling_f(int n, int i) {
@@ -93,6 +94,73 @@ __global__ __launch_bounds__(kSampleBlock) void sample_kernel(
   const int nch = (max_deriv + 1) * D;
   const int64_t out0 = b * static_cast<int64_t>(nch) * n_max;
   int nvalid = 0;
+  // Sample k's segment and time in it by the reference's rule (the valid
+  // samples form a prefix of 0 .. n_max-1).
+  auto locate = [&](int k, int* seg_o, double* tin_o, double* acc_o) {
+    bool valid = false;
+    int seg = 0;
+    double tin = 0.0, acc = 0.0;
+    if (i0 >= 0 && k < n_max) {
+      acc = seg0_s[0] + static_cast<double>(k) * dt;
+      tin = seg0_s[1] + static_cast<double>(k) * dt;
+      seg = i0;
+      while (seg < S && tin > T_s[seg]) {
+        tin -= T_s[seg];
+        ++seg;
+      }
+      valid = acc < t_end && seg < S;
+    }
+    *seg_o = seg;
+    *tin_o = tin;
+    *acc_o = acc;
+    return valid;
+  };
+  if (scaled && (n_max & 1) == 0) {
+    // Two consecutive samples per lane and 16-byte stores: each store
+    // instruction writes 1 KB contiguous (round 5; the 8-byte stores below
+    // write 512 B).  Rows start at even sample offsets (n_max even).
+    for (int rep = 0; rep < kSamplesPerLane / 2; ++rep) {
+      const int k = blockIdx.x * kSamplesPerLane * kSampleBlock + rep * 2 * kSampleBlock + 2 * tid;
+      int sg0, sg1;
+      double tn0, tn1, ac0, ac1;
+      const bool v0 = locate(k, &sg0, &tn0, &ac0);
+      const bool v1 = locate(k + 1, &sg1, &tn1, &ac1);
+      if (v0) {
+        const double* cs0 = cs_s + sg0 * nK * D * N;
+        const double* cs1 = cs_s + (v1 ? sg1 : sg0) * nK * D * N;
+        double* out = samples + out0 + k;
+#pragma unroll
+        for (int dv = 0; dv < N; ++dv) {
+          if (dv >= nK) break;
+#pragma unroll
+          for (int d = 0; d < kMaxD; ++d) {
+            if (d >= D) break;
+            const double* c0 = cs0 + (dv * D + d) * N;
+            const double* c1 = cs1 + (dv * D + d) * N;
+            double a = c0[N - 1], c = c1[N - 1];
+#pragma unroll
+            for (int j = N - 2; j >= dv; --j) {
+              a = fma(a, tn0, c0[j]);
+              c = fma(c, tn1, c1[j]);
+            }
+            double* o = out + static_cast<int64_t>(dv * D + d) * n_max;
+            if (v1)  // streamed once: non-temporal stores
+              __builtin_nontemporal_store(v2d{a, c}, reinterpret_cast<v2d*>(o));
+            else
+              __builtin_nontemporal_store(a, o);
+          }
+        }
+        if (sample_times) {
+          double* o = sample_times + b * static_cast<int64_t>(n_max) + k;
+          if (v1)
+            __builtin_nontemporal_store(v2d{ac0, ac1}, reinterpret_cast<v2d*>(o));
+          else
+            __builtin_nontemporal_store(ac0, o);
+        }
+      }
+      nvalid += (v0 ? 1 : 0) + (v1 ? 1 : 0);
+    }
+  } else
   for (int rep = 0; rep < kSamplesPerLane; ++rep) {
     const int k = (blockIdx.x * kSamplesPerLane + rep) * kSampleBlock + tid;
     // Sample k exists iff acc0 + k dt < t_end and its segment stays below S
