@@ -100,3 +100,22 @@ def test_sampling_rejects_bad_arguments(ctx, dev):
         mtg.sample_trajectories(c, t, 0.0)
     with pytest.raises(MTGError):
         mtg.sample_trajectories(c, t, 0.1, max_derivative=10)
+
+
+@pytest.mark.parametrize("n_max", [1001, 1000, 64])
+def test_sampling_row_lengths(ctx, dev, oracle, n_max):
+    """An odd n_max takes the 8-byte store path, an even one the paired
+    16-byte path; both give the padded run's values, times and counts (a
+    row shorter than the trajectory ends the count at n_max)."""
+    import mav_tube_trajectory_generation_amd as mtg
+    N, D, S = 10, 3, 10
+    cd, td, _, _ = _solve(ctx, dev, oracle, N, D, S, [211, 212, 213])
+    ref_s, ref_t, ref_c = mtg.sample_trajectories(cd, td, 0.01, max_derivative=3)
+    smp, st, cnt = mtg.sample_trajectories(cd, td, 0.01, max_derivative=3, n_max=n_max)
+    torch.cuda.synchronize()
+    ref_c, cnt = ref_c.cpu().numpy(), cnt.cpu().numpy()
+    assert np.array_equal(cnt, np.minimum(ref_c, n_max))
+    for b in range(3):
+        n = int(cnt[b])
+        assert torch.equal(smp[b, :, :n], ref_s[b, :, :n])
+        assert torch.equal(st[b, :n], ref_t[b, :n])
