@@ -18,6 +18,8 @@
 #   ab <ENV> <args>          A/B of an environment switch of the library
 #                            (e.g. MTG_WAVE2, MTG_STD_RUNTIME_S) on one bench
 #                            line, alternating 3 times         -> ab_<ENV>.txt
+#   envs                     HIP runtime switches (kernel arguments, graph
+#                            packets) on the C2 line at K = 20  -> envs.txt
 #   events                   bench.py --events device vs system (timing-event
 #                            release scope) on C2 at K = 20 / 200 and B = 8192,
 #                            alternating 3 times                -> events.txt
