@@ -131,9 +131,9 @@ case "$mode" in
   envs)  # HIP runtime switches on the C2 line at K = 20 (one run each, twice)
     mkdir -p gpurun_out/envs
     for rep in 1 2; do
-      for e in NONE=1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 \
+      for e in ${MTG_ENVS:-NONE=1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 \
                HIP_FORCE_DEV_KERNARG=0 HIP_FORCE_DEV_KERNARG=1 DEBUG_CLR_KERNARG_HDP_FLUSH_WA=0 \
-               DEBUG_HIP_KERNARG_COPY_OPT=0 DEBUG_HIP_KERNARG_COPY_OPT=1 ROC_USE_FGS_KERNARG=0; do
+               DEBUG_HIP_KERNARG_COPY_OPT=0 DEBUG_HIP_KERNARG_COPY_OPT=1 ROC_USE_FGS_KERNARG=0}; do
         env $e timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --warmup 5 \
           > gpurun_out/envs/${e}_$rep.json 2> gpurun_out/envs/${e}_$rep.err || { echo "$e failed"; exit 1; }
         kline gpurun_out/envs/${e}_$rep.json ${e}_$rep
