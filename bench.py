@@ -209,9 +209,12 @@ def cpu_baseline(wl, N, D, r, S, seconds, reps, sample_args=None, optimizer="fd"
                       "(orc_time_optimize_sbplx)") if optimizer == "sbplx" else
                      (1, 50, 0.0, None, "50-evaluation time optimisations (orc_time_optimize)")),
             "tube": (2, 0, 0.0, radii, "tube QCQP solves (oracle primal-dual IPM, tol 1e-10)"),
-            "time-qcqp": (5, 0, 0.0, radii,
-                          "time-objective evaluations with the QCQP inner solve and the central-"
-                          "difference gradient (2S+1 oracle IPM solves each)"),
+            "time-qcqp": ((7, 50, 0.0, radii, "50-evaluation LN_SBPLX time optimisations "
+                           "with the QCQP inner solve (orc_tube_time_optimize_sbplx)")
+                          if optimizer == "sbplx" else
+                          (5, 0, 0.0, radii,
+                           "time-objective evaluations with the QCQP inner solve and the "
+                           "central-difference gradient (2S+1 oracle IPM solves each)")),
             "extrema": (4, 0, 0.0, None, "soft-constraint evaluations (two "
                         "computeMaximumOfMagnitude searches, companion-matrix roots)"),
         }.get(wl, (3, None, None, None, None))
@@ -453,6 +456,8 @@ def config_name(wl, B, world, S, global_batch=None):
         return "C3: 4096 x 10-segment tube QCQP"
     if wl == "time" and S == 10 and B == 4096 and world == 1:
         return "C5: 4096 x 50-evaluation time allocation"
+    if wl == "time-qcqp" and S == 10 and B == 4096 and world == 1:
+        return "C5 (QCQP inner solve): 4096 x 50-evaluation time allocation"
     if wl == "collision":
         return f"demo: {B} x main.cpp's 4-segment collision objective per GPU"
     return f"{wl}: {B} x {S}-segment per GPU"
@@ -595,7 +600,8 @@ def main():
         global_batch = 65536
         B = shard_range(global_batch, world, rank)[1]
     else:
-        B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096, "time-qcqp": 1024,
+        B = args.batch or {"linear": 1024, "time": 4096, "tube": 4096,
+                           "time-qcqp": 4096 if args.optimizer == "sbplx" else 1024,
                            "sample": 1024, "extrema": 1024, "collision": 4096}[wl]
         global_batch = B * world
     seed0 = 105 + shard_range(global_batch, world, rank)[0]  # contiguous shard
@@ -813,6 +819,39 @@ def main():
             flop_note = (f"SURVEY 8(d) C3: {f_iter:.0f} FLOP/iteration x {iters} IPM iterations "
                          f"per launch (measured, {iters / B:.1f} per problem); status "
                          f"histogram {hist}")
+        elif args.optimizer == "sbplx":
+            # Config 5 in the reference's own kOptimizeTime path: LN_SBPLX
+            # (the default algorithm) over objectiveFunctionTime with
+            # solveQCQP() at every evaluation (nonlinear_impl:332-397,
+            # 877-945), 50 evaluations per trajectory.  One step = the whole
+            # optimisation: 50 rounds of one batched tube launch each plus the
+            # machine step (mtg_tube_time_optimize_ex, optimizer 1).
+            from mav_tube_trajectory_generation_amd._abi import make_time_params
+            E = 50
+            tparams = make_time_params(500.0, 0.1, 0.1, 1.0, 2, None, 100.0, optimizer="sbplx")
+            ws = torch.empty(mtg.tube_time_workspace_bytes(N, S, B, tparams, True),
+                             dtype=torch.uint8, device=dev)
+
+            def step():
+                return mtg.tube_time_optimize(ctx, N, r, pos_d, tfix, radii, times_d,
+                                              max_evals=E, optimizer="sbplx", workspace=ws)
+
+            res = step()
+            torch.cuda.synchronize(dev)
+            ev = res["evals"].cpu().numpy()
+            rh = {int(k): int(v) for k, v in zip(*np.unique(res["result"].cpu().numpy(),
+                                                             return_counts=True))}
+            # inputs once + times, cost, evals, result, status out
+            bytes_per_traj = (((S + 1) * 3 + 3 * N + 2 * S + S) * 8 + (S + 1) * 8 + 3 * 4)
+            metric = ("LN_SBPLX time optimisations/sec with the QCQP inner solve "
+                      f"({B} x 10-seg, N=10, 3D, {E} evaluations)")
+            flops_per_step = f_iter * (iters / B) * float(ev.sum())
+            flop_note = (f"approximate: {f_iter:.0f} FLOP/iteration x {iters / B:.1f} IPM "
+                         f"iterations per solve (the T0 probe) x {int(ev.sum())} evaluations "
+                         "per step (one QCQP each); kernel_ms is the whole step (50 tube "
+                         "launches + the machine steps)")
+            extra_cfg = {"optimizer": "sbplx", "max_evals": E, "mean_evals": float(ev.mean()),
+                         "results": rh}
         else:
             # config 5's callback in the fork's form (solveQCQP inside
             # objectiveFunctionTime, nonlinear_impl:892) with the central-
@@ -971,7 +1010,8 @@ def main():
     alg_bytes = bytes_per_traj * B
     gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
     config_key = (f"{wl}:B{B}:S{S}" + (":soft" if getattr(args, "soft", False) else "")
-                  + (":sbplx" if wl == "time" and args.optimizer == "sbplx" else ""))
+                  + (":sbplx" if wl in ("time", "time-qcqp") and args.optimizer == "sbplx"
+                     else ""))
     dev_kernel = device_kernel(wl, plan, B, N, D, r, S)
     traffic = load_pmc_traffic(f"{config_key}:{dev_kernel}", kernel_ms)
     timing = (f"HIP events ({args.events}-scope release) around one graph replay of the K "

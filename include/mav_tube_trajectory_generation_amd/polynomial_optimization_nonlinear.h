@@ -812,9 +812,11 @@ class PolynomialOptimizationNonLinear {
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
     double J = 0.0;
     int32_t evals = 0;
-    mtg_time_params tp = timeParams(2);
-    tp.optimizer = 0;  // the QCQP form runs the descent (mtg_tube_time_optimize)
-    const int st = poly_opt_.optimizeTimeQCQP(tp, budget, &times, &J, &evals);
+    // LN_SBPLX (the default algorithm) runs NLopt's Subplex restated on the
+    // device over the QCQP objective; any other algorithm the descent
+    const mtg_time_params tp = timeParams(2);
+    int32_t res = 0;
+    const int st = poly_opt_.optimizeTimeQCQP(tp, budget, &times, &J, &evals, 1e-10, 100, &res);
     poly_opt_.updateSegmentTimes(times);
     poly_opt_.solveQCQP();
     qcqp_time_optimized_ = true;
@@ -828,7 +830,7 @@ class PolynomialOptimizationNonLinear {
                       : J - optimization_info_.cost_trajectory - optimization_info_.cost_time;
     for (const auto& c : soft_)
       optimization_info_.maxima[c.first] = poly_opt_.computeMaximumOfMagnitude(c.first, nullptr);
-    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? res : -1;  // nlopt_result
     optimization_info_.optimization_time =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return optimization_info_.stopping_reason;

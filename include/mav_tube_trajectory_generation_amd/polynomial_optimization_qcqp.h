@@ -195,16 +195,18 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
     return J;
   }
 
-  // optimizeTime over that objective (mtg_tube_time_optimize): `times` in =
-  // the setup times (also the control-point times), out = optimised.
+  // optimizeTime over that objective (mtg_tube_time_optimize_ex): `times`
+  // in = the setup times (also the control-point times), out = optimised
+  // (NLopt's x with params.optimizer 1, LN_SBPLX).  *result (nullable): the
+  // nlopt_result code.  Returns the trajectory status (MTG_TRAJ_*).
   int optimizeTimeQCQP(const mtg_time_params& params, int max_evals, std::vector<double>* times,
-                       double* cost, int32_t* evals, double tol = 1e-10,
-                       int max_iter = 100) const {
+                       double* cost, int32_t* evals, double tol = 1e-10, int max_iter = 100,
+                       int32_t* result = nullptr) const {
     MTG_CHECK(times != nullptr && times->size() == this->n_segments_, "times size");
     std::vector<double> pos, df, radii;
     packTubeInputs(&pos, &df, &radii);
     internal::DeviceBuffer<double> d_pos, d_df, d_t, d_r, d_cost(1);
-    internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
+    internal::DeviceBuffer<int32_t> d_ev(1), d_res(1), d_st(1);
     internal::DeviceBuffer<unsigned char> d_ws(
         workspaceBytes(static_cast<int>(this->n_segments_), params, 1));
     d_pos.upload(pos);
@@ -212,16 +214,17 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
     d_t.upload(*times);
     d_r.upload(radii);
     internal::checkStatus(
-        mtg_tube_time_optimize(internal::defaultContext(), N, this->derivative_to_optimize_,
-                               static_cast<int>(this->n_segments_), 1, d_pos.get(), d_df.get(),
-                               d_r.get(), d_t.get(), tol, max_iter, &params, max_evals,
-                               d_cost.get(), d_ev.get(), d_st.get(), d_ws.get(), d_ws.size(),
-                               nullptr),
-        "mtg_tube_time_optimize");
+        mtg_tube_time_optimize_ex(internal::defaultContext(), N, this->derivative_to_optimize_,
+                                  static_cast<int>(this->n_segments_), 1, d_pos.get(),
+                                  d_df.get(), d_r.get(), d_t.get(), tol, max_iter, &params,
+                                  max_evals, d_cost.get(), d_ev.get(), d_res.get(), d_st.get(),
+                                  d_ws.get(), d_ws.size(), nullptr),
+        "mtg_tube_time_optimize_ex");
     internal::synchronize();
     d_t.download(times->data(), times->size());
     if (cost) d_cost.download(cost, 1);
     if (evals) d_ev.download(evals, 1);
+    if (result) d_res.download(result, 1);
     int32_t st = 0;
     d_st.download(&st, 1);
     return st;

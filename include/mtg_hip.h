@@ -144,8 +144,14 @@ int mtg_linear_solve(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                      const double* times, double* coeffs, double* cost,
                      double* free_vals, int32_t* status, void* stream);
 
-/* Same, host pointers in and out (copies + synchronises).  Used by the C++
- * single-trajectory shim PolynomialOptimization<N>::solveLinear(). */
+/* Same, host pointers in and out.  Used by the C++ single-trajectory shim
+ * PolynomialOptimization<N>::solveLinear().  The plan keeps persistent
+ * staging (pinned host + device buffers and a stream of its own, created on
+ * first use, grown when a larger B arrives): a steady-state call is one
+ * host-to-device copy, one launch and one device-to-host copy on that
+ * stream, then a wait on that stream only (no allocation, no device-wide
+ * synchronisation).  Calls on one plan are serialised (the staging is
+ * shared); use separate plans for concurrent host threads. */
 int mtg_linear_solve_host(const mtg_plan* plan, int64_t B,
                           const double* fixed_vals, const double* times,
                           double* coeffs, double* cost, double* free_vals,
@@ -403,22 +409,41 @@ int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* Batched segment-time optimisation over that objective (optimizeTime,
- * nonlinear_impl:332-397, in the fork's QCQP form): the optimiser of
- * mtg_time_optimize (projected, scaled steepest descent with expand /
- * backtrack on the grad_mode 2 gradient, bounds [0.1, 2 T0], max_evals
- * counted evaluations), stopping also at a non-finite gradient.  Each round
- * is one tube launch over B x (2S+1) problems (every trial with its gradient
- * points).  The call enqueues max_evals rounds; a trajectory that has
- * stopped is skipped by every later round on the device (its QCQP
- * workgroups exit at once), so there is no host round trip.
+ * nonlinear_impl:332-397, in the fork's QCQP form), bounds [0.1, 2 T0],
+ * max_evals counted evaluations.  params->optimizer selects the optimiser as
+ * in mtg_time_optimize:
+ *   1  LN_SBPLX, the reference's default (polynomial_optimization_nonlinear.h
+ *      :61): NLopt's Subplex restated on the device (mtg_sbplx_device.h) on
+ *      objectiveFunctionTime with solveQCQP() at every evaluation (:891-892),
+ *      initial steps initial_stepsize_rel T0, ftol f_rel / f_abs.  Each round
+ *      is one tube launch over B problems (one evaluation per trajectory);
+ *      times_io is NLopt's x (the best point) and cost its value (opt_f).  A
+ *      T0 below 0.1 is NLopt's invalid start: result -1 (nlopt::FAILURE, as
+ *      optimizeTime returns it), no evaluation, times unchanged, cost NaN.
+ *   0  the projected, scaled steepest descent of mtg_time_optimize on the
+ *      grad_mode 2 gradient, stopping also at a non-finite gradient; each
+ *      round is one tube launch over B x (2S+1) problems (every trial with
+ *      its gradient points).
+ * The call enqueues max_evals rounds; a trajectory that has stopped is
+ * skipped by every later round on the device (its QCQP workgroups exit at
+ * once), so there is no host round trip.
  *   times_io  B x S  in: T0 (also the control-point times), out: optimised
- *   cost B, evals B, status B (nullable); workspace as above (optimize = 1). */
+ *   cost B, evals B, status B (nullable); workspace as above (optimize = 1,
+ *   with the same params: the LN_SBPLX workspace holds the machine states).
+ * The _ex form adds result (B, nullable): the nlopt_result code as in
+ * mtg_time_optimize_ex. */
 int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
                            const double* positions, const double* fixed_vals,
                            const double* radii, double* times_io, double tol, int max_iter,
                            const mtg_time_params* params, int max_evals, double* cost,
                            int32_t* evals, int32_t* status, void* workspace,
                            size_t workspace_bytes, void* stream);
+int mtg_tube_time_optimize_ex(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                              const double* positions, const double* fixed_vals,
+                              const double* radii, double* times_io, double tol, int max_iter,
+                              const mtg_time_params* params, int max_evals, double* cost,
+                              int32_t* evals, int32_t* result, int32_t* status, void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Batched trajectory sampling: Trajectory::evaluateRange (src/trajectory.cpp:

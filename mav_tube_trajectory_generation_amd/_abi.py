@@ -222,6 +222,11 @@ SIGNATURES = {
                                               ctypes.c_double, ctypes.c_int,
                                               ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
                                               _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "mtg_tube_time_optimize_ex": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp,
+                                                 _vp, ctypes.c_double, ctypes.c_int,
+                                                 ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
+                                                 _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "mtg_select_local": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "mtg_select_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64]),

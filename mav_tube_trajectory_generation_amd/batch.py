@@ -599,28 +599,36 @@ def tube_time_cost(ctx, N, r, positions, fixed_vals, times_cp, times, radii, tim
 
 def tube_time_optimize(ctx, N, r, positions, fixed_vals, radii, times, max_evals,
                        time_penalty=500.0, increment=0.1, soft=None, soft_weight=100.0,
-                       tol=1e-10, max_iter=100, workspace=None):
-    """optimizeTime in the fork's QCQP form (mtg_tube_time_optimize).  times
-    [B, S] are the initial times (and the control-point times); returns
-    dict(times, cost, evals, status) with new tensors."""
+                       tol=1e-10, max_iter=100, workspace=None, optimizer="fd", f_rel=0.05,
+                       f_abs=-1.0, initial_stepsize_rel=0.1):
+    """optimizeTime in the fork's QCQP form (mtg_tube_time_optimize_ex).  times
+    [B, S] are the initial times (and the control-point times).  optimizer
+    "sbplx" runs LN_SBPLX, the reference's default (one QCQP per evaluation,
+    f_rel / f_abs / initial_stepsize_rel as NonlinearOptimizationParameters);
+    "fd" the projected central-difference descent.  Returns dict(times, cost,
+    evals, result, status) with new tensors; result is the nlopt_result code."""
     import torch
     B, S = times.shape
     dev = times.device
     _tube_geometry(N, positions, fixed_vals, radii, B, S)
     _require(times, (B, S), "times")
-    p = make_time_params(time_penalty, increment, 0.1, 1.0, 2, soft, soft_weight)
+    p = make_time_params(time_penalty, increment, 0.1, 1.0, 2, soft, soft_weight,
+                         optimizer=optimizer, f_rel=f_rel, f_abs=f_abs,
+                         initial_stepsize_rel=initial_stepsize_rel)
     t = times.clone()
     cost = torch.empty(B, dtype=torch.float64, device=dev)
     evals = torch.empty(B, dtype=torch.int32, device=dev)
+    result = torch.empty(B, dtype=torch.int32, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
     nbytes = tube_time_workspace_bytes(N, S, B, p, True)
     ws = _workspace(workspace, nbytes, dev)
-    check(lib().mtg_tube_time_optimize(ctx.handle, N, r, S, B, _ptr(positions),
-                                       _ptr(fixed_vals), _ptr(radii), _ptr(t), tol, max_iter,
-                                       ctypes.byref(p), max_evals, _ptr(cost), _ptr(evals),
-                                       _ptr(status), _ptr(ws), ws.numel() * ws.element_size(),
-                                       _stream(dev)), "mtg_tube_time_optimize")
-    return dict(times=t, cost=cost, evals=evals, status=status)
+    check(lib().mtg_tube_time_optimize_ex(ctx.handle, N, r, S, B, _ptr(positions),
+                                          _ptr(fixed_vals), _ptr(radii), _ptr(t), tol, max_iter,
+                                          ctypes.byref(p), max_evals, _ptr(cost), _ptr(evals),
+                                          _ptr(result), _ptr(status), _ptr(ws),
+                                          ws.numel() * ws.element_size(), _stream(dev)),
+          "mtg_tube_time_optimize_ex")
+    return dict(times=t, cost=cost, evals=evals, result=result, status=status)
 
 
 def sample_trajectories(coeffs, times, dt, t_start=0.0, t_end=-1.0, max_derivative=0,

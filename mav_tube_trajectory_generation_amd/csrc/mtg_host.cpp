@@ -21,12 +21,33 @@ struct mtg_ctx {
   std::map<std::pair<int, int>, double*> tables;  // (N, r) -> H(1), A(1)^-1
 };
 
+// Persistent staging of the host-memory entry point (mtg_linear_solve_host),
+// created on first use and grown on demand: a pinned host buffer, the same
+// layout on the device and a non-blocking stream of the plan's own, so a
+// steady-state call is one H2D copy, one launch and one D2H copy on that
+// stream, then a wait on that stream only (no allocation, no device-wide
+// synchronisation).  Layout (bytes, each part 256-aligned): inputs
+// [fixed_vals | times], outputs [coeffs | cost | free_vals | status].
+struct mtg_staging {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  char* host = nullptr;
+  char* dev = nullptr;
+  size_t bytes = 0;
+  ~mtg_staging() {
+    if (stream) (void)hipStreamDestroy(stream);
+    if (host) (void)hipHostFree(host);
+    if (dev) (void)hipFree(dev);
+  }
+};
+
 struct mtg_plan {
   mtg_ctx* ctx = nullptr;
   mtg::PlanDev dev{};
   int* d_slots = nullptr;
   int* d_free_map = nullptr;
   int* d_fixed_map = nullptr;
+  std::unique_ptr<mtg_staging> stage{new mtg_staging};
 };
 
 namespace {
@@ -337,37 +358,60 @@ int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_v
                           const double* times, double* coeffs, double* cost,
                           double* free_vals, int32_t* status) {
   clear_stale_error();
-  if (!plan || B < 0 || !times || !coeffs) return MTG_ERR_INVALID_ARG;
+  if (!plan || B < 0 || B > 0x7fffffff || !times || !coeffs) return MTG_ERR_INVALID_ARG;
+  if (plan->dev.nf > 0 && !fixed_vals) return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   const PlanDev& pl = plan->dev;
   const size_t nfv = static_cast<size_t>(B) * pl.D * pl.nf;
   const size_t nt = static_cast<size_t>(B) * pl.S;
   const size_t nc = static_cast<size_t>(B) * pl.S * pl.D * pl.N;
   const size_t npv = static_cast<size_t>(B) * pl.D * pl.np;
-  DevBuf<double> dfv, dt, dc, dcost, dfree;
-  DevBuf<int32_t> dst;
-  if (dfv.alloc(nfv) || dt.alloc(nt) || dc.alloc(nc) || dcost.alloc(B) ||
-      dfree.alloc(npv) || dst.alloc(B))
+  auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t o_t = up(nfv * sizeof(double)), o_out = up(o_t + nt * sizeof(double));
+  const size_t o_cost = up(o_out + nc * sizeof(double));
+  const size_t o_free = up(o_cost + B * sizeof(double));
+  const size_t o_st = up(o_free + npv * sizeof(double));
+  const size_t total = up(o_st + B * sizeof(int32_t));
+  mtg_staging& sg = *plan->stage;
+  std::lock_guard<std::mutex> lock(sg.mu);
+  if (!sg.stream) {
+    if (hipSetDevice(plan->ctx->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&sg.stream, hipStreamNonBlocking) != hipSuccess) {
+      sg.stream = nullptr;
+      return MTG_ERR_HIP;
+    }
+  }
+  if (sg.bytes < total) {
+    if (sg.host) (void)hipHostFree(sg.host);
+    if (sg.dev) (void)hipFree(sg.dev);
+    sg.host = sg.dev = nullptr;
+    sg.bytes = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&sg.host), total, hipHostMallocDefault) !=
+            hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&sg.dev), total) != hipSuccess)
+      return MTG_ERR_HIP;
+    sg.bytes = total;
+  }
+  if (nfv) std::memcpy(sg.host, fixed_vals, nfv * sizeof(double));
+  std::memcpy(sg.host + o_t, times, nt * sizeof(double));
+  if (hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, sg.stream) != hipSuccess)
     return MTG_ERR_HIP;
-  if (nfv && hipMemcpy(dfv.p, fixed_vals, nfv * sizeof(double), hipMemcpyHostToDevice))
-    return MTG_ERR_HIP;
-  if (hipMemcpy(dt.p, times, nt * sizeof(double), hipMemcpyHostToDevice)) return MTG_ERR_HIP;
-  int rc = mtg_linear_solve(plan, B, dfv.p, dt.p, dc.p, dcost.p, npv ? dfree.p : nullptr,
-                            dst.p, nullptr);
+  auto d = [&](size_t off) { return reinterpret_cast<double*>(sg.dev + off); };
+  int rc = from_hip(mtg::launch_linear_solve(
+      pl, B, nfv ? d(0) : nullptr, d(o_t), d(o_out), d(o_cost), npv ? d(o_free) : nullptr,
+      reinterpret_cast<int32_t*>(sg.dev + o_st), sg.stream));
   if (rc) return rc;
-  if (hipDeviceSynchronize()) return MTG_ERR_HIP;
-  if (hipMemcpy(coeffs, dc.p, nc * sizeof(double), hipMemcpyDeviceToHost)) return MTG_ERR_HIP;
-  if (cost && hipMemcpy(cost, dcost.p, B * sizeof(double), hipMemcpyDeviceToHost))
+  if (hipMemcpyAsync(sg.host + o_out, sg.dev + o_out, total - o_out, hipMemcpyDeviceToHost,
+                     sg.stream) != hipSuccess ||
+      hipStreamSynchronize(sg.stream) != hipSuccess)
     return MTG_ERR_HIP;
-  if (free_vals && npv &&
-      hipMemcpy(free_vals, dfree.p, npv * sizeof(double), hipMemcpyDeviceToHost))
-    return MTG_ERR_HIP;
-  std::vector<int32_t> st(B);
-  if (hipMemcpy(st.data(), dst.p, B * sizeof(int32_t), hipMemcpyDeviceToHost))
-    return MTG_ERR_HIP;
-  if (status) std::memcpy(status, st.data(), B * sizeof(int32_t));
-  for (int32_t s : st)
-    if (s != MTG_TRAJ_OK) return MTG_ERR_NUMERIC;
+  std::memcpy(coeffs, sg.host + o_out, nc * sizeof(double));
+  if (cost) std::memcpy(cost, sg.host + o_cost, B * sizeof(double));
+  if (free_vals && npv) std::memcpy(free_vals, sg.host + o_free, npv * sizeof(double));
+  const int32_t* st = reinterpret_cast<const int32_t*>(sg.host + o_st);
+  if (status) std::memcpy(status, st, B * sizeof(int32_t));
+  for (int64_t b = 0; b < B; ++b)
+    if (st[b] != MTG_TRAJ_OK) return MTG_ERR_NUMERIC;
   return MTG_OK;
 }
 
@@ -814,10 +858,8 @@ int mtg_time_optimize_ex(const mtg_plan* plan, int64_t B, const double* fixed_va
   if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
   if (!valid_soft(plan, params, true)) return MTG_ERR_INVALID_ARG;
   if (params->optimizer != 0 && params->optimizer != 1) return MTG_ERR_INVALID_ARG;
-  // LN_SBPLX takes no inequality constraints (NLopt rejects them), and its
-  // LDS state holds at most kMaxN segments
-  if (params->optimizer == 1 &&
-      ((params->hard_constraints && params->n_soft > 0) || plan->dev.S > mtg::sbplx::kMaxN))
+  // LN_SBPLX takes no inequality constraints (NLopt rejects them)
+  if (params->optimizer == 1 && params->hard_constraints && params->n_soft > 0)
     return MTG_ERR_INVALID_ARG;
   if (B == 0) return MTG_OK;
   return from_hip(mtg::launch_time_optimize(plan->dev, B, fixed_vals, times_io, *params,
@@ -936,15 +978,15 @@ int mtg_tube_time_cost(mtg_ctx* ctx, int N, int r, int S, int64_t B, const doubl
                              workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
-int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
-                           const double* positions, const double* fixed_vals,
-                           const double* radii, double* times_io, double tol, int max_iter,
-                           const mtg_time_params* params, int max_evals, double* cost,
-                           int32_t* evals, int32_t* status, void* workspace,
-                           size_t workspace_bytes, void* stream) {
+int mtg_tube_time_optimize_ex(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                              const double* positions, const double* fixed_vals,
+                              const double* radii, double* times_io, double tol, int max_iter,
+                              const mtg_time_params* params, int max_evals, double* cost,
+                              int32_t* evals, int32_t* result, int32_t* status, void* workspace,
+                              size_t workspace_bytes, void* stream) {
   clear_stale_error();
-  // the QCQP-inner-solve optimiser is the projected descent only
-  if (params && params->optimizer != 0) return MTG_ERR_UNSUPPORTED;
+  // optimizer 0: the projected descent; 1: LN_SBPLX (the reference's default)
+  if (params && params->optimizer != 0 && params->optimizer != 1) return MTG_ERR_INVALID_ARG;
   mtg::TubeArgs a;
   // times_cp = the initial times (read before the first write of times_io).
   int rc = tube_args(ctx, N, r, S, B, positions, fixed_vals, times_io, times_io, radii, &a);
@@ -955,8 +997,19 @@ int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
   if (B == 0) return MTG_OK;
   if (!workspace) return MTG_ERR_INVALID_ARG;
   return mtg::tube_time_optimize(a, times_io, tol, max_iter, *params, max_evals, cost, evals,
-                                 status, workspace, workspace_bytes,
+                                 result, status, workspace, workspace_bytes,
                                  static_cast<hipStream_t>(stream));
+}
+
+int mtg_tube_time_optimize(mtg_ctx* ctx, int N, int r, int S, int64_t B,
+                           const double* positions, const double* fixed_vals,
+                           const double* radii, double* times_io, double tol, int max_iter,
+                           const mtg_time_params* params, int max_evals, double* cost,
+                           int32_t* evals, int32_t* status, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  return mtg_tube_time_optimize_ex(ctx, N, r, S, B, positions, fixed_vals, radii, times_io, tol,
+                                   max_iter, params, max_evals, cost, evals, nullptr, status,
+                                   workspace, workspace_bytes, stream);
 }
 
 int mtg_generate_random_problems(int N, int D, int S, int64_t B, uint64_t seed0,

@@ -175,7 +175,7 @@ int tube_time_cost(const TubeArgs& a, double tol, int max_iter, const mtg_time_p
                    size_t workspace_bytes, hipStream_t st);
 int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_iter,
                        const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
-                       int32_t* status, void* workspace, size_t workspace_bytes,
+                       int32_t* result, int32_t* status, void* workspace, size_t workspace_bytes,
                        hipStream_t st);
 
 constexpr int kMaxLdsBytes = 160 * 1024;

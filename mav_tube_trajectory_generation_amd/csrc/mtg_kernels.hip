@@ -335,6 +335,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
       mach.init(S, t.T(), p.initial_stepsize_rel > 0.0 ? p.initial_stepsize_rel : 0.1,
                 max_evals, p.f_rel, p.f_abs);
     __syncthreads();
+    if (sbs->done) phase = kDone;  // start outside the bounds (NLopt: FAILURE)
   }
   while (phase != kDone) {
     double viol;
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_kernel(
   fl = t.flag()[0];
   __syncthreads();
   if (sb) {  // NLopt's x and opt_f: the best point and its value
-    for (int i = t.lane; i < S; i += kWave) Tcur[i] = sbs->x[i];
+    for (int i = t.lane; i < S; i += kWave) Tcur[i] = sbplx::best_x(sbs)[i];
     f = sbs->minf;
     evals = sbs->nevals;
     res = sbs->result;
@@ -497,14 +498,16 @@ static hipError_t launch_time_opt_n(const PlanDev& pl, int64_t B, const double* 
                                     hipStream_t st) {
   const Layout lay = make_layout(N, pl.S, pl.D);
   if (p.n_soft > 0) {
-    const size_t bytes = sbplx_state_offset(lay, pl.S, pl.D, N, true) + sbplx::kStateBytes;
+    const size_t bytes =
+        sbplx_state_offset(lay, pl.S, pl.D, N, true) + sbplx::state_bytes(pl.S);
     hipError_t e = prepare_lds(time_optimize_kernel<N, true>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_kernel<N, true>), dim3(static_cast<unsigned>(B)),
                        dim3(kWave), bytes, st, pl, df, times, p, max_evals, cost, evals, solves,
                        result, status);
   } else {
-    const size_t bytes = sbplx_state_offset(lay, pl.S, pl.D, N, false) + sbplx::kStateBytes;
+    const size_t bytes =
+        sbplx_state_offset(lay, pl.S, pl.D, N, false) + sbplx::state_bytes(pl.S);
     hipError_t e = prepare_lds(time_optimize_kernel<N, false>, bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((time_optimize_kernel<N, false>), dim3(static_cast<unsigned>(B)),

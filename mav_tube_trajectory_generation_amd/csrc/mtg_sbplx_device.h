@@ -23,22 +23,36 @@
 namespace mtg {
 namespace sbplx {
 
-constexpr int kMaxN = 16;  // segments (the time kernels' S <= 16)
 constexpr int kNsMin = 2, kNsMax = 5;
 constexpr double kPsi = 0.25, kOmega = 0.1;
 constexpr double kAlpha = 1.0, kBeta = 0.5, kGamma = 2.0, kDelta = 0.5;
 // nlopt_result codes
 constexpr int kFailure = -1, kFtol = 3, kXtol = 4, kMaxEval = 5;
 
+// The fixed part of the state; the n-sized arrays follow it (state_bytes(n)):
+// x, xprev, dx, xstep, lb, ub (n doubles each), then the permutation p (n
+// ints).  The subspace solver's arrays are fixed (ns <= kNsMax).
 struct State {
-  double x[kMaxN], xprev[kMaxN], dx[kMaxN], xstep[kMaxN], lb[kMaxN], ub[kMaxN];
   double pts[kNsMax + 1][kNsMax + 1];  // simplex: value, then the point
   double xs[kNsMax], lbs[kNsMax], ubs[kNsMax], sstep[kNsMax], c[kNsMax], xcur[kNsMax];
   double minf, fdiff, fdiff_max, normi, normdx, init_diam, fr, ftol_rel, ftol_abs;
-  int p[kMaxN];
   int n, maxeval, nevals, pc, result, done, i, is, ns, nsubs, k, lo, hi, last;
 };
-constexpr size_t kStateBytes = (sizeof(State) + 15) / 16 * 16;
+constexpr size_t kHdrBytes = (sizeof(State) + 15) / 16 * 16;
+// Bytes of the state of an n-variable problem (16-byte multiple).
+__host__ __device__ constexpr size_t state_bytes(int n) {
+  return kHdrBytes + ((sizeof(double) * 6 + sizeof(int)) * static_cast<size_t>(n) + 15) / 16 * 16;
+}
+// Array k (0 x, 1 xprev, 2 dx, 3 xstep, 4 lb, 5 ub) of the state.
+__device__ inline double* arr(State* s, int k) {
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(s) + kHdrBytes) + k * s->n;
+}
+__device__ inline const double* arr(const State* s, int k) {
+  return reinterpret_cast<const double*>(reinterpret_cast<const char*>(s) + kHdrBytes) +
+         k * s->n;
+}
+// NLopt's x: the best point (valid once done).
+__device__ inline const double* best_x(const State* s) { return arr(s, 0); }
 
 enum Pc {
   kFirst, kOuter, kSubsel, kNmInit, kNmInitGot, kNmIter, kNmReflGot, kNmExpGot, kNmConGot,
@@ -70,25 +84,65 @@ __device__ inline bool reflect(int n, double* xnew, const double* c, double scal
 struct Machine {
   State* s;
 
+  __device__ double* x() { return arr(s, 0); }
+  __device__ double* xprev() { return arr(s, 1); }
+  __device__ double* dx() { return arr(s, 2); }
+  __device__ double* xstep() { return arr(s, 3); }
+  __device__ double* lb() { return arr(s, 4); }
+  __device__ double* ub() { return arr(s, 5); }
+  __device__ int* p() { return reinterpret_cast<int*>(arr(s, 6)); }
+
   // Start from the times in T (S values): lb 0.1, ub 2 T0, steps
   // step_rel T0 (optimizeTime, nonlinear_impl:343-358, 370-378).
   __device__ void init(int n, const double* T, double step_rel, int maxeval, double ftol_rel,
                        double ftol_abs) {
     s->n = n;
+    for (int i = 0; i < n; ++i) {
+      x()[i] = T[i];
+      lb()[i] = 0.1;  // kOptimizationTimeLowerBound
+      ub()[i] = 2.0 * T[i];
+      xstep()[i] = step_rel * T[i];
+    }
+    start(maxeval, ftol_rel, ftol_abs);
+  }
+  // Start from x0 with bounds [lb, ub] and initial steps (each n values; the
+  // caller's arrays may be the ones the kernel evaluates at).
+  __device__ void init_box(int n, const double* x0, const double* lo, const double* hi,
+                           const double* step, int maxeval, double ftol_rel, double ftol_abs) {
+    s->n = n;
+    for (int i = 0; i < n; ++i) {
+      x()[i] = x0[i];
+      lb()[i] = lo[i];
+      ub()[i] = hi[i];
+      xstep()[i] = step[i];
+    }
+    start(maxeval, ftol_rel, ftol_abs);
+  }
+  // Common tail of init / init_box.  NLopt refuses a start outside its
+  // bounds (or lb > ub) before the first evaluation (nlopt_optimize:
+  // NLOPT_INVALID_ARGS, which nlopt::opt::optimize throws and optimizeTime
+  // turns into nlopt::FAILURE, nonlinear_impl:389-394): the machine is then
+  // done at once with result kFailure, no evaluation, x = x0, minf NaN.  The
+  // caller checks `done` before its first evaluation.
+  __device__ void start(int maxeval, double ftol_rel, double ftol_abs) {
+    const int n = s->n;
     s->maxeval = maxeval;
     s->ftol_rel = ftol_rel;
     s->ftol_abs = ftol_abs;
+    bool ok = true;
     for (int i = 0; i < n; ++i) {
-      s->x[i] = T[i];
-      s->lb[i] = 0.1;  // kOptimizationTimeLowerBound
-      s->ub[i] = 2.0 * T[i];
-      s->xstep[i] = step_rel * T[i];
-      s->dx[i] = 0.0;
+      dx()[i] = 0.0;
+      ok = ok && !(lb()[i] > ub()[i] || x()[i] < lb()[i] || x()[i] > ub()[i]);
     }
     s->nevals = 0;
     s->done = 0;
     s->result = 0;
-    s->pc = kFirst;  // T already holds the first point
+    s->minf = HUGE_VAL;
+    s->pc = kFirst;  // the caller's point array already holds the first point
+    if (!ok) {
+      s->minf = __builtin_nan("");
+      finish(kFailure);
+    }
   }
 
   __device__ double& pf(int i) { return s->pts[i][0]; }
@@ -97,8 +151,8 @@ struct Machine {
   // The full point for the subspace point xsub: x with the subspace
   // coordinates replaced (sbplx's subspace_func).
   __device__ void request(const double* xsub, double* T, int next) {
-    for (int j = 0; j < s->n; ++j) T[j] = s->x[j];
-    for (int k = 0; k < s->ns; ++k) T[s->p[s->is + k]] = xsub[k];
+    for (int j = 0; j < s->n; ++j) T[j] = x()[j];
+    for (int k = 0; k < s->ns; ++k) T[p()[s->is + k]] = xsub[k];
     s->pc = next;
   }
   // NLopt's CHECK_EVAL: count; keep the best subspace point; stop at maxeval.
@@ -123,7 +177,7 @@ struct Machine {
   // Returns true when the machine continues (pc set), false when finished.
   __device__ void nm_return(int code) {
     if (s->fdiff > s->fdiff_max) s->fdiff_max = s->fdiff;
-    for (int k = 0; k < s->ns; ++k) s->x[s->p[s->is + k]] = s->xs[k];
+    for (int k = 0; k < s->ns; ++k) x()[p()[s->is + k]] = s->xs[k];
     if (code == kFailure) return finish(kXtol);
     if (code != kXtol) return finish(code);
     if (!s->last) {
@@ -140,22 +194,22 @@ struct Machine {
         return finish(kFtol);
     }
     const int n = s->n;
-    for (int k = 0; k < n; ++k) s->dx[k] = s->x[k] - s->xprev[k];
+    for (int k = 0; k < n; ++k) dx()[k] = x()[k] - xprev()[k];
     double scale;
     if (s->nsubs == 1) {
       scale = kPsi;
     } else {
       double stepnorm = 0.0, dxnorm = 0.0;
       for (int k = 0; k < n; ++k) {
-        stepnorm += fabs(s->xstep[k]);
-        dxnorm += fabs(s->dx[k]);
+        stepnorm += fabs(xstep()[k]);
+        dxnorm += fabs(dx()[k]);
       }
       scale = dxnorm / stepnorm;
       scale = scale < kOmega ? kOmega : scale;
       scale = scale > 1.0 / kOmega ? 1.0 / kOmega : scale;
     }
     for (int k = 0; k < n; ++k)
-      s->xstep[k] = s->dx[k] == 0.0 ? -(s->xstep[k] * scale) : copysign(s->xstep[k] * scale, s->dx[k]);
+      xstep()[k] = dx()[k] == 0.0 ? -(xstep()[k] * scale) : copysign(xstep()[k] * scale, dx()[k]);
     s->pc = kOuter;
   }
 
@@ -173,22 +227,22 @@ struct Machine {
           break;
         }
         case kOuter: {
-          for (int k = 0; k < n; ++k) s->xprev[k] = s->x[k];
+          for (int k = 0; k < n; ++k) xprev()[k] = x()[k];
           s->fdiff_max = 0.0;
           s->nsubs = 0;
           // stable insertion sort of the indices by decreasing |dx|
           for (int k = 0; k < n; ++k) {
             const int v = k;
-            const double key = fabs(s->dx[v]);
+            const double key = fabs(dx()[v]);
             int j = k;
-            while (j > 0 && fabs(s->dx[s->p[j - 1]]) < key) {
-              s->p[j] = s->p[j - 1];
+            while (j > 0 && fabs(dx()[p()[j - 1]]) < key) {
+              p()[j] = p()[j - 1];
               --j;
             }
-            s->p[j] = v;
+            p()[j] = v;
           }
           double nd = 0.0;
-          for (int k = 0; k < n; ++k) nd += fabs(s->dx[k]);
+          for (int k = 0; k < n; ++k) nd += fabs(dx()[k]);
           s->normdx = nd;
           s->normi = 0.0;
           s->i = 0;
@@ -204,9 +258,9 @@ struct Machine {
             const int nk = i + kNsMax > n ? n : i + kNsMax;
             double best = -HUGE_VAL, norm = s->normi;
             size = kNsMin;
-            for (int k = i; k < i + kNsMin - 1; ++k) norm += fabs(s->dx[s->p[k]]);
+            for (int k = i; k < i + kNsMin - 1; ++k) norm += fabs(dx()[p()[k]]);
             for (int k = i + kNsMin - 1; k < nk; ++k) {
-              norm += fabs(s->dx[s->p[k]]);
+              norm += fabs(dx()[p()[k]]);
               const int rest = n - k - 1;
               if ((rest + kNsMax - 1) / kNsMax > rest / kNsMin) continue;
               const double g = k + 1 < n ? norm / (k + 1) - (s->normdx - norm) / (n - (k + 1))
@@ -216,7 +270,7 @@ struct Machine {
                 size = (k + 1) - i;
               }
             }
-            for (int k = i; k < i + size; ++k) s->normi += fabs(s->dx[s->p[k]]);
+            for (int k = i; k < i + size; ++k) s->normi += fabs(dx()[p()[k]]);
             s->last = 0;
           } else {
             size = n - i;
@@ -226,11 +280,11 @@ struct Machine {
           s->ns = size;
           ++s->nsubs;
           for (int k = 0; k < size; ++k) {
-            const int q = s->p[i + k];
-            s->xs[k] = s->x[q];
-            s->sstep[k] = s->xstep[q];
-            s->lbs[k] = s->lb[q];
-            s->ubs[k] = s->ub[q];
+            const int q = p()[i + k];
+            s->xs[k] = x()[q];
+            s->sstep[k] = xstep()[q];
+            s->lbs[k] = lb()[q];
+            s->ubs[k] = ub()[q];
           }
           // Nelder-Mead from xs, f(xs) = minf
           s->fdiff = HUGE_VAL;

@@ -155,7 +155,7 @@ __host__ __device__ inline size_t time_std_bytes(int N, int S, int D, bool soft)
 size_t time_std_lds_bytes(int N, int S, int D, bool soft) { return time_std_bytes(N, S, D, soft); }
 // The optimiser kernels add the LN_SBPLX machine's state after that.
 static size_t time_std_opt_lds_bytes(int N, int S, int D, bool soft) {
-  return (time_std_bytes(N, S, D, soft) + 15) / 16 * 16 + sbplx::kStateBytes;
+  return (time_std_bytes(N, S, D, soft) + 15) / 16 * 16 + sbplx::state_bytes(S);
 }
 
 // objectiveFunctionTime / getCostAndGradientTime on one trajectory per
@@ -281,6 +281,7 @@ __device__ __attribute__((always_inline)) void time_optimize_body(
       mach.init(S, T, p.initial_stepsize_rel > 0.0 ? p.initial_stepsize_rel : 0.1, max_evals,
                 p.f_rel, p.f_abs);
     __syncthreads();
+    if (sbs->done) phase = kDone;  // start outside the bounds (NLopt: FAILURE)
   }
   MTG_STAMP(460);
   while (phase != kDone) {
@@ -355,7 +356,7 @@ __device__ __attribute__((always_inline)) void time_optimize_body(
   __syncthreads();
   MTG_STAMP(461);
   if (sb) {  // NLopt's x and opt_f: the best point and its value
-    for (int i = lane; i < S; i += kWave) Tcur[i] = sbs->x[i];
+    for (int i = lane; i < S; i += kWave) Tcur[i] = sbplx::best_x(sbs)[i];
     f = sbs->minf;
     evals = sbs->nevals;
     res = sbs->result;
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(kWave) void time_optimize_wave_kernel(
     int32_t* __restrict__ result_out, int32_t* __restrict__ status) {
   using G = wave::Geo<N, R, D, S>;
   constexpr int CB = kSoft ? S * D * N + kMaxSoftConstraints * (N + 2) : 0;
-  constexpr int SB = static_cast<int>(sbplx::kStateBytes / sizeof(double));
+  constexpr int SB = static_cast<int>(sbplx::state_bytes(S) / sizeof(double));
   __shared__ __attribute__((aligned(16))) double sm[(G::L_N + CB + 1) / 2 * 2 + SB];
   wave::Solver<N, R, D, S> sv;
   sv.init(sm);

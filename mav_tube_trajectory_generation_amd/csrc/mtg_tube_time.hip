@@ -21,6 +21,7 @@
 #include <cmath>
 
 #include "mtg_internal.h"
+#include "mtg_sbplx_device.h"
 
 namespace mtg {
 
@@ -80,6 +81,8 @@ __global__ void tube_time_finish_kernel(int S, int64_t B, int P, const double* _
 struct OptState {
   double *T0, *Tc, *g, *Ttr, *f, *alpha;
   int32_t *evals, *done, *st;
+  char* sb;         // LN_SBPLX: one machine state per trajectory (sb_bytes each)
+  size_t sb_bytes;
 };
 
 __global__ void tube_time_opt_init_kernel(int S, int64_t B, const double* __restrict__ times,
@@ -174,6 +177,73 @@ __global__ void tube_time_opt_final_kernel(int S, int64_t B, OptState s,
   }
 }
 
+// LN_SBPLX over the QCQP objective (optimizer 1), the reference's default
+// optimizeTime (nonlinear_impl:332-397: NLopt's Subplex from T0, bounds
+// [0.1, 2 T0], initial steps initial_stepsize_rel T0, maxeval, ftol) on
+// objectiveFunctionTime with solveQCQP() at every evaluation (:891-892).  One
+// evaluation per trajectory per round; the machine (mtg_sbplx_device.h) of
+// trajectory b lives in the workspace and one thread advances it between
+// rounds.  NLopt evaluates T0 first, so the initial solveQCQP (:342) is the
+// first round's solve.
+__device__ inline sbplx::State* sb_state(const OptState& s, int64_t b) {
+  return reinterpret_cast<sbplx::State*>(s.sb + static_cast<size_t>(b) * s.sb_bytes);
+}
+
+__global__ void tube_time_sbplx_init_kernel(int S, int64_t B, const double* __restrict__ times,
+                                            double step_rel, int max_evals, double ftol_rel,
+                                            double ftol_abs, OptState s) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  for (int i = 0; i < S; ++i) {
+    const double t = times[b * S + i];
+    s.T0[b * S + i] = t;
+    s.Ttr[b * S + i] = t;
+  }
+  sbplx::Machine m{sb_state(s, b)};
+  m.init(S, s.Ttr + b * S, step_rel, max_evals, ftol_rel, ftol_abs);
+  s.done[b] = m.s->done;  // a start outside the bounds: no evaluation
+  s.st[b] = MTG_TRAJ_OK;
+}
+
+// Hand the round's J to the machine; it writes the next point into Ttr or
+// finishes.  The QCQP status of the first evaluation (T0) is the one
+// reported.
+__global__ void tube_time_sbplx_step_kernel(int S, int64_t B, int first,
+                                            const double* __restrict__ Jall,
+                                            const int32_t* __restrict__ qstatus, OptState s) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B || s.done[b]) return;
+  if (first) s.st[b] = qstatus[b];
+  sbplx::Machine m{sb_state(s, b)};
+  m.resume(Jall[b], s.Ttr + b * S);
+  if (m.s->done) s.done[b] = 1;
+}
+
+// NLopt's x and opt_f (the best point and its value), the evaluations used
+// and the nlopt_result code.
+__global__ void tube_time_sbplx_final_kernel(int S, int64_t B, OptState s,
+                                             double* __restrict__ times_io,
+                                             double* __restrict__ cost,
+                                             int32_t* __restrict__ evals,
+                                             int32_t* __restrict__ result,
+                                             int32_t* __restrict__ status) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const sbplx::State* st = sb_state(s, b);
+  const double* x = sbplx::best_x(st);
+  for (int i = 0; i < S; ++i) times_io[b * S + i] = x[i];
+  if (cost) cost[b] = st->minf;
+  if (evals) evals[b] = st->nevals;
+  if (result) result[b] = st->result;
+  if (status) status[b] = s.st[b];
+}
+
+__global__ void tube_time_opt_result_kernel(int64_t B, int max_evals, OptState s,
+                                            int32_t* __restrict__ result) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b < B) result[b] = s.evals[b] >= max_evals ? sbplx::kMaxEval : sbplx::kXtol;
+}
+
 unsigned blocks_for(int64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
 // Caller-owned workspace (mtg_tube_time_workspace_bytes), carved in a fixed
@@ -196,7 +266,7 @@ struct Carver {
   }
 };
 size_t carve(void* base, int N, int S, int64_t B, int P, int n_soft, bool optimiser,
-             Workspace* w) {
+             bool sbplx_opt, Workspace* w) {
   Carver c{static_cast<char*>(base)};
   const int64_t BP = B * P;
   w->coeffs = c.take<double>(BP * S * 3 * N);
@@ -217,6 +287,10 @@ size_t carve(void* base, int N, int S, int64_t B, int P, int n_soft, bool optimi
     w->s.evals = c.take<int32_t>(B);
     w->s.done = c.take<int32_t>(B);
     w->s.st = c.take<int32_t>(B);
+    if (sbplx_opt) {
+      w->s.sb_bytes = sbplx::state_bytes(S);
+      w->s.sb = c.take<char>(B * static_cast<int64_t>(w->s.sb_bytes));
+    }
   }
   return c.off;
 }
@@ -268,7 +342,10 @@ hipError_t evaluate_points(const TubeArgs& a, int P, const double* T, double tol
   return hipGetLastError();
 }
 
+// LN_SBPLX is gradient-free: one point per round.
+bool sbplx_of(const mtg_time_params& p, bool optimiser) { return optimiser && p.optimizer == 1; }
 int points_of(const mtg_time_params& p, int S, bool optimiser) {
+  if (sbplx_of(p, optimiser)) return 1;
   return (optimiser || p.grad_mode == 2) ? 2 * S + 1 : 1;
 }
 
@@ -277,7 +354,9 @@ int points_of(const mtg_time_params& p, int S, bool optimiser) {
 size_t tube_time_workspace_bytes(int N, int S, int64_t B, const mtg_time_params& p,
                                  bool optimiser) {
   Workspace w;
-  return carve(nullptr, N, S, B, points_of(p, S, optimiser), p.n_soft, optimiser, &w) + 256;
+  return carve(nullptr, N, S, B, points_of(p, S, optimiser), p.n_soft, optimiser,
+               sbplx_of(p, optimiser), &w) +
+         256;
 }
 
 int64_t tube_time_problems(int S, int64_t B, const mtg_time_params& p, bool optimiser) {
@@ -291,7 +370,7 @@ int tube_time_cost(const TubeArgs& a, double tol, int max_iter, const mtg_time_p
   Workspace w;
   if (tube_time_workspace_bytes(a.N, a.S, a.B, p, false) > workspace_bytes)
     return MTG_ERR_INVALID_ARG;
-  carve(workspace, a.N, a.S, a.B, P, p.n_soft, false, &w);
+  carve(workspace, a.N, a.S, a.B, P, p.n_soft, false, false, &w);
   const hipError_t e = evaluate_points(a, P, a.times, tol, max_iter, p, w, nullptr, nullptr,
                                        cost, p.grad_mode == 2 ? grad : nullptr, status, st);
   return e == hipSuccess ? MTG_OK : MTG_ERR_HIP;
@@ -303,16 +382,23 @@ int tube_time_cost(const TubeArgs& a, double tol, int max_iter, const mtg_time_p
 // know when to stop and the whole call can be captured in a graph.
 int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_iter,
                        const mtg_time_params& p, int max_evals, double* cost, int32_t* evals,
-                       int32_t* status, void* workspace, size_t workspace_bytes,
+                       int32_t* result, int32_t* status, void* workspace, size_t workspace_bytes,
                        hipStream_t st) {
   const int S = a.S, P = points_of(p, S, true);
   const int64_t B = a.B;
+  const bool sb = sbplx_of(p, true);
   Workspace w;
   if (tube_time_workspace_bytes(a.N, S, B, p, true) > workspace_bytes) return MTG_ERR_INVALID_ARG;
-  carve(workspace, a.N, S, B, P, p.n_soft, true, &w);
+  carve(workspace, a.N, S, B, P, p.n_soft, true, sb, &w);
   const OptState& s = w.s;
-  hipLaunchKernelGGL(tube_time_opt_init_kernel, dim3(blocks_for(B * S)), dim3(256), 0, st, S, B,
-                     times_io, s);
+  if (sb) {
+    hipLaunchKernelGGL(tube_time_sbplx_init_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S, B,
+                       times_io, p.initial_stepsize_rel > 0.0 ? p.initial_stepsize_rel : 0.1,
+                       max_evals, p.f_rel, p.f_abs, s);
+  } else {
+    hipLaunchKernelGGL(tube_time_opt_init_kernel, dim3(blocks_for(B * S)), dim3(256), 0, st, S,
+                       B, times_io, s);
+  }
   if (hipGetLastError() != hipSuccess) return MTG_ERR_HIP;
   // Control-point maps stay at the initial times (built once at setup,
   // qcqp_impl:152-157); Q and A^-1 follow the evaluation points.
@@ -322,12 +408,25 @@ int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_
     hipError_t e = evaluate_points(q, P, s.Ttr, tol, max_iter, p, w, s.done, w.Jall, nullptr,
                                    nullptr, nullptr, st);
     if (e != hipSuccess) return MTG_ERR_HIP;
-    hipLaunchKernelGGL(tube_time_opt_step_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S, B, P,
-                       round == 0 ? 1 : 0, max_evals, p.increment, w.Jall, w.qstatus, s);
+    if (sb)
+      hipLaunchKernelGGL(tube_time_sbplx_step_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S,
+                         B, round == 0 ? 1 : 0, w.Jall, w.qstatus, s);
+    else
+      hipLaunchKernelGGL(tube_time_opt_step_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S, B,
+                         P, round == 0 ? 1 : 0, max_evals, p.increment, w.Jall, w.qstatus, s);
     if (hipGetLastError() != hipSuccess) return MTG_ERR_HIP;
   }
-  hipLaunchKernelGGL(tube_time_opt_final_kernel, dim3(blocks_for(B * S)), dim3(256), 0, st, S, B,
-                     s, times_io, cost, evals, status);
+  if (sb) {
+    hipLaunchKernelGGL(tube_time_sbplx_final_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S, B,
+                       s, times_io, cost, evals, result, status);
+  } else {
+    hipLaunchKernelGGL(tube_time_opt_final_kernel, dim3(blocks_for(B * S)), dim3(256), 0, st, S,
+                       B, s, times_io, cost, evals, status);
+    // the descent's stopping reason: 5 at max_evals, 4 when its step vanished
+    if (result && hipGetLastError() == hipSuccess)
+      hipLaunchKernelGGL(tube_time_opt_result_kernel, dim3(blocks_for(B)), dim3(256), 0, st, B,
+                         max_evals, s, result);
+  }
   return hipGetLastError() == hipSuccess ? MTG_OK : MTG_ERR_HIP;
 }
 

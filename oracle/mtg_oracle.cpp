@@ -2008,6 +2008,50 @@ int orc_tube_time_cost(int N, int D, int r, int S, int K, const uint8_t* mask,
   return 0;
 }
 
+// optimizeTime in the fork's form with the reference's default LN_SBPLX
+// (nonlinear_impl:332-397): NLopt's Subplex (orc_sbplx.cpp) on
+// objectiveFunctionTime with solveQCQP() at every evaluation (:891-892),
+// control-point maps at the initial times (built once at setup,
+// qcqp_impl:152-157), bounds [0.1, 2 T0], initial steps step_rel T0,
+// maxeval max_evals, ftol f_rel / f_abs (:95-101).  The initial solveQCQP
+// (:342) only stores trajectory_initial_; NLopt's first evaluation solves
+// at T0 again, so it is not repeated here.  times_io: in T0, out NLopt's x;
+// *cost opt_f; result the nlopt_result code; status the QCQP return at T0
+// (0, or the orc_tube_qcqp_solve failure code); history (nullable,
+// max_evals x S) the evaluated points in order.
+int orc_tube_time_optimize_sbplx(int N, int D, int r, int S, int K, const uint8_t* mask,
+                                 const double* vals, const double* radii, double* times_io,
+                                 double tol, int max_iter, double time_penalty, int max_evals,
+                                 double f_rel, double f_abs, double step_rel, int n_soft,
+                                 const int* soft_derivatives, const double* soft_limits,
+                                 double soft_weight, double soft_maximum_cost, double* cost,
+                                 int* evals, int* result, double* history) {
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  const std::vector<double> T0(times_io, times_io + S);
+  int k = 0;
+  auto objective = [&](const double* tp) {
+    if (history && k < max_evals)
+      std::memcpy(history + static_cast<size_t>(k) * S, tp, sizeof(double) * S);
+    ++k;
+    const std::vector<double> t(tp, tp + S);
+    return tubeTimeObjective(N, D, r, S, K, mask, vals, T0.data(), radii, tol, max_iter,
+                             time_penalty, &soft, t);
+  };
+  std::vector<double> lb(S, 0.1), ub(S), step(S);
+  for (int i = 0; i < S; ++i) {
+    ub[i] = 2.0 * T0[i];
+    step[i] = step_rel * T0[i];
+  }
+  double minf = 0.0;
+  int nev = 0;
+  const int res = orc_sbplx_run(S, objective, lb.data(), ub.data(), times_io, &minf, step.data(),
+                                max_evals, f_rel, f_abs, &nev);
+  if (cost) *cost = minf;
+  if (evals) *evals = nev;
+  if (result) *result = res;
+  return 0;
+}
+
 // mtg_tube_time_optimize's algorithm: timeOptimizeImpl's steps on the QCQP
 // objective, control-point maps at the initial times, stopping also at a
 // non-finite objective or gradient.
@@ -2066,8 +2110,8 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                        const uint8_t* masks, const double* vals, const double* times,
                        const double* radii, int param_i, double param_d, int threads,
                        double min_seconds, int64_t* units, double* seconds) {
-  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 6) return -1;
-  if ((kind == 2 || kind == 5) && !radii) return -1;
+  if (B < 1 || threads < 1 || !masks || !vals || !times || kind < 1 || kind > 7) return -1;
+  if ((kind == 2 || kind == 5 || kind == 7) && !radii) return -1;
   if (kind == 3 && !(param_d > 0.0)) return -1;
   const size_t mstride = static_cast<size_t>(S + 1) * K;
   // kinds 3, 4: coefficients solved before the clock starts.
@@ -2114,6 +2158,18 @@ int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,
                                     nullptr))
           failed = 1;
         acc += c;
+        ++n;
+      } else if (kind == 7) {
+        // optimizeTime in the fork's QCQP form with LN_SBPLX, maxeval param_i
+        std::vector<double> t(tb, tb + S);
+        double c = 0.0;
+        int ev = 0, res = 0;
+        if (orc_tube_time_optimize_sbplx(N, D, r, S, K, mk, vl,
+                                         radii + static_cast<size_t>(b) * S * 2, t.data(), 1e-10,
+                                         100, 500.0, param_i, 0.05, -1.0, 0.1, 0, nullptr,
+                                         nullptr, 100.0, 1.0e12, &c, &ev, &res, nullptr))
+          failed = 1;
+        acc += std::isfinite(c) ? c : 0.0;
         ++n;
       } else if (kind == 2) {
         double c = 0.0;

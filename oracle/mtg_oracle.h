@@ -178,6 +178,16 @@ int orc_tube_time_optimize(int N, int D, int r, int S, int K, const uint8_t* mas
                            const double* soft_limits, double soft_weight,
                            double soft_maximum_cost, double* cost, int* evals);
 
+// optimizeTime in the fork's QCQP form with LN_SBPLX (orc_sbplx.cpp): the
+// reference's default kOptimizeTime path (nonlinear_impl:332-397, 877-945).
+int orc_tube_time_optimize_sbplx(int N, int D, int r, int S, int K, const uint8_t* mask,
+                                 const double* vals, const double* radii, double* times_io,
+                                 double tol, int max_iter, double time_penalty, int max_evals,
+                                 double f_rel, double f_abs, double step_rel, int n_soft,
+                                 const int* soft_derivatives, const double* soft_limits,
+                                 double soft_weight, double soft_maximum_cost, double* cost,
+                                 int* evals, int* result, double* history);
+
 // CPU baseline timing (bench.py cpu_baseline leg): repeat setupFromVertices +
 // solveLinear + computeCost (the region polynomial_timing_evaluation.cpp:
 // 93-110 times) over B trajectories given in dense vertex form
@@ -244,7 +254,8 @@ int orc_sbplx_test(int n, const double* lb, const double* ub, double* x, const d
 // max |a| <= 5 (two computeMaximumOfMagnitude searches) on coefficients
 // solved before the clock starts; kind 5: orc_tube_time_cost with the
 // grad_mode 2 gradient (2S + 1 QCQP solves, times_cp = times); kind 6:
-// orc_time_optimize_sbplx with max_evals = param_i (f_rel 0.05, step 0.1).  *units =
+// orc_time_optimize_sbplx with max_evals = param_i (f_rel 0.05, step 0.1); kind
+// 7: orc_tube_time_optimize_sbplx with max_evals = param_i.  *units =
 // optimisations (1), solves (2), samples (3, one sample = all derivatives of
 // all dimensions at one time), trajectories (4) or evaluations (5).
 int orc_bench_workload(int kind, int N, int D, int r, int S, int K, int B,

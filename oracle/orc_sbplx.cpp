@@ -200,6 +200,16 @@ int orc_sbplx_run(int n, const std::function<double(const double*)>& f, const do
   stop.ftol_rel = ftol_rel;
   stop.ftol_abs = ftol_abs;
   int ret = kSbplxSuccess;
+  // NLopt refuses a start outside the bounds (or lb > ub) before evaluating
+  // anything (nlopt_optimize returns NLOPT_INVALID_ARGS; nlopt::opt::optimize
+  // throws and optimizeTime returns nlopt::FAILURE, nonlinear_impl:389-394):
+  // x unchanged, no evaluation.
+  for (int i = 0; i < n; ++i)
+    if (lb[i] > ub[i] || x[i] < lb[i] || x[i] > ub[i]) {
+      *minf = std::numeric_limits<double>::quiet_NaN();
+      if (nevals) *nevals = 0;
+      return kSbplxFailure;
+    }
   *minf = f(x);
   ++stop.nevals;
   std::vector<double> xstep(xstep0, xstep0 + n), xprev(n), dx(n, 0.0);

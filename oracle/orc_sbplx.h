@@ -3,7 +3,7 @@
 #pragma once
 #include <functional>
 
-constexpr int kSbplxFailure = -1;  // NLOPT_FAILURE (a degenerate initial simplex)
+constexpr int kSbplxFailure = -1;  // NLOPT_FAILURE (degenerate simplex; start out of bounds)
 constexpr int kSbplxSuccess = 1;   // NLOPT_SUCCESS
 constexpr int kSbplxFtol = 3;      // NLOPT_FTOL_REACHED
 constexpr int kSbplxXtol = 4;      // NLOPT_XTOL_REACHED

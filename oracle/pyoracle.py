@@ -405,6 +405,37 @@ def tube_time_optimize(N, r, vertices, times, radii, max_evals, tol=1e-10, max_i
     return t, float(cost[0]), evals.value
 
 
+def tube_time_optimize_sbplx(N, r, vertices, times, radii, max_evals, tol=1e-10, max_iter=100,
+                             time_penalty=500.0, f_rel=0.05, f_abs=-1.0, step_rel=0.1,
+                             soft=None, soft_weight=100.0, soft_maximum_cost=1.0e12):
+    """orc_tube_time_optimize_sbplx: optimizeTime in the fork's QCQP form with
+    LN_SBPLX (nonlinear_impl:332-397, 877-945).  Returns dict(times, cost,
+    evals, result, history [evals, S])."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    t = np.array(times, dtype=np.float64)
+    radii = np.ascontiguousarray(radii, dtype=np.float64).reshape(S, 2)
+    cost = np.zeros(1)
+    evals = ctypes.c_int()
+    result = ctypes.c_int()
+    hist = np.zeros((max_evals, S))
+    ns, der, lim = _soft_arrays(soft)
+    L = lib()
+    L.orc_tube_time_optimize_sbplx.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+        ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, _ip, _dp,
+        ctypes.c_double, ctypes.c_double, _dp, ctypes.POINTER(ctypes.c_int),
+        ctypes.POINTER(ctypes.c_int), _dp]
+    _check(L.orc_tube_time_optimize_sbplx(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                          _d(vertices.vals), _d(radii), _d(t), tol, max_iter,
+                                          time_penalty, max_evals, f_rel, f_abs, step_rel, ns,
+                                          der.ctypes.data_as(_ip), _d(lim), soft_weight,
+                                          soft_maximum_cost, _d(cost), ctypes.byref(evals),
+                                          ctypes.byref(result), _d(hist)),
+           "tube_time_optimize_sbplx")
+    return dict(times=t, cost=float(cost[0]), evals=evals.value, result=result.value,
+                history=hist[:evals.value])
+
+
 def evaluate_range(N, coeffs, times, t_start, t_end, dt, derivative, max_out=None):
     """Trajectory::evaluateRange (trajectory.cpp:74-134) on coeffs [S, D, N]."""
     coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)

@@ -10,6 +10,8 @@
 //   test_polynomial_optimization gpu    -> the parity tests proper
 #define MTG_CHECK_THROWS 1
 
+#include <algorithm>
+#include <chrono>
 #include <fstream>
 #include <random>
 #include <sstream>
@@ -677,6 +679,83 @@ TEST(gpu, TimeCostWithQCQPInnerSolve) {
   traj.getSegments(&segs);
   EXPECT_TRUE(segs.size() == 4);
   EXPECT_LE(std::fabs(segs.front().evaluate(0.0, 0)[0] - 2.7), 1e-9);
+}
+
+// The reference's own kOptimizeTime path with its defaults: LN_SBPLX over
+// objectiveFunctionTime with solveQCQP() at every evaluation
+// (nonlinear_impl:332-397, 877-945).  The shim's result (evaluations,
+// nlopt_result, optimised times, cost) follows the oracle's Subplex over its
+// own interior-point QCQP (orc_tube_time_optimize_sbplx).
+TEST(gpu, OptimizeTimeQCQPSbplxMatchesOracle) {
+  const Vertex::Vector vs = mainCppVertices();
+  const std::vector<double> t0 = estimateSegmentTimes(vs, 2.0, 2.0);
+  const std::vector<std::pair<double, double>> radii(4, {0.15, 0.15});
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.weights.w_c = 0.0;
+  p.solve_time_with_qcqp = true;
+  p.max_iterations = 40;
+  EXPECT_TRUE(p.algorithm == nlopt::LN_SBPLX);
+  PolynomialOptimizationNonLinear<10> opt(3, p);
+  opt.setupFromVertices(vs, t0, radii, 4);
+  const int res = opt.optimize();
+  const OptimizationInfo info = opt.getOptimizationInfo();
+  Trajectory traj;
+  opt.getTrajectory(&traj);
+  const std::vector<double> t1 = traj.getSegmentTimes();
+  const Dense d = toDense(vs, 5);
+  std::vector<double> ot = t0, rad(8, 0.15);
+  double oc = 0.0;
+  int oev = 0, ores = 0;
+  EXPECT_TRUE(orc_tube_time_optimize_sbplx(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(),
+                                           rad.data(), ot.data(), 1e-10, 100, p.time_penalty,
+                                           40, p.f_rel, p.f_abs, p.initial_stepsize_rel, 0,
+                                           nullptr, nullptr, 100.0, 1e12, &oc, &oev, &ores,
+                                           nullptr) == 0);
+  std::fprintf(stderr, "QCQP LN_SBPLX: result %d (oracle %d), evals %d (oracle %d)\n", res,
+               ores, static_cast<int>(info.n_iterations), oev);
+  EXPECT_TRUE(res == ores);
+  EXPECT_TRUE(info.n_iterations == oev);
+  EXPECT_LE(relErr(t1, ot), 1e-6);
+  EXPECT_LE(relErr(info.cost_trajectory + info.cost_time, oc), 1e-6);
+}
+
+// kOptimizeTime with the default LN_SBPLX on more than 16 segments (the
+// machine's state is sized by the segment count): the objective does not
+// rise and the bounds hold.
+TEST(gpu, OptimizeTimeSbplxManySegments) {
+  const Fixture f{3, 4, 24, 111, 3.0, 5.0};
+  const Vertex::Vector vs = fixtureVertices(f, 10);
+  const std::vector<double> t0 = estimateSegmentTimes(vs, f.vmax, f.amax);
+  NonlinearOptimizationParameters p;
+  p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.weights.w_c = 0.0;
+  p.max_iterations = 60;
+  PolynomialOptimizationNonLinear<10> opt(f.D, p);
+  opt.setupFromVertices(vs, t0, std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}), f.r);
+  const double J0 = opt.evaluateTimeCost(t0);
+  const int res = opt.optimize();
+  EXPECT_TRUE(res == nlopt::MAXEVAL_REACHED || res == nlopt::FTOL_REACHED ||
+              res == nlopt::XTOL_REACHED);
+  std::vector<double> t1;
+  opt.getPolynomialOptimizationRef().getSegmentTimes(&t1);
+  const OptimizationInfo info = opt.getOptimizationInfo();
+  EXPECT_TRUE(info.n_iterations >= 1 && info.n_iterations <= 60);
+  EXPECT_LE(opt.evaluateTimeCost(t1), J0);
+  for (size_t i = 0; i < t1.size(); ++i) {
+    EXPECT_TRUE(t1[i] >= 0.1 - 1e-15);
+    EXPECT_TRUE(t1[i] <= 2.0 * t0[i] + 1e-12);
+  }
+  const Dense d = toDense(vs, 5);
+  std::vector<double> ot = t0;
+  double oc = 0.0;
+  int oev = 0, ores = 0;
+  EXPECT_TRUE(orc_time_optimize_sbplx(10, f.D, f.r, f.S, 5, d.mask.data(), d.vals.data(),
+                                      ot.data(), p.time_penalty, 60, p.f_rel, p.f_abs,
+                                      p.initial_stepsize_rel, 0, nullptr, nullptr, 100.0, 1e12,
+                                      &oc, &oev, &ores, nullptr) == 0);
+  EXPECT_TRUE(res == ores && info.n_iterations == oev);
+  EXPECT_LE(relErr(t1, ot), 1e-6);
 }
 
 // Extrema test of the reference (test_polynomial_optimization.cpp:370-400):
@@ -1640,6 +1719,53 @@ TEST(gpu, EndpointBoundsRejectPositionMagnitude) {
   opt.setOccupancyGrid(occ, nx, ny, nz);
   opt.addMaximumMagnitudeConstraint(derivative_order::POSITION, 20.0);
   EXPECT_THROW(opt.optimize());
+}
+
+// Latency of the drop-in single-trajectory call (run on demand: the
+// "latency" group).  PolynomialOptimization<10>::solveLinear() at S = 3 (C1,
+// BASELINE.json configs[0]) and S = 10 goes through mtg_linear_solve_host:
+// one H2D copy, one launch and one D2H copy on the plan's own stream.  Each
+// call is timed alone (steady_clock) after a warm-up; the oracle's
+// setupFromVertices + solveLinear + computeCost on one host core
+// (orc_bench_linear, the reference's timed region) is timed beside it.
+// Prints one JSON line per size.
+TEST(latency, SolveLinearSingle) {
+  for (int S : {3, 10}) {
+    const Fixture f{3, 4, S, 105, 3.0, 5.0};
+    const Vertex::Vector vs = fixtureVertices(f, 10);
+    const std::vector<double> t = estimateSegmentTimes(vs, f.vmax, f.amax);
+    PolynomialOptimization<10> opt(f.D);
+    opt.setupFromVertices(vs, t, f.r);
+    for (int i = 0; i < 200; ++i) EXPECT_TRUE(opt.solveLinear());
+    const int reps = 5000;
+    std::vector<double> us(reps);
+    const auto t_all = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; ++i) {
+      const auto a = std::chrono::steady_clock::now();
+      opt.solveLinear();
+      us[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a)
+                  .count();
+    }
+    const double mean =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_all)
+            .count() / reps;
+    std::sort(us.begin(), us.end());
+    const Dense d = toDense(vs, 5);
+    int64_t n = 0;
+    double sec = 0.0;
+    EXPECT_TRUE(orc_bench_linear(10, f.D, f.r, S, 5, 1, d.mask.data(), d.vals.data(), t.data(),
+                                 1, 2.0, &n, &sec) == 0);
+    const double cpu_us = sec / static_cast<double>(n) * 1e6;
+    std::printf("LATENCY {\"call\": \"PolynomialOptimization<10>::solveLinear\", \"S\": %d, "
+                "\"D\": 3, \"reps\": %d, \"median_us\": %.3f, \"p10_us\": %.3f, "
+                "\"p90_us\": %.3f, \"mean_us\": %.3f, \"cpu_port_us\": %.3f, "
+                "\"cpu_cores\": 1}\n",
+                S, reps, us[reps / 2], us[reps / 10], us[reps * 9 / 10], mean, cpu_us);
+    // the solution is the oracle's (the staging path returns the same data)
+    Segment::Vector segs;
+    opt.getSegments(&segs);
+    checkPath(vs, segs, 10);
+  }
 }
 
 int main(int argc, char** argv) {

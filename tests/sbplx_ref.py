@@ -48,6 +48,10 @@ def test_fn(x):
 def sbplx(f, lb, ub, x0, xstep0, maxeval, ftol_rel, ftol_abs):
     """Returns (code, best x, best f, evaluation history)."""
     n = len(x0)
+    # NLopt refuses a start outside the bounds before any evaluation
+    # (NLOPT_INVALID_ARGS; optimizeTime returns nlopt::FAILURE)
+    if any(lo > hi or x < lo or x > hi for x, lo, hi in zip(x0, lb, ub)):
+        return FAILURE, list(x0), float("nan"), []
     st = {"x": list(x0), "minf": None, "nevals": 0, "hist": []}
 
     def evaluate(point):

@@ -59,3 +59,18 @@ def test_time_optimize_sbplx_contract(oracle):
         # the reported cost is the objective at the returned point
         Jt, _ = oracle.time_cost(N, r, v, t, grad_mode=0)
         assert abs(Jt - J) <= 1e-9 * abs(J)
+
+
+@pytest.mark.parametrize("x0", [[0.5, 0.08, 0.7], [0.04, 1.0, 1.0]], ids=["below_lb", "lb_gt_ub"])
+def test_start_out_of_bounds_is_failure(oracle, x0):
+    """A start below kOptimizationTimeLowerBound (0.1), or with lb > ub = 2 T0,
+    is NLopt's invalid start (NLOPT_INVALID_ARGS before any evaluation, which
+    optimizeTime returns as nlopt::FAILURE, nonlinear_impl:389-394): both
+    restatements return -1 with no evaluation and x unchanged."""
+    x0 = np.array(x0)
+    lb, ub, step = np.full(3, 0.1), 2.0 * x0, 0.1 * x0
+    code, x, minf, nev, hist = oracle.sbplx_test(lb, ub, x0, step, 40, 0.05, -1.0)
+    assert code == -1 and nev == 0 and np.array_equal(x, x0) and np.isnan(minf)
+    pcode, px, pminf, phist = sbplx_ref.sbplx(sbplx_ref.test_fn, list(lb), list(ub), list(x0),
+                                               list(step), 40, 0.05, -1.0)
+    assert pcode == -1 and phist == [] and px == list(x0)

@@ -85,6 +85,42 @@ def test_select_global_matches_rule(ctx, dev):
                    for x, y in zip(got, ref)), (t, got, ref)
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_select_global_steps_matches_rule(ctx, dev, world):
+    """mtg_select_global_steps, the per-step winners of a bucket at world > 1
+    (shard.select_steps after the RCCL all-gather), on synthetic [world, G,
+    3] rings: NaN costs, empty shards (index -1, cost inf), ties across ranks
+    and buckets with n < G.  Each row g < n must be the select_global rule
+    over the ranks' row g; rows >= n are left untouched."""
+    from mav_tube_trajectory_generation_amd._abi import check, lib
+    from mav_tube_trajectory_generation_amd.batch import _ptr, _stream
+    G = 16
+    rng = np.random.default_rng(world)
+    ring = np.empty((world, G, 3))
+    ring[..., 0] = rng.uniform(1.0, 2.0, (world, G))
+    ring[..., 1] = rng.integers(0, 65536, (world, G)).astype(np.float64)
+    ring[..., 2] = np.arange(world)[:, None]
+    ring[:, 1, 0] = np.nan                      # no finite cost anywhere
+    ring[0, 2, 0] = np.nan                      # NaN on one rank only
+    ring[:, 3, 0] = 1.25                        # a tie on every rank: the first rank
+    ring[-1, 4, :2] = (np.inf, -1.0)            # an empty shard
+    ring[:, 5, :2] = (np.inf, -1.0)             # every shard empty
+    ring[1, 6, 0] = 0.0                         # the winner on rank 1
+    ring[-1, 7, :2] = (0.5, -1.0)               # a finite cost with index -1 never wins
+    flat = torch.from_numpy(np.ascontiguousarray(ring.reshape(-1))).to(dev)
+    for n in (G, 9, 1):
+        out = torch.full((G, 3), 7.0, dtype=torch.float64, device=dev)
+        check(lib().mtg_select_global_steps(_ptr(flat), world, G, n, _ptr(out), _stream(dev)),
+              "mtg_select_global_steps")
+        got = out.cpu().numpy()
+        for g in range(n):
+            ref = _ref_global(ring[:, g])
+            assert all((x == y) or (np.isnan(x) and np.isnan(y)) or
+                       (math.isinf(x) and math.isinf(y)) for x, y in zip(got[g], ref)), \
+                (world, n, g, got[g], ref)
+        assert (got[n:] == 7.0).all(), (world, n)
+
+
 def test_select_best_device_one_rank_rccl(ctx, dev):
     """The whole device selection step (local kernel, RCCL all-gather, global
     kernel) on a one-rank process group, inside a captured HIP graph."""

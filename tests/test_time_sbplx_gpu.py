@@ -24,19 +24,21 @@ torch = pytest.importorskip("torch")
 N, D, R = 10, 3, 4
 
 
-def _run(ctx, dev, S, B, E, kernel="auto", seed0=105, **kw):
+def _run(ctx, dev, S, B, E, kernel="auto", seed0=105, d=D, r=R, times_fn=None, **kw):
     import mav_tube_trajectory_generation_amd as mtg
-    mask, fixed, times, _ = mtg.generate_random_problems(N, D, S, B, seed0=seed0)
-    plan = mtg.LinearPlan(ctx, N, D, R, S, mask).set_kernel(kernel)
+    mask, fixed, times, _ = mtg.generate_random_problems(N, d, S, B, seed0=seed0)
+    if times_fn is not None:
+        times_fn(times)
+    plan = mtg.LinearPlan(ctx, N, d, r, S, mask).set_kernel(kernel)
     fd, td = torch.from_numpy(fixed).to(dev), torch.from_numpy(times).to(dev)
     out = plan.time_optimize(fd, td, max_evals=E, optimizer="sbplx", **kw)
     torch.cuda.synchronize()
     return plan, fd, td, times, {k: v.cpu().numpy() for k, v in out.items()}
 
 
-def _agree(oracle, out, times, S, E, picks, seed0=105, **kw):
+def _agree(oracle, out, times, S, E, picks, seed0=105, d=D, r=R, **kw):
     def ref(b):
-        return b, oracle.time_optimize_sbplx(N, R, standard_vertices(N, S, D, seed0 + b),
+        return b, oracle.time_optimize_sbplx(N, r, standard_vertices(N, S, d, seed0 + b),
                                              times[b], E, **kw)
     agree, n = 0, 0
     with cf.ThreadPoolExecutor(max_workers=8) as ex:
@@ -82,12 +84,49 @@ def test_sbplx_segment_counts(ctx, dev, oracle, S):
         assert agree >= n - 1, (S, E, agree, n)
 
 
-def test_sbplx_generic_and_runtime_kernels(ctx, dev, oracle):
+def test_sbplx_generic_kernel(ctx, dev, oracle):
     """The generic-pattern kernel runs the same machine."""
     S, B, E = 6, 32, 60
     _, _, _, times, out = _run(ctx, dev, S, B, E, kernel="generic")
     agree, n = _agree(oracle, out, times, S, E, list(range(0, B, 4)))
     assert agree >= n - 1, (agree, n)
+
+
+@pytest.mark.parametrize("d,r,S", [(2, 4, 6), (3, 3, 6), (1, 2, 5), (3, 4, 20)],
+                         ids=["D2", "r3", "D1r2", "S20"])
+def test_sbplx_runtime_s_kernel(ctx, dev, oracle, d, r, S):
+    """The runtime-S standard kernel (time_optimize_std_kernel: r = 2/3,
+    D < 3, or S beyond the compile-time-S kernels' 16) runs the same machine,
+    its state sized by S in LDS after the solver's (more than 16 segments,
+    the default kOptimizeTime path of the C++ shim for long trajectories)."""
+    B, E = 24, 60
+    _, _, _, times, out = _run(ctx, dev, S, B, E, d=d, r=r)
+    assert (out["status"] == 0).all()
+    agree, n = _agree(oracle, out, times, S, E, list(range(0, B, 3)), d=d, r=r)
+    assert agree >= n - 1, (d, r, S, agree, n)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "generic"])
+def test_sbplx_start_out_of_bounds(ctx, dev, oracle, kernel):
+    """A segment time below kOptimizationTimeLowerBound (0.1) is NLopt's
+    invalid start (nlopt_optimize returns NLOPT_INVALID_ARGS before any
+    evaluation; optimizeTime returns nlopt::FAILURE, nonlinear_impl:389-394):
+    result -1, no evaluation, times unchanged, cost NaN, as the oracle."""
+    S, B, E = 5, 4, 30
+
+    def shorten(t):
+        t[1, 2] = 0.08
+        t[3, 0] = 0.04  # lb > ub as well
+
+    _, _, _, times, out = _run(ctx, dev, S, B, E, kernel=kernel, times_fn=shorten)
+    for b in (1, 3):
+        assert out["result"][b] == -1 and out["evals"][b] == 0, (b, out["result"][b])
+        assert np.array_equal(out["times"][b], times[b]) and np.isnan(out["cost"][b])
+        Tc, fc, ec, rc, _ = oracle.time_optimize_sbplx(
+            N, R, standard_vertices(N, S, D, 105 + b), times[b], E)
+        assert rc == -1 and ec == 0 and np.array_equal(Tc, times[b])
+    for b in (0, 2):
+        assert out["result"][b] in (3, 4, 5) and out["evals"][b] >= 1
 
 
 def test_sbplx_soft_constraints(ctx, dev, oracle):
