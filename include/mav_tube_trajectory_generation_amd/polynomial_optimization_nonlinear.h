@@ -1009,16 +1009,20 @@ class PolynomialOptimizationNonLinear {
     std::vector<double> times = segmentTimesOfQcqp();
     const size_t np = poly_opt_.getNumberFreeConstraints();
     internal::DeviceBuffer<double> d_df, d_dp, d_t, d_cost(1);
-    internal::DeviceBuffer<int32_t> d_ev(1), d_st(1);
+    internal::DeviceBuffer<int32_t> d_ev(1), d_res(1), d_st(1);
     d_df.upload(packFixedQcqp());
     d_dp.upload(x0);
     d_t.upload(times);
+    // LN_SBPLX (the default) runs NLopt's Subplex restated on the device over
+    // all S + D n_p variables (:610-706); any other algorithm the
+    // block-alternating descent
     const mtg_time_params p = timeParams(0);
     const int budget = params_.max_iterations > 0 ? params_.max_iterations : 1000;
-    internal::checkStatus(mtg_time_free_optimize(poly_opt_.getPlan(), 1, d_df.get(), d_dp.get(),
-                                                 d_t.get(), &p, budget, d_cost.get(), d_ev.get(),
-                                                 d_st.get(), nullptr),
-                          "mtg_time_free_optimize");
+    internal::checkStatus(mtg_time_free_optimize_ex(poly_opt_.getPlan(), 1, d_df.get(),
+                                                    d_dp.get(), d_t.get(), &p, budget,
+                                                    d_cost.get(), d_ev.get(), d_res.get(),
+                                                    d_st.get(), nullptr),
+                          "mtg_time_free_optimize_ex");
     internal::synchronize();
     const std::vector<double> x = d_dp.download();
     d_t.download(times.data(), times.size());
@@ -1026,9 +1030,10 @@ class PolynomialOptimizationNonLinear {
       for (size_t i = 0; i < np; ++i) free[d][i] = x[d * np + i];
     poly_opt_.updateSegmentTimes(times);
     poly_opt_.setFreeConstraints(free);
-    int32_t evals = 0, st = 0;
+    int32_t evals = 0, st = 0, res = 0;
     d_ev.download(&evals, 1);
     d_st.download(&st, 1);
+    d_res.download(&res, 1);
     double J = 0.0, tot = 0.0;
     d_cost.download(&J, 1);
     for (double t : times) tot += t;
@@ -1038,7 +1043,9 @@ class PolynomialOptimizationNonLinear {
     optimization_info_.cost_soft_constraints =
         soft_.empty() ? 0.0
                       : J - optimization_info_.cost_trajectory - optimization_info_.cost_time;
-    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? 5 /* MAXEVAL_REACHED */ : -1;
+    // nlopt_result of the device Subplex; the descent reports MAXEVAL_REACHED
+    const int code = p.optimizer == 1 ? res : 5;
+    optimization_info_.stopping_reason = st == MTG_TRAJ_OK ? code : -1;
     optimization_info_.optimization_time =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     free_optimized_ = true;

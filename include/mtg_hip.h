@@ -332,6 +332,23 @@ int mtg_time_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_
                            double* free_io, double* times_io, const mtg_time_params* params,
                            int max_evals, double* cost, int32_t* evals, int32_t* status,
                            void* stream);
+/* The same with params->optimizer selecting the optimiser and the stopping
+ * reason per trajectory (result, B, nullable; nlopt_result codes):
+ *   0  the block-alternating descent above (result 5 / 4 as the time
+ *      optimiser's descent; not reported: result untouched);
+ *   1  LN_SBPLX, the reference's own algorithm for this objective (the
+ *      default, polynomial_optimization_nonlinear.h:61): NLopt's Subplex
+ *      restated on the device over all S + D n_free variables (its state in
+ *      LDS sized by that count), bounds as above, initial steps
+ *      initial_stepsize_rel |x0| (:664-675), maxeval max_evals, ftol f_rel /
+ *      f_abs.  free_io / times_io out = NLopt's x, cost = opt_f.  A start
+ *      with a zero entry (NLopt rejects a zero initial step) or a time below
+ *      0.1 returns result -1 (nlopt::FAILURE) with no evaluation and x
+ *      unchanged.  `increment` is not used. */
+int mtg_time_free_optimize_ex(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                              double* free_io, double* times_io, const mtg_time_params* params,
+                              int max_evals, double* cost, int32_t* evals, int32_t* result,
+                              int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * Tube QCQP (PolynomialOptimizationConstrained<N>, qcqp_impl).  The tube

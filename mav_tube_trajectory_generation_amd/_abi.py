@@ -156,6 +156,9 @@ SIGNATURES = {
     "mtg_time_free_optimize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp,
                                               ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
                                               _vp, _vp, _vp]),
+    "mtg_time_free_optimize_ex": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp,
+                                                 ctypes.POINTER(TimeParams), ctypes.c_int, _vp,
+                                                 _vp, _vp, _vp, _vp]),
     "mtg_plan_kernel": (ctypes.c_int, [_vp]),
     "mtg_collision_cost": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int,

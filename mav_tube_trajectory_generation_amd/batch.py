@@ -311,10 +311,13 @@ class LinearPlan:
         return dict(free=d, cost=cost, evals=evals, status=status)
 
     def time_free_optimize(self, fixed_vals, free_vals, times, max_evals=50, time_penalty=500.0,
-                           increment=0.1, soft=None, soft_weight=100.0):
+                           increment=0.1, soft=None, soft_weight=100.0, optimizer="fd",
+                           f_rel=0.05, f_abs=-1.0, initial_stepsize_rel=0.1):
         """Optimise segment times and free derivatives together
-        (mtg_time_free_optimize, optimizeTimeAndFreeConstraints) on copies;
-        returns dict(times, free, cost, evals, status)."""
+        (mtg_time_free_optimize_ex, optimizeTimeAndFreeConstraints) on copies;
+        optimizer "sbplx" runs LN_SBPLX over [T; d_p] (the reference's
+        algorithm), "fd" the block-alternating descent.  Returns dict(times,
+        free, cost, evals, result, status)."""
         import torch
         B = times.shape[0]
         _require(times, (B, self.S), "times")
@@ -325,12 +328,16 @@ class LinearPlan:
         d = free_vals.clone()
         cost = torch.empty(B, dtype=torch.float64, device=dev)
         evals = torch.empty(B, dtype=torch.int32, device=dev)
+        result = torch.full((B,), 0, dtype=torch.int32, device=dev)
         status = torch.empty(B, dtype=torch.int32, device=dev)
-        p = make_time_params(time_penalty, increment, 0.1, 1.0, 0, soft, soft_weight)
-        check(lib().mtg_time_free_optimize(self._h, B, _ptr(fixed_vals), _ptr(d), _ptr(t),
-                                           ctypes.byref(p), max_evals, _ptr(cost), _ptr(evals),
-                                           _ptr(status), _stream(dev)), "mtg_time_free_optimize")
-        return dict(times=t, free=d, cost=cost, evals=evals, status=status)
+        p = make_time_params(time_penalty, increment, 0.1, 1.0, 0, soft, soft_weight,
+                             optimizer=optimizer, f_rel=f_rel, f_abs=f_abs,
+                             initial_stepsize_rel=initial_stepsize_rel)
+        check(lib().mtg_time_free_optimize_ex(self._h, B, _ptr(fixed_vals), _ptr(d), _ptr(t),
+                                              ctypes.byref(p), max_evals, _ptr(cost),
+                                              _ptr(evals), _ptr(result), _ptr(status),
+                                              _stream(dev)), "mtg_time_free_optimize_ex")
+        return dict(times=t, free=d, cost=cost, evals=evals, result=result, status=status)
 
     def collision_cost(self, coeffs, times, occupancy, params, grad=True):
         """Collision cost over a dense occupancy grid (mtg_collision_cost,

@@ -26,6 +26,7 @@
 #include "mtg_extrema_device.h"
 #include "mtg_free_device.h"
 #include "mtg_internal.h"
+#include "mtg_sbplx_device.h"
 
 namespace mtg {
 
@@ -394,6 +395,95 @@ __global__ __launch_bounds__(kWave) void time_free_optimize_kernel(
   }
 }
 
+// LDS of the LN_SBPLX form: the free layout, then the evaluation point X
+// (S + D np values) and the machine state.
+struct FreeSbplxLds {
+  size_t x, state, bytes;
+};
+__host__ __device__ inline FreeSbplxLds free_sbplx_lds(int N, int S, int D, int np, bool soft) {
+  FreeSbplxLds f;
+  const int n = S + D * np;
+  f.x = (free_lds(N, S, D, np, soft).bytes + 15) / 16 * 16;
+  f.state = (f.x + sizeof(double) * n + 15) / 16 * 16;
+  f.bytes = f.state + sbplx::state_bytes(n);
+  return f;
+}
+
+// kOptimizeFreeConstraintsAndTime with the reference's own algorithm:
+// NLopt's LN_SBPLX (the default, polynomial_optimization_nonlinear.h:61;
+// optimizeTimeAndFreeConstraints, nonlinear_impl:610-706) over
+// x = [T; d_p] (d_p dimension-major, :653-662) on
+// objectiveFunctionTimeAndConstraints (:947-1019: updateSegmentTimes(T),
+// setFreeConstraints(d_p), computeCost() + time_penalty (sum T)^2 [+ soft];
+// no re-solve).  Bounds T in [0.1, 2 |T0|], d_p in [-2 |d0|, 2 |d0|], initial
+// steps initial_stepsize_rel |x0| (:664-675), maxeval, ftol (:95-101).  The
+// machine (mtg_sbplx_device.h) runs on lane 0 with its state in LDS sized by
+// n = S + D np; the wave evaluates.  x0 with a zero entry (a zero initial
+// step) or a time below 0.1 is NLopt's invalid argument: result -1
+// (nlopt::FAILURE, :681-691, 696-703), no evaluation, x unchanged.
+template <int N, bool kSoft>
+__global__ __launch_bounds__(kWave) void time_free_sbplx_kernel(
+    PlanDev pl, const double* __restrict__ fixed_vals, double* __restrict__ free_io,
+    double* __restrict__ times_io, mtg_time_params p, int max_evals, double* __restrict__ cost,
+    int32_t* __restrict__ evals_out, int32_t* __restrict__ result_out,
+    int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int S = pl.S, D = pl.D, nf = pl.nf, np = pl.np, n = D * np, nx = S + n;
+  const Layout lay = make_layout(N, S, D);
+  const FreeLds fl = free_lds(N, S, D, np, kSoft);
+  const FreeSbplxLds fs = free_sbplx_lds(N, S, D, np, kSoft);
+  Traj<N> t{S, D, pl.r, &lay, smem, reinterpret_cast<int*>(smem + lay.ndouble),
+            static_cast<int>(threadIdx.x), pl.fmask, pl.use_mask != 0};
+  const int64_t b = blockIdx.x;
+  double* cbuf = lds_at<double>(smem, fl.cbuf);
+  double* X = lds_at<double>(smem, fs.x);
+  auto* sbs = lds_at<sbplx::State>(smem, fs.state);
+  sbplx::Machine mach{sbs};
+  const bool bad = free_setup(t, pl, fixed_vals + b * D * nf, nullptr, times_io + b * S);
+  auto slot_of = [&](int i) { return pl.free_map[i % np] * D + i / np; };
+  double f = NAN;
+  int evals = 0, res = sbplx::kFailure;
+  if (!bad) {
+    const double step_rel = p.initial_stepsize_rel > 0.0 ? p.initial_stepsize_rel : 0.1;
+    if (t.lane == 0) sbs->n = nx;
+    for (int i = t.lane; i < nx; i += kWave) X[i] = i < S ? t.T()[i] : free_io[b * n + i - S];
+    __syncthreads();
+    for (int i = t.lane; i < nx; i += kWave) {  // the bounds of :665-677, filled in parallel
+      const double v = X[i], a = fabs(v);
+      mach.x()[i] = v;
+      mach.lb()[i] = i < S ? 0.1 : -2.0 * a;
+      mach.ub()[i] = 2.0 * a;
+      mach.xstep()[i] = step_rel * a;
+    }
+    __syncthreads();
+    if (t.lane == 0) mach.start(max_evals, p.f_rel, p.f_abs);
+    __syncthreads();
+    while (!sbs->done) {
+      // the point X: times (powers recomputed) and d_p into the vertex table
+      for (int i = t.lane; i < S; i += kWave) t.T()[i] = X[i];
+      for (int i = t.lane; i < n; i += kWave) t.dv()[slot_of(i)] = X[S + i];
+      __syncthreads();
+      t.compute_powers();
+      __syncthreads();
+      const double J = free_objective<N, kSoft>(t, pl.tab, p, 1, cbuf);
+      if (t.lane == 0) mach.resume(J, X);
+      __syncthreads();
+    }
+    const double* xb = sbplx::best_x(sbs);
+    for (int i = t.lane; i < S; i += kWave) times_io[b * S + i] = xb[i];
+    for (int i = t.lane; i < n; i += kWave) free_io[b * n + i] = xb[S + i];
+    f = sbs->minf;
+    evals = sbs->nevals;
+    res = sbs->result;
+  }
+  if (t.lane == 0) {
+    if (cost) cost[b] = f;
+    if (evals_out) evals_out[b] = evals;
+    if (result_out) result_out[b] = res;
+    if (status) status[b] = bad ? MTG_TRAJ_BAD_TIME : MTG_TRAJ_OK;
+  }
+}
+
 namespace {
 template <typename K>
 hipError_t prepare_lds_free(K kernel, size_t bytes) {
@@ -473,6 +563,32 @@ hipError_t time_free_opt_n(const PlanDev& pl, int64_t B, const double* df, doubl
 size_t free_lds_bytes(int N, int S, int D, int np, bool soft) {
   return free_lds(N, S, D, np, soft).bytes;
 }
+size_t free_sbplx_lds_bytes(int N, int S, int D, int np, bool soft) {
+  return free_sbplx_lds(N, S, D, np, soft).bytes;
+}
+
+template <int N>
+hipError_t time_free_sbplx_n(const PlanDev& pl, int64_t B, const double* df, double* dp,
+                             double* times, const mtg_time_params& p, int max_evals,
+                             double* cost, int32_t* evals, int32_t* result, int32_t* status,
+                             hipStream_t st) {
+  const bool soft = p.n_soft > 0;
+  const size_t bytes = free_sbplx_lds(N, pl.S, pl.D, pl.np, soft).bytes;
+  if (soft) {
+    hipError_t e = prepare_lds_free(time_free_sbplx_kernel<N, true>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_free_sbplx_kernel<N, true>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, dp, times, p, max_evals, cost, evals,
+                       result, status);
+  } else {
+    hipError_t e = prepare_lds_free(time_free_sbplx_kernel<N, false>, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((time_free_sbplx_kernel<N, false>), dim3(static_cast<unsigned>(B)),
+                       dim3(kWave), bytes, st, pl, df, dp, times, p, max_evals, cost, evals,
+                       result, status);
+  }
+  return hipGetLastError();
+}
 
 #define MTG_FREE_DISPATCH(FN, ...)        \
   switch (pl.N) {                         \
@@ -492,8 +608,12 @@ hipError_t launch_free_cost(const PlanDev& pl, int64_t B, const double* df, cons
 
 hipError_t launch_time_free_optimize(const PlanDev& pl, int64_t B, const double* df, double* dp,
                                      double* times, const mtg_time_params& p, int max_evals,
-                                     double* cost, int32_t* evals, int32_t* status,
-                                     hipStream_t st) {
+                                     double* cost, int32_t* evals, int32_t* result,
+                                     int32_t* status, hipStream_t st) {
+  if (p.optimizer == 1) {
+    MTG_FREE_DISPATCH(time_free_sbplx_n, pl, B, df, dp, times, p, max_evals, cost, evals, result,
+                      status, st)
+  }
   MTG_FREE_DISPATCH(time_free_opt_n, pl, B, df, dp, times, p, max_evals, cost, evals, status, st)
 }
 

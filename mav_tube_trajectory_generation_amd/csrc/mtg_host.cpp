@@ -796,24 +796,36 @@ int mtg_free_cost(const mtg_plan* plan, int64_t B, const double* fixed_vals,
                                         static_cast<hipStream_t>(stream)));
 }
 
-int mtg_time_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
-                           double* free_io, double* times_io, const mtg_time_params* params,
-                           int max_evals, double* cost, int32_t* evals, int32_t* status,
-                           void* stream) {
+int mtg_time_free_optimize_ex(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                              double* free_io, double* times_io, const mtg_time_params* params,
+                              int max_evals, double* cost, int32_t* evals, int32_t* result,
+                              int32_t* status, void* stream) {
   clear_stale_error();
   if (!plan || !params || B < 0 || B > 0x7fffffff || !times_io || max_evals < 1)
     return MTG_ERR_INVALID_ARG;
   if ((plan->dev.nf > 0 && !fixed_vals) || plan->dev.np < 1 || !free_io)
     return MTG_ERR_INVALID_ARG;
-  if (!(params->increment > 0)) return MTG_ERR_INVALID_ARG;
+  if (params->optimizer != 0 && params->optimizer != 1) return MTG_ERR_INVALID_ARG;
+  if (params->optimizer == 0 && !(params->increment > 0)) return MTG_ERR_INVALID_ARG;
   if (!valid_soft(plan, params)) return MTG_ERR_INVALID_ARG;
-  if (mtg::free_lds_bytes(plan->dev.N, plan->dev.S, plan->dev.D, plan->dev.np,
-                          params->n_soft > 0) > static_cast<size_t>(mtg::kMaxLdsBytes))
-    return MTG_ERR_UNSUPPORTED;
+  const bool soft = params->n_soft > 0;
+  const PlanDev& pl = plan->dev;
+  const size_t lds = params->optimizer == 1
+                         ? mtg::free_sbplx_lds_bytes(pl.N, pl.S, pl.D, pl.np, soft)
+                         : mtg::free_lds_bytes(pl.N, pl.S, pl.D, pl.np, soft);
+  if (lds > static_cast<size_t>(mtg::kMaxLdsBytes)) return MTG_ERR_UNSUPPORTED;
   if (B == 0) return MTG_OK;
-  return from_hip(mtg::launch_time_free_optimize(plan->dev, B, fixed_vals, free_io, times_io,
-                                                 *params, max_evals, cost, evals, status,
+  return from_hip(mtg::launch_time_free_optimize(pl, B, fixed_vals, free_io, times_io, *params,
+                                                 max_evals, cost, evals, result, status,
                                                  static_cast<hipStream_t>(stream)));
+}
+
+int mtg_time_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
+                           double* free_io, double* times_io, const mtg_time_params* params,
+                           int max_evals, double* cost, int32_t* evals, int32_t* status,
+                           void* stream) {
+  return mtg_time_free_optimize_ex(plan, B, fixed_vals, free_io, times_io, params, max_evals,
+                                   cost, evals, nullptr, status, stream);
 }
 
 int mtg_free_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,

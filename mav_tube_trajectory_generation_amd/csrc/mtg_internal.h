@@ -107,11 +107,13 @@ hipError_t launch_free_optimize(const PlanDev& pl, int64_t B, const double* df, 
                                 const double* times, const double* lower, const double* upper,
                                 const mtg_time_params& p, int max_evals, double* cost,
                                 int32_t* evals, int32_t* status, hipStream_t st);
+// p.optimizer 1: LN_SBPLX over [T; d_p] (result: nlopt_result codes).
 hipError_t launch_time_free_optimize(const PlanDev& pl, int64_t B, const double* df, double* dp,
                                      double* times, const mtg_time_params& p, int max_evals,
-                                     double* cost, int32_t* evals, int32_t* status,
-                                     hipStream_t st);
+                                     double* cost, int32_t* evals, int32_t* result,
+                                     int32_t* status, hipStream_t st);
 size_t free_lds_bytes(int N, int S, int D, int np, bool soft);
+size_t free_sbplx_lds_bytes(int N, int S, int D, int np, bool soft);
 inline bool use_std_kernel(const PlanDev& pl) {
   return pl.std_pattern && pl.kernel != MTG_KERNEL_GENERIC;
 }

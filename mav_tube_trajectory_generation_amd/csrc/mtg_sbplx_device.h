@@ -6,11 +6,15 @@
 // ftol_abs = f_abs, maxeval = max_iterations) and driven by optimizeTime
 // (:332-397: initial step initial_stepsize_rel T0, bounds [0.1, 2 T0]).
 //
-// The time kernels (mtg_time_std.hip, mtg_kernels.hip) evaluate the
-// objective at one call site in a loop; this machine decides the next point.
-// Its state lives in LDS and lane 0 advances it: init() sets the first point
-// (the start), resume(f) takes the value of the point it asked for and
-// writes the next one into T (or sets done).  The control flow is NLopt's
+// The time kernels (mtg_time_std.hip, mtg_kernels.hip), the free-derivative
+// and time kernel (mtg_free.hip) and the tube-QCQP time optimiser
+// (mtg_tube_time.hip) evaluate the objective at one call site in a loop; this
+// machine decides the next point.  Its state (state_bytes(n): a fixed part
+// plus six n-vectors and the permutation) lives in LDS, or in the caller's
+// global workspace for the tube optimiser, and one lane advances it:
+// init() / init_box() set the first point (the start), resume(f) takes the
+// value of the point it asked for and writes the next one into T (or sets
+// done).  The control flow is NLopt's
 // (sbplx.c, nldrmd.c) unrolled into resume states; the CPU restatement it is
 // checked against evaluation for evaluation is oracle/orc_sbplx.cpp
 // (tests/test_time_sbplx_gpu.py).  Tie rules as the oracle: simplex order
@@ -121,9 +125,12 @@ struct Machine {
   // Common tail of init / init_box.  NLopt refuses a start outside its
   // bounds (or lb > ub) before the first evaluation (nlopt_optimize:
   // NLOPT_INVALID_ARGS, which nlopt::opt::optimize throws and optimizeTime
-  // turns into nlopt::FAILURE, nonlinear_impl:389-394): the machine is then
-  // done at once with result kFailure, no evaluation, x = x0, minf NaN.  The
-  // caller checks `done` before its first evaluation.
+  // turns into nlopt::FAILURE, nonlinear_impl:389-394), and a zero initial
+  // step (nlopt_set_initial_step, thrown at set_initial_step, :376 / :682):
+  // the machine is then done at once with result kFailure, no evaluation,
+  // x = x0, minf NaN.  The caller checks `done` before its first evaluation.
+  // start() can also be called directly after the caller has filled n, x,
+  // lb, ub and xstep (e.g. by all lanes of a wave).
   __device__ void start(int maxeval, double ftol_rel, double ftol_abs) {
     const int n = s->n;
     s->maxeval = maxeval;
@@ -133,6 +140,7 @@ struct Machine {
     for (int i = 0; i < n; ++i) {
       dx()[i] = 0.0;
       ok = ok && !(lb()[i] > ub()[i] || x()[i] < lb()[i] || x()[i] > ub()[i]);
+      ok = ok && xstep()[i] != 0.0;  // nlopt_set_initial_step: "zero step size"
     }
     s->nevals = 0;
     s->done = 0;
@@ -149,9 +157,11 @@ struct Machine {
   __device__ double* pp(int i) { return &s->pts[i][1]; }
 
   // The full point for the subspace point xsub: x with the subspace
-  // coordinates replaced (sbplx's subspace_func).
+  // coordinates replaced (sbplx's subspace_func).  T equals x outside the
+  // current subspace at every request (x changes only in nm_return, which
+  // writes the subspace's final coordinates into T as well), so only the
+  // subspace's ns <= 5 coordinates are written, not all n.
   __device__ void request(const double* xsub, double* T, int next) {
-    for (int j = 0; j < s->n; ++j) T[j] = x()[j];
     for (int k = 0; k < s->ns; ++k) T[p()[s->is + k]] = xsub[k];
     s->pc = next;
   }
@@ -175,9 +185,13 @@ struct Machine {
   // The subspace solver returned `code`: write its best point back, then
   // the next subspace, the sweep's termination tests and step update.
   // Returns true when the machine continues (pc set), false when finished.
-  __device__ void nm_return(int code) {
+  __device__ void nm_return(int code, double* T) {
     if (s->fdiff > s->fdiff_max) s->fdiff_max = s->fdiff;
-    for (int k = 0; k < s->ns; ++k) x()[p()[s->is + k]] = s->xs[k];
+    for (int k = 0; k < s->ns; ++k) {
+      const int q = p()[s->is + k];
+      x()[q] = s->xs[k];
+      T[q] = s->xs[k];  // keeps T == x outside the next subspace (request)
+    }
     if (code == kFailure) return finish(kXtol);
     if (code != kXtol) return finish(code);
     if (!s->last) {
@@ -312,7 +326,7 @@ struct Machine {
             }
             pt[k] = v;
             if (close_to(v, xk)) {
-              nm_return(kFailure);
+              nm_return(kFailure, T);
               if (s->done) return;
               break;
             }
@@ -325,7 +339,7 @@ struct Machine {
         case kNmInitGot: {
           const int k = s->k;
           pf(k + 1) = f;
-          if (check_eval(pp(k + 1), f)) return nm_return(kMaxEval);
+          if (check_eval(pp(k + 1), f)) return nm_return(kMaxEval, T);
           s->k = k + 1;
           s->pc = kNmInit;
           break;
@@ -355,12 +369,12 @@ struct Machine {
           double diam = 0.0;
           for (int j = 0; j < m; ++j) diam += fabs(xl[j] - xh[j]);
           if (diam < kPsi * s->init_diam) {
-            nm_return(kXtol);
+            nm_return(kXtol, T);
             if (s->done) return;
             break;
           }
           if (!reflect(m, s->xcur, s->c, kAlpha, xh, s->lbs, s->ubs)) {
-            nm_return(kXtol);
+            nm_return(kXtol, T);
             if (s->done) return;
             break;
           }
@@ -369,11 +383,11 @@ struct Machine {
         case kNmReflGot: {
           const int m = s->ns, lo = s->lo, hi = s->hi;
           s->fr = f;
-          if (check_eval(s->xcur, f)) return nm_return(kMaxEval);
+          if (check_eval(s->xcur, f)) return nm_return(kMaxEval, T);
           const double fr = f;
           if (fr < pf(lo)) {  // expansion
             if (!reflect(m, pp(hi), s->c, kGamma, pp(hi), s->lbs, s->ubs)) {
-              nm_return(kXtol);
+              nm_return(kXtol, T);
               if (s->done) return;
               break;
             }
@@ -391,7 +405,7 @@ struct Machine {
           // contraction: inside if fh <= fr, outside otherwise
           const double fh = pf(hi);
           if (!reflect(m, s->xcur, s->c, fh <= fr ? -kBeta : kBeta, pp(hi), s->lbs, s->ubs)) {
-            nm_return(kXtol);
+            nm_return(kXtol, T);
             if (s->done) return;
             break;
           }
@@ -399,7 +413,7 @@ struct Machine {
         }
         case kNmExpGot: {
           const int m = s->ns, hi = s->hi;
-          if (check_eval(pp(hi), f)) return nm_return(kMaxEval);
+          if (check_eval(pp(hi), f)) return nm_return(kMaxEval, T);
           if (f >= s->fr) {
             for (int j = 0; j < m; ++j) pp(hi)[j] = s->xcur[j];
             pf(hi) = s->fr;
@@ -411,7 +425,7 @@ struct Machine {
         }
         case kNmConGot: {
           const int m = s->ns, hi = s->hi;
-          if (check_eval(s->xcur, f)) return nm_return(kMaxEval);
+          if (check_eval(s->xcur, f)) return nm_return(kMaxEval, T);
           if (f < s->fr && f < pf(hi)) {
             for (int j = 0; j < m; ++j) pp(hi)[j] = s->xcur[j];
             pf(hi) = f;
@@ -432,7 +446,7 @@ struct Machine {
           }
           s->k = k;
           if (!reflect(m, pp(k), pp(lo), -kDelta, pp(k), s->lbs, s->ubs)) {
-            nm_return(kXtol);
+            nm_return(kXtol, T);
             if (s->done) return;
             break;
           }
@@ -441,7 +455,7 @@ struct Machine {
         case kNmShrGot: {
           const int k = s->k;
           pf(k) = f;
-          if (check_eval(pp(k), f)) return nm_return(kMaxEval);
+          if (check_eval(pp(k), f)) return nm_return(kMaxEval, T);
           s->k = k + 1;
           s->pc = kNmShrink;
           break;

@@ -562,7 +562,11 @@ struct Tube {
   // dead from the step update to the next direction).
   __device__ int mid() const { return nthr > kWave ? nv / 2 : nv - 1; }
 
-  __device__ void factor(int* fail, bool with_constraints) {
+  // reg > 0: the retry after a non-positive pivot (ipm()): every block's
+  // S_a lanes scale their diagonal entry by 1 + reg (|S_ii| reg added), a
+  // diagonal regularisation of the block elimination (the oracle adds
+  // reg K_ii to its dense K; both steps converge to the same optimum).
+  __device__ void factor(int* fail, bool with_constraints, double reg = 0.0) {
     const double* Gcp = sm + L->Gc;
     int bad = 0;
     unsigned long long tf = 0;
@@ -680,6 +684,10 @@ struct Tube {
       if (sb) schur(sm + L->Wb, sm + L->Li + (a + 1) * kTri);
 #pragma unroll
       for (int i = 0; i < BS; ++i) col[i] = fma(rows_sum(acc[i]), r0, col[i]);
+      if (reg > 0.0) {  // workgroup-uniform: the retry only
+#pragma unroll
+        for (int i = 0; i < BS; ++i) col[i] = fma(reg * r0 * is_zero(i - cc), fabs(col[i]), col[i]);
+      }
       // Forward elimination (below the pivot) on all columns at once; the
       // pivot column is broadcast with v_readlane.
       MTG_TACC(222, tf);
@@ -990,21 +998,31 @@ struct Tube {
   // with the dual residual within 1e5 * tol instead, not converged
   // (status 1).
   static constexpr double kComplFloor = 0.01;
+  static constexpr double kKktReg = 1e-10;
   __device__ int ipm(double tol, int max_iter, int* status, int* bad) {
     int* fail = bad + 1;
     if (tid == 0) *fail = 0;
     __syncthreads();
-    // Unconstrained start: P x = -q.
+    // Unconstrained start: P x = -q.  Where P is numerically singular (long
+    // segments: with T = 20 s a vertex's position barely changes the snap
+    // cost, T^-7, and P's equilibrated spectrum reaches -1e-12) the start is
+    // the tube axis instead: every intermediate vertex at its position, its
+    // higher derivatives zero, so every control point sits on the vertex,
+    // strictly inside its tubes and sphere (the oracle's rule).  The
+    // constrained Newton systems add the constraints' curvature.
     factor(fail, false);
     __syncthreads();
     if (*fail) {
-      if (tid == 0) *bad |= 2;
-      *status = 2;
-      return 0;
+      for (int idx = tid; idx < nv * BS; idx += nthr) {
+        const int a = idx / BS, d = (idx / M) % 3, m = idx % M;
+        sm[L->x + idx] = m == 0 ? sm[L->pos + (a + 1) * 3 + d] : 0.0;
+      }
+      __syncthreads();
+    } else {
+      for (int idx = tid; idx < nv * BS; idx += nthr) sm[L->rhs + idx] = -sm[L->q + idx];
+      __syncthreads();
+      solve(L->rhs, L->x);
     }
-    for (int idx = tid; idx < nv * BS; idx += nthr) sm[L->rhs + idx] = -sm[L->q + idx];
-    __syncthreads();
-    solve(L->rhs, L->x);
     control_points(sm + L->x, L->cp);
     __syncthreads();
     for (int k = tid; k < nc; k += nthr) {
@@ -1089,10 +1107,19 @@ struct Tube {
       const int brk = near ? 3 : (stalled ? 1 : 2);
       MTG_TACC(200, tl);
       MTG_TACC(201, tl);
-      if (tid == 0) *fail = 0;
-      __syncthreads();
-      factor(fail, true);
-      __syncthreads();
+      // A non-positive pivot (lam / s ~ 1e12 on active constraints swamps
+      // the rest of K in rounding) is retried once on K + kKktReg diag(K);
+      // the regularised Newton step still converges to the same optimum,
+      // where stopping left 16 % of the points of the time optimiser's box
+      // [0.1, 2 T0] without a value (the oracle's rule).  One call site, so
+      // the factorisation is instantiated once.
+      for (double reg = 0.0;; reg = kKktReg) {
+        if (tid == 0) *fail = 0;
+        __syncthreads();
+        factor(fail, true, reg);
+        __syncthreads();
+        if (!*fail || reg > 0.0) break;
+      }
       MTG_TACC(202, tl);
       if (*fail) {
         *status = brk;

@@ -859,6 +859,7 @@ struct TubeProblem {
   // replacing MSK_optimizetrm (qcqp_impl:700-712).  Status 0 converged,
   // 1 iteration cap / stalled, 2 breakdown, 3 near-optimal at a breakdown.
   static constexpr double kComplFloor = 0.01;
+  static constexpr double kKktReg = 1e-10;
   int solveIPM(double tol, int max_iter, std::vector<double>* xout, int* iters) {
     Mat P;
     std::vector<double> q;
@@ -866,12 +867,26 @@ struct TubeProblem {
     const int n = npk;
     const int m = static_cast<int>(cons.size());
     // Start from the unconstrained minimiser P x = -q.
+    // Where P is numerically singular (long segments: with T = 20 s a
+    // vertex's position barely changes the snap cost, T^-7) the start is the
+    // tube axis: every intermediate vertex at its position, its higher
+    // derivatives zero (control points on the vertex, strictly inside every
+    // tube and sphere).  The device kernel uses the same rule.
     std::vector<double> x(n, 0.0);
     {
       Mat L = P;
-      if (!cholesky(&L)) return -20;
-      for (int i = 0; i < n; ++i) x[i] = -q[i];
-      cholesky_solve(L, &x);
+      if (cholesky(&L)) {
+        for (int i = 0; i < n; ++i) x[i] = -q[i];
+        cholesky_solve(L, &x);
+      } else {
+        const int h = N / 2;
+        for (int d = 0; d < D; ++d)
+          for (int v = 1; v < S; ++v) {
+            std::vector<double> pv;
+            lp.vertices[v].get(0, &pv);
+            x[d * (S - 1) * h + (v - 1) * h] = pv[d];
+          }
+      }
     }
     std::vector<double> s(m), lam(m, 1.0), g(m);
     for (int k = 0; k < m; ++k) {
@@ -936,9 +951,21 @@ struct TubeProblem {
             Kmat(c.supp[u], c.supp[v]) +=
                 lam[k] * c.quad[static_cast<size_t>(u) * ms + v] + w * a[k][u] * a[k][v];
       }
-      if (!cholesky(&Kmat)) {
-        status = brk;
-        break;
+      // A non-positive pivot (lam / s ~ 1e12 on active constraints swamps
+      // the rest of K in rounding) is retried once on K + kKktReg diag(K);
+      // the regularised Newton step still converges (to the same optimum),
+      // where stopping left 16 % of the points of the time optimiser's box
+      // [0.1, 2 T0] without a value (the device kernel uses the same rule).
+      {
+        Mat K0 = Kmat;
+        if (!cholesky(&Kmat)) {
+          for (int i = 0; i < n; ++i) K0(i, i) += kKktReg * K0(i, i);
+          Kmat = K0;
+          if (!cholesky(&Kmat)) {
+            status = brk;
+            break;
+          }
+        }
       }
       auto direction = [&](const std::vector<double>& rc, std::vector<double>* dx,
                            std::vector<double>* dl, std::vector<double>* ds) {

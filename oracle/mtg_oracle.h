@@ -289,6 +289,16 @@ int orc_time_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mas
                            double soft_weight, double soft_maximum_cost, int max_evals,
                            double* cost, int* evals);
 
+// optimizeTimeAndFreeConstraints with LN_SBPLX over [T; d_p] (the reference's
+// default algorithm; see mtg_oracle.cpp).  dp_io: D x np, times_io: S.
+int orc_time_free_optimize_sbplx(int N, int D, int r, int S, int K, const uint8_t* mask,
+                                 const double* vals, double* dp_io, double* times_io,
+                                 double time_penalty, int n_soft, const int* soft_derivatives,
+                                 const double* soft_limits, double soft_weight,
+                                 double soft_maximum_cost, int max_evals, double f_rel,
+                                 double f_abs, double step_rel, double* cost, int* evals,
+                                 int* result, double* history);
+
 // Collision cost of getCostAndGradientCollision (nonlinear_impl:1609-1780)
 // over a dense occupancy grid (see mtg_oracle.cpp).  dp: D x np (D = 3);
 // params: res, min_bound[3], max_bound[3], epsilon, robot_radius,

@@ -596,6 +596,36 @@ def time_free_optimize(N, r, vertices, times, dp0, max_evals, time_penalty=500.0
     return t, dp, float(cost[0]), evals.value
 
 
+def time_free_optimize_sbplx(N, r, vertices, times, dp0, max_evals, time_penalty=500.0,
+                             f_rel=0.05, f_abs=-1.0, step_rel=0.1, soft=None, soft_weight=100.0,
+                             soft_maximum_cost=1.0e12):
+    """orc_time_free_optimize_sbplx: optimizeTimeAndFreeConstraints with
+    LN_SBPLX over [T; d_p].  Returns dict(times, dp, cost, evals, result,
+    history [evals, S + D np])."""
+    S, D, K = vertices.S, vertices.D, vertices.K
+    t = np.ascontiguousarray(times, dtype=np.float64).copy()
+    dp = np.ascontiguousarray(dp0, dtype=np.float64).copy()
+    n = S + dp.size
+    cost = np.zeros(1)
+    evals = ctypes.c_int()
+    result = ctypes.c_int()
+    hist = np.zeros((max_evals, n))
+    ns, der, lim = _soft_arrays(soft)
+    L = lib()
+    L.orc_time_free_optimize_sbplx.argtypes = [ctypes.c_int] * 5 + [
+        _u8p, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int, _ip, _dp, ctypes.c_double,
+        ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp,
+        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), _dp]
+    _check(L.orc_time_free_optimize_sbplx(N, D, r, S, K, vertices.mask.ctypes.data_as(_u8p),
+                                          _d(vertices.vals), _d(dp), _d(t), time_penalty, ns,
+                                          der.ctypes.data_as(_ip), _d(lim), soft_weight,
+                                          soft_maximum_cost, max_evals, f_rel, f_abs, step_rel,
+                                          _d(cost), ctypes.byref(evals), ctypes.byref(result),
+                                          _d(hist)), "time_free_optimize_sbplx")
+    return dict(times=t, dp=dp, cost=float(cost[0]), evals=evals.value, result=result.value,
+                history=hist[:evals.value])
+
+
 def collision_cost(N, r, vertices, times, dp, occupancy, params, box_side=20):
     """orc_collision_cost: getCostAndGradientCollision on a dense grid.
     occupancy: float32 [nz, ny, nx]; params: dict of map_resolution,

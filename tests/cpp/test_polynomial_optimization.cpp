@@ -1406,34 +1406,39 @@ TEST(gpu, CollisionCostMatchesOracle) {
 }
 
 // kOptimizeFreeConstraintsAndTime (optimizeTimeAndFreeConstraints,
-// nonlinear_impl:610-706): the shim runs mtg_time_free_optimize from the tube
-// QCQP start; the same steps as the oracle port, a lower objective, bounds
-// held.
-TEST(gpu, OptimizeTimeAndFreeConstraints) {
+// nonlinear_impl:610-706) from the tube QCQP start: with the default
+// LN_SBPLX the shim runs the device Subplex over all S + 3 n_p variables
+// (mtg_time_free_optimize_ex, optimizer 1) and follows the oracle's Subplex
+// (orc_time_free_optimize_sbplx); with another algorithm the
+// block-alternating descent and the oracle port of it.  The objective does
+// not rise and the bounds hold.
+void runTimeAndFreeConstraints(nlopt::algorithm algo) {
   const Vertex::Vector vs = mainCppVertices();
   const std::vector<double> times = estimateSegmentTimes(vs, 2.0, 2.0);
   NonlinearOptimizationParameters p;
   p.objective = NonlinearOptimizationParameters::kOptimizeFreeConstraintsAndTime;
   p.weights.w_c = 0.0;
-  p.max_iterations = 30;
+  p.algorithm = algo;
+  p.max_iterations = algo == nlopt::LN_SBPLX ? 120 : 30;
   PolynomialOptimizationNonLinear<10> opt(3, p);
   opt.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(4, {0.15, 0.15}), 4);
   EXPECT_TRUE(opt.solveQCQP() == 0);
   std::vector<VectorXd> fc;
   opt.getConstrainedOptimizationRef().getFreeConstraints(&fc);
   const double J0 = opt.evaluateTimeAndFreeConstraintsCost(times, fc);
-  EXPECT_TRUE(opt.optimize() > 0);
+  const int res = opt.optimize();
+  EXPECT_TRUE(res > 0);
   const OptimizationInfo info = opt.getOptimizationInfo();
-  EXPECT_TRUE(info.n_iterations >= 2 && info.n_iterations <= 30);
+  EXPECT_TRUE(info.n_iterations >= 2 && info.n_iterations <= p.max_iterations);
   std::vector<double> t1;
   opt.getConstrainedOptimizationRef().getSegmentTimes(&t1);
   std::vector<VectorXd> f1;
   opt.getConstrainedOptimizationRef().getFreeConstraints(&f1);
   const double J1 = opt.evaluateTimeAndFreeConstraintsCost(t1, f1);
-  EXPECT_TRUE(J1 < J0);
+  EXPECT_LE(J1, J0);
   EXPECT_LE(relErr(J1, info.cost_trajectory + info.cost_time), 1e-9);
   for (size_t i = 0; i < t1.size(); ++i) EXPECT_TRUE(t1[i] >= 0.1 && t1[i] <= 2.0 * times[i]);
-  // Oracle port from the same start.
+  // Oracle from the same start.
   Dense d = toDense(vs, 5);
   for (int v = 1; v < d.S; ++v)
     for (int k = 0; k < 5; ++k) d.mask[v * 5 + k] = 0;
@@ -1441,13 +1446,30 @@ TEST(gpu, OptimizeTimeAndFreeConstraints) {
   for (const VectorXd& v : fc)
     for (long i = 0; i < v.size(); ++i) x.push_back(v[i]);
   double oJ = 0.0;
-  int oev = 0;
-  EXPECT_TRUE(orc_time_free_optimize(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), x.data(),
-                                     ot.data(), p.time_penalty, p.increment_time, 0, nullptr,
-                                     nullptr, 100.0, 1e12, 30, &oJ, &oev) == 0);
+  int oev = 0, ores = 0;
+  if (algo == nlopt::LN_SBPLX) {
+    EXPECT_TRUE(orc_time_free_optimize_sbplx(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(),
+                                             x.data(), ot.data(), p.time_penalty, 0, nullptr,
+                                             nullptr, 100.0, 1e12, p.max_iterations, p.f_rel,
+                                             p.f_abs, p.initial_stepsize_rel, &oJ, &oev, &ores,
+                                             nullptr) == 0);
+    EXPECT_TRUE(ores == res);
+  } else {
+    EXPECT_TRUE(orc_time_free_optimize(10, 3, 4, 4, 5, d.mask.data(), d.vals.data(), x.data(),
+                                       ot.data(), p.time_penalty, p.increment_time, 0, nullptr,
+                                       nullptr, 100.0, 1e12, 30, &oJ, &oev) == 0);
+  }
+  std::fprintf(stderr, "  free+time (%s): evals %d (oracle %d), J %.12g (oracle %.12g)\n",
+               algo == nlopt::LN_SBPLX ? "LN_SBPLX" : "descent",
+               static_cast<int>(info.n_iterations), oev, J1, oJ);
   EXPECT_TRUE(oev == info.n_iterations);
   EXPECT_LE(relErr(J1, oJ), 1e-6);
   EXPECT_LE(relErr(t1, ot), 1e-6);
+}
+
+TEST(gpu, OptimizeTimeAndFreeConstraints) { runTimeAndFreeConstraints(nlopt::LN_SBPLX); }
+TEST(gpu, OptimizeTimeAndFreeConstraintsDescent) {
+  runTimeAndFreeConstraints(nlopt::LN_BOBYQA);
 }
 
 // The reference demo (src/main.cpp:15-126): kOptimizeFreeConstraintsAndCollision

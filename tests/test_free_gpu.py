@@ -203,3 +203,74 @@ def test_time_free_optimize_vs_oracle(ctx, dev, oracle, pattern):
             assert np.max(np.abs(dp - dpo) / scale) <= 1e-5
             agree += 1
     assert agree >= 5, agree
+
+
+def _sbplx_batch(ctx, dev, oracle, S, pattern, seeds, E, zero=None):
+    vs, ts, d0s, dfs = [], [], [], []
+    for seed in seeds:
+        v, times = _problem(oracle, S, 3, seed, pattern)
+        plan, df = _plan(ctx, v)
+        vs.append(v)
+        ts.append(times)
+        d0s.append(oracle.linear_solve(N, R, v, times)["dp"])
+        dfs.append(df)
+    d0 = np.stack(d0s)
+    if zero is not None:
+        d0[zero] = 0.0
+    times = np.stack(ts)
+    out = plan.time_free_optimize(_T(dev, np.stack(dfs)), _T(dev, d0), _T(dev, times),
+                                  max_evals=E, optimizer="sbplx")
+    torch.cuda.synchronize()
+    return plan, vs, times, d0, {k: v.cpu().numpy() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("S,E", [(5, 250), (10, 400)])
+def test_time_free_sbplx_vs_oracle(ctx, dev, oracle, S, E):
+    """kOptimizeFreeConstraintsAndTime on the reference's own algorithm:
+    LN_SBPLX over x = [T; d_p] (optimizeTimeAndFreeConstraints,
+    nonlinear_impl:610-706; objectiveFunctionTimeAndConstraints, :947-1019)
+    on the fork's tube pattern (S + 3 (S-1) M variables: 65 at S = 5, 145 at
+    S = 10), from the linear solve's d_p.  The device's Subplex and the
+    oracle's restatement (orc_time_free_optimize_sbplx) take the same path on
+    all but one of 8 trajectories: evaluation count, nlopt_result, final times
+    and d_p (1e-6), cost (1e-6).  Every trajectory keeps its bounds and the
+    budget, and its cost is the objective at the returned point, no higher
+    than at the start.  NLopt itself is absent (parity unpinned vs NLopt)."""
+    seeds = range(720, 728)
+    plan, vs, times, d0, out = _sbplx_batch(ctx, dev, oracle, S, "tube", seeds, E)
+    assert (out["status"] == 0).all()
+    assert set(np.unique(out["result"])) <= {3, 4, 5}
+    assert np.all((out["evals"] >= 1) & (out["evals"] <= E))
+    T, dp = out["times"], out["free"]
+    assert np.all(T >= 0.1 - 1e-15) and np.all(T <= 2 * times + 1e-12)
+    assert np.all(np.abs(dp) <= 2 * np.abs(d0) + 1e-12)
+    agree = 0
+    for b, v in enumerate(vs):
+        J0, _ = oracle.free_cost(N, R, v, times[b], d0[b], mode=1)
+        assert out["cost"][b] <= J0 * (1 + 1e-12), b
+        Jc, _ = oracle.free_cost(N, R, v, T[b], dp[b], mode=1)
+        assert rel_err(out["cost"][b], Jc) <= 1e-9, b
+        r = oracle.time_free_optimize_sbplx(N, R, v, times[b], d0[b], E)
+        if (r["evals"] == out["evals"][b] and r["result"] == out["result"][b]
+                and np.max(np.abs(T[b] - r["times"]) / r["times"]) <= 1e-6):
+            assert rel_err(out["cost"][b], r["cost"]) <= 1e-6, b
+            scale = np.maximum(np.abs(r["dp"]), 1e-6 * np.max(np.abs(r["dp"])))
+            assert np.max(np.abs(dp[b] - r["dp"]) / scale) <= 1e-5, b
+            agree += 1
+    assert agree >= len(vs) - 1, agree
+
+
+def test_time_free_sbplx_zero_start_entry(ctx, dev, oracle):
+    """A zero entry of x0 is a zero initial step, which NLopt rejects before
+    optimising (nlopt_set_initial_step; the reference returns nlopt::FAILURE,
+    nonlinear_impl:681-691): result -1, no evaluation, x unchanged, on the
+    device and in the oracle.  The other trajectories run normally."""
+    S, E = 4, 60
+    plan, vs, times, d0, out = _sbplx_batch(ctx, dev, oracle, S, "tube", range(740, 743), E,
+                                            zero=(1, 2, 3))
+    assert out["result"][1] == -1 and out["evals"][1] == 0 and np.isnan(out["cost"][1])
+    assert np.array_equal(out["times"][1], times[1]) and np.array_equal(out["free"][1], d0[1])
+    r = oracle.time_free_optimize_sbplx(N, R, vs[1], times[1], d0[1], E)
+    assert r["result"] == -1 and r["evals"] == 0 and np.array_equal(r["dp"], d0[1])
+    for b in (0, 2):
+        assert out["result"][b] in (3, 4, 5) and out["evals"][b] >= 1
