@@ -2418,6 +2418,66 @@ int orc_free_optimize(int N, int D, int r, int S, int K, const uint8_t* mask,
   return 0;
 }
 
+// optimizeTimeAndFreeConstraints (nonlinear_impl:610-706) with the
+// reference's default LN_SBPLX (orc_sbplx.cpp) over x = [T; d_p] (d_p
+// dimension-major, :653-662) on objectiveFunctionTimeAndConstraints
+// (:947-1019, freeCostImpl mode 1: no re-solve): bounds T in [0.1, 2 |T0|],
+// d_p in [-2 |d0|, 2 |d0|], initial steps step_rel |x0| (:664-675), maxeval
+// max_evals, ftol f_rel / f_abs.  NLopt rejects a zero initial step
+// (nlopt_set_initial_step) before optimising, which the reference returns as
+// nlopt::FAILURE (:681-691): result -1, no evaluation, x unchanged.
+// dp_io: D x np, times_io: S; out NLopt's x; history (nullable, max_evals x
+// (S + D np)) the evaluated points.
+int orc_time_free_optimize_sbplx(int N, int D, int r, int S, int K, const uint8_t* mask,
+                                 const double* vals, double* dp_io, double* times_io,
+                                 double time_penalty, int n_soft, const int* soft_derivatives,
+                                 const double* soft_limits, double soft_weight,
+                                 double soft_maximum_cost, int max_evals, double f_rel,
+                                 double f_abs, double step_rel, double* cost, int* evals,
+                                 int* result, double* history) {
+  if (!dp_io || !times_io || max_evals < 1) return -1;
+  LinearProblem lp;
+  int rc = setupLinear(N, D, r, S, K, mask, vals, times_io, &lp);
+  if (rc) return rc;
+  const int np = lp.np, n = S + D * np;
+  if (np < 1) return -1;
+  const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
+  std::vector<double> x(n), lb(n), ub(n), step(n);
+  for (int i = 0; i < S; ++i) x[i] = times_io[i];
+  for (int i = 0; i < D * np; ++i) x[S + i] = dp_io[i];
+  for (int i = 0; i < n; ++i) {
+    const double a = std::fabs(x[i]);
+    step[i] = step_rel * a;
+    lb[i] = i < S ? 0.1 : -2.0 * a;
+    ub[i] = 2.0 * a;
+  }
+  int k = 0;
+  std::vector<double> t(S);
+  auto objective = [&](const double* xp) {
+    if (history && k < max_evals)
+      std::memcpy(history + static_cast<size_t>(k) * n, xp, sizeof(double) * n);
+    ++k;
+    t.assign(xp, xp + S);
+    lp.updateSegmentTimes(t);
+    double J = 0.0;
+    freeCostImpl(lp, xp + S, 1, time_penalty, n_soft > 0 ? &soft : nullptr, &J, nullptr);
+    return J;
+  };
+  double minf = std::numeric_limits<double>::quiet_NaN();
+  int nev = 0, res = kSbplxFailure;
+  bool zero_step = false;
+  for (double v : step) zero_step = zero_step || v == 0.0;
+  if (!zero_step)
+    res = orc_sbplx_run(n, objective, lb.data(), ub.data(), x.data(), &minf, step.data(),
+                        max_evals, f_rel, f_abs, &nev);
+  for (int i = 0; i < S; ++i) times_io[i] = x[i];
+  for (int i = 0; i < D * np; ++i) dp_io[i] = x[S + i];
+  if (cost) *cost = minf;
+  if (evals) *evals = nev;
+  if (result) *result = res;
+  return 0;
+}
+
 // The mtg_time_free_optimize algorithm (time_free_optimize_kernel) restated on
 // the oracle objective: optimizeTimeAndFreeConstraints (nonlinear_impl:
 // 610-706) with objectiveFunctionTimeAndConstraints (:947-1019, mode 1 of
