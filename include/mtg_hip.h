@@ -53,12 +53,21 @@ enum {
   MTG_ERR_UNSUPPORTED = -4,  /* size beyond the kernels' LDS budget */
   MTG_ERR_NUMERIC = -5       /* at least one trajectory failed (see status) */
 };
+/* HIP error state: an entry point that launches device work clears the
+ * thread's pending HIP error (hipGetLastError) before it launches, so that a
+ * failed call made earlier by the caller or another library is not reported
+ * as this call's MTG_ERR_HIP; check your own HIP calls before calling one of
+ * these.  Getters, size queries (*_workspace_bytes, mtg_coll_field_bytes,
+ * mtg_tube_num_constraints), mtg_generate_random_problems and the create /
+ * destroy calls leave the pending error untouched. */
 
 /* Per-trajectory status codes written by batched kernels. */
 enum {
   MTG_TRAJ_OK = 0,
   MTG_TRAJ_BAD_TIME = 1,     /* a segment time <= 0 (linear_impl:296) */
-  MTG_TRAJ_NOT_SPD = 2,      /* free-derivative system not positive definite */
+  MTG_TRAJ_NOT_SPD = 2,      /* free-derivative system not positive definite
+                                (tube QCQP: its KKT system broke down twice,
+                                plain and regularised, away from the optimum) */
   MTG_TRAJ_NOT_CONVERGED = 3, /* interior-point solve hit its iteration cap */
   MTG_TRAJ_NEAR_OPTIMAL = 4   /* interior-point solve stopped where its KKT
                                  system broke down, every residual within
@@ -146,11 +155,12 @@ int mtg_linear_solve(const mtg_plan* plan, int64_t B, const double* fixed_vals,
 
 /* Same, host pointers in and out.  Used by the C++ single-trajectory shim
  * PolynomialOptimization<N>::solveLinear().  The plan keeps persistent
- * staging (pinned host + device buffers and a stream of its own, created on
- * first use, grown when a larger B arrives): a steady-state call is one
- * host-to-device copy, one launch and one device-to-host copy on that
- * stream, then a wait on that stream only (no allocation, no device-wide
- * synchronisation).  Calls on one plan are serialised (the staging is
+ * staging (a pinned, device-mapped host buffer, a device buffer and a
+ * stream of its own, created on first use, grown when a larger B arrives): a
+ * steady-state call of up to 64 KB of inputs and outputs (a single
+ * trajectory) is one launch reading and writing the mapped host buffer, then
+ * a wait on that stream; larger calls add one host-to-device and one
+ * device-to-host copy.  No allocation, no device-wide synchronisation.  Calls on one plan are serialised (the staging is
  * shared); use separate plans for concurrent host threads. */
 int mtg_linear_solve_host(const mtg_plan* plan, int64_t B,
                           const double* fixed_vals, const double* times,
@@ -378,9 +388,13 @@ int mtg_time_free_optimize_ex(const mtg_plan* plan, int64_t B, const double* fix
  * primal-dual interior-point method (MOSEK in the reference), then recover
  * coefficients (qcqp_impl:777-785).  Outputs: x B x 3(S-1)M, coeffs
  * B x S x 3 x N, cost B (computeCost), iters B, status B (nullable except
- * coeffs).  Where a time is not positive (MTG_TRAJ_BAD_TIME) or the start
- * system is not positive definite (MTG_TRAJ_NOT_SPD with 0 iterations), x,
- * coeffs and cost are NaN.  B < 2^26 (one 64-lane workgroup per
+ * coeffs).  Where a time is not positive (MTG_TRAJ_BAD_TIME) x, coeffs and
+ * cost are NaN.  Where R_pp is numerically singular (very long segments) the
+ * interior-point method starts on the tube axis instead of at the
+ * unconstrained minimiser (intermediate vertices at their positions, higher
+ * derivatives zero); a KKT factorisation with a non-positive pivot is
+ * retried once with a 1e-10 relative diagonal regularisation before the
+ * solve stops (MTG_TRAJ_NOT_SPD when away from the optimum).  B < 2^26 (one 64-lane workgroup per
  * trajectory).
  */
 int mtg_tube_num_constraints(int N, int S);

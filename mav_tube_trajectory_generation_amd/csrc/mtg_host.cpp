@@ -22,16 +22,21 @@ struct mtg_ctx {
 };
 
 // Persistent staging of the host-memory entry point (mtg_linear_solve_host),
-// created on first use and grown on demand: a pinned host buffer, the same
-// layout on the device and a non-blocking stream of the plan's own, so a
-// steady-state call is one H2D copy, one launch and one D2H copy on that
-// stream, then a wait on that stream only (no allocation, no device-wide
-// synchronisation).  Layout (bytes, each part 256-aligned): inputs
+// created on first use and grown on demand: a pinned, device-mapped host
+// buffer, a device buffer of the same layout and a non-blocking stream of
+// the plan's own.  Small calls (the single-trajectory shim: up to
+// kZeroCopyBytes) run zero-copy: the kernel reads its inputs from and writes
+// its outputs to the mapped host buffer, so a steady-state call is one launch
+// and a wait on that stream.  Larger calls copy in and out by DMA (one H2D
+// copy, one launch, one D2H copy).  No allocation, no device-wide
+// synchronisation.  Layout (bytes, each part 256-aligned): inputs
 // [fixed_vals | times], outputs [coeffs | cost | free_vals | status].
+constexpr size_t kZeroCopyBytes = 64 * 1024;
 struct mtg_staging {
   std::mutex mu;
   hipStream_t stream = nullptr;
   char* host = nullptr;
+  char* hdev = nullptr;  // device address of the mapped host buffer
   char* dev = nullptr;
   size_t bytes = 0;
   ~mtg_staging() {
@@ -58,9 +63,11 @@ int from_hip(hipError_t e) { return e == hipSuccess ? MTG_OK : MTG_ERR_HIP; }
 
 // The launch helpers report hipGetLastError() after their launches, and the
 // runtime keeps the last error of ANY failed HIP call on this thread (the
-// caller's, or another library's) until it is read.  Every entry point
-// therefore clears that slot first, so a stale error is never returned as
-// this call's MTG_ERR_HIP.  Round 4's failed graph captures were exactly
+// caller's, or another library's) until it is read.  The entry points that
+// launch work (and so read that slot afterwards) clear it first, so a stale
+// error is never returned as this call's MTG_ERR_HIP; getters, size queries,
+// the host-only generator and the create / destroy calls (which check their
+// HIP calls' return values directly) leave the caller's pending error alone.  Round 4's failed graph captures were exactly
 // that: an experiment's event-record call failed inside the capture and the
 // next mtg_linear_solve reported it ("Graph capture").
 void clear_stale_error() { (void)hipGetLastError(); }
@@ -202,7 +209,6 @@ const char* mtg_status_string(int status) {
 int mtg_version(void) { return 100; }
 
 int mtg_ctx_create(int device, mtg_ctx** out) {
-  clear_stale_error();
   if (!out) return MTG_ERR_INVALID_ARG;
   *out = nullptr;
   int n = 0;
@@ -216,7 +222,6 @@ int mtg_ctx_create(int device, mtg_ctx** out) {
 }
 
 int mtg_ctx_destroy(mtg_ctx* ctx) {
-  clear_stale_error();
   if (!ctx) return MTG_ERR_INVALID_ARG;
   (void)hipSetDevice(ctx->device);
   for (auto& kv : ctx->tables) (void)hipFree(kv.second);
@@ -228,7 +233,6 @@ int mtg_ctx_device(const mtg_ctx* ctx) { return ctx ? ctx->device : MTG_ERR_INVA
 
 int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fixed_mask,
                     mtg_plan** out) {
-  clear_stale_error();
   if (!ctx || !out || !fixed_mask) return MTG_ERR_INVALID_ARG;
   *out = nullptr;
   if (!valid_N(N) || D < 1 || D > mtg::kMaxD || r < 0 || r > N / 2 - 1 || S < 1)
@@ -298,7 +302,6 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fix
 }
 
 int mtg_plan_destroy(mtg_plan* plan) {
-  clear_stale_error();
   if (!plan) return MTG_ERR_INVALID_ARG;
   (void)hipFree(plan->d_slots);
   (void)hipFree(plan->d_free_map);
@@ -308,7 +311,6 @@ int mtg_plan_destroy(mtg_plan* plan) {
 }
 
 int mtg_plan_set_kernel(mtg_plan* plan, int kernel) {
-  clear_stale_error();
   if (!plan || kernel < MTG_KERNEL_AUTO || kernel > MTG_KERNEL_LANE_PAIR)
     return MTG_ERR_INVALID_ARG;
   if (kernel == MTG_KERNEL_STANDARD && !plan->dev.std_pattern) return MTG_ERR_UNSUPPORTED;
@@ -322,20 +324,17 @@ int mtg_plan_set_kernel(mtg_plan* plan, int kernel) {
 }
 
 int mtg_plan_kernel(const mtg_plan* plan) {
-  clear_stale_error();
   if (!plan) return MTG_ERR_INVALID_ARG;
   if (plan->dev.kernel >= MTG_KERNEL_LANE) return plan->dev.kernel;
   return mtg::use_std_kernel(plan->dev) ? MTG_KERNEL_STANDARD : MTG_KERNEL_GENERIC;
 }
 
 int mtg_plan_kernel_for_batch(const mtg_plan* plan, int64_t B) {
-  clear_stale_error();
   if (!plan || B < 0) return MTG_ERR_INVALID_ARG;
   return mtg::linear_kernel_for_batch(plan->dev, B);
 }
 
 int mtg_plan_counts(const mtg_plan* plan, int* n_fixed, int* n_free) {
-  clear_stale_error();
   if (!plan) return MTG_ERR_INVALID_ARG;
   if (n_fixed) *n_fixed = plan->dev.nf;
   if (n_free) *n_free = plan->dev.np;
@@ -384,9 +383,11 @@ int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_v
   if (sg.bytes < total) {
     if (sg.host) (void)hipHostFree(sg.host);
     if (sg.dev) (void)hipFree(sg.dev);
-    sg.host = sg.dev = nullptr;
+    sg.host = sg.hdev = sg.dev = nullptr;
     sg.bytes = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&sg.host), total, hipHostMallocDefault) !=
+    if (hipHostMalloc(reinterpret_cast<void**>(&sg.host), total, hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&sg.hdev), sg.host, 0) !=
             hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&sg.dev), total) != hipSuccess)
       return MTG_ERR_HIP;
@@ -394,17 +395,20 @@ int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_v
   }
   if (nfv) std::memcpy(sg.host, fixed_vals, nfv * sizeof(double));
   std::memcpy(sg.host + o_t, times, nt * sizeof(double));
-  if (hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, sg.stream) != hipSuccess)
+  const bool zc = total <= kZeroCopyBytes;
+  char* base = zc ? sg.hdev : sg.dev;
+  if (!zc &&
+      hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, sg.stream) != hipSuccess)
     return MTG_ERR_HIP;
-  auto d = [&](size_t off) { return reinterpret_cast<double*>(sg.dev + off); };
+  auto d = [&](size_t off) { return reinterpret_cast<double*>(base + off); };
   int rc = from_hip(mtg::launch_linear_solve(
       pl, B, nfv ? d(0) : nullptr, d(o_t), d(o_out), d(o_cost), npv ? d(o_free) : nullptr,
-      reinterpret_cast<int32_t*>(sg.dev + o_st), sg.stream));
+      reinterpret_cast<int32_t*>(base + o_st), sg.stream));
   if (rc) return rc;
-  if (hipMemcpyAsync(sg.host + o_out, sg.dev + o_out, total - o_out, hipMemcpyDeviceToHost,
-                     sg.stream) != hipSuccess ||
-      hipStreamSynchronize(sg.stream) != hipSuccess)
+  if (!zc && hipMemcpyAsync(sg.host + o_out, sg.dev + o_out, total - o_out,
+                            hipMemcpyDeviceToHost, sg.stream) != hipSuccess)
     return MTG_ERR_HIP;
+  if (hipStreamSynchronize(sg.stream) != hipSuccess) return MTG_ERR_HIP;
   std::memcpy(coeffs, sg.host + o_out, nc * sizeof(double));
   if (cost) std::memcpy(cost, sg.host + o_cost, B * sizeof(double));
   if (free_vals && npv) std::memcpy(free_vals, sg.host + o_free, npv * sizeof(double));
@@ -566,7 +570,6 @@ static bool valid_coll_params(const mtg_plan* plan, int mode, const mtg_coll_par
 
 int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
                                  const mtg_coll_params* params, int optimize) {
-  clear_stale_error();
   if (B < 0 || !valid_coll_params(plan, mode, params)) return MTG_ERR_INVALID_ARG;
   if (mtg::coll_problems(plan->dev, B, mode, *params) > 0x7fffffff) return MTG_ERR_INVALID_ARG;
   return static_cast<int64_t>(
@@ -574,7 +577,6 @@ int64_t mtg_coll_workspace_bytes(const mtg_plan* plan, int64_t B, int mode,
 }
 
 int64_t mtg_coll_field_bytes(int nx, int ny, int nz) {
-  clear_stale_error();
   if (nx < 0 || ny < 0 || nz < 0) return MTG_ERR_INVALID_ARG;
   return static_cast<int64_t>(nx) * ny * nz * mtg::kFieldSlots * sizeof(uint16_t);
 }
@@ -669,7 +671,6 @@ static size_t select_ws_layout(const mtg_plan* plan, int64_t B, size_t* off_cost
 }
 
 int64_t mtg_select_workspace_bytes(const mtg_plan* plan, int64_t B) {
-  clear_stale_error();
   if (!plan || B < 0) return MTG_ERR_INVALID_ARG;
   size_t a, b;
   return static_cast<int64_t>(select_ws_layout(plan, B, &a, &b));
@@ -888,7 +889,6 @@ int mtg_time_optimize(const mtg_plan* plan, int64_t B, const double* fixed_vals,
 }
 
 int mtg_tube_num_constraints(int N, int S) {
-  clear_stale_error();
   if (!valid_N(N) || S < 1) return MTG_ERR_INVALID_ARG;
   return (S - 1) + S * (N - 2) + 2 * S * (N - 2);
 }
@@ -958,7 +958,6 @@ static bool valid_tube_time_params(int N, int S, const mtg_time_params* p) {
 
 int64_t mtg_tube_time_workspace_bytes(int N, int S, int64_t B, const mtg_time_params* params,
                                       int optimize) {
-  clear_stale_error();
   if (!valid_N(N) || S < 2 || B < 0 || !valid_tube_time_params(N, S, params))
     return MTG_ERR_INVALID_ARG;
   if (!tube_grid_ok(S, mtg::tube_time_problems(S, B, *params, optimize != 0)))
@@ -1028,7 +1027,6 @@ int mtg_generate_random_problems(int N, int D, int S, int64_t B, uint64_t seed0,
                                  double pos_bound, double v_max, double a_max,
                                  uint8_t* fixed_mask, double* fixed_vals, double* times,
                                  double* positions) {
-  clear_stale_error();
   using namespace mav_trajectory_generation;
   if (!valid_N(N) || D < 1 || S < 1 || B < 0 || !(pos_bound > 0) || !(v_max > 0) ||
       !(a_max > 0))

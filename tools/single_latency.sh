@@ -16,3 +16,16 @@ grep LATENCY "$out.txt"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 180 rocprofv3 --hip-trace --stats -d "$OLDPWD/$out.prof" -o run -- $bin latency \
   > "$OLDPWD/$out.prof.log" 2>&1
+cd "$OLDPWD"
+python3 - "$out" <<'PY'
+import glob, sqlite3, sys
+out = sys.argv[1]
+db = glob.glob(f"{out}.prof/**/*.db", recursive=True)[0]
+rows = sqlite3.connect(db).execute(
+    "select name, count(*), avg(end-start) from regions group by name order by count(*) desc")
+with open(f"{out}_hip_api.txt", "w") as f:
+    f.write("HIP API calls of the latency run under rocprofv3 --hip-trace: name, count, mean ns\n")
+    for n, c, a in rows:
+        f.write(f"{n:32s} {c:8d} {a:14.1f}\n")
+print(open(f"{out}_hip_api.txt").read())
+PY
