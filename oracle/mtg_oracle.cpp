@@ -574,6 +574,13 @@ struct QConstraint {
   double cst = 0.0;
 };
 
+// Warm-start state of the interior-point method (the device's
+// Tube::warm_start): x, s, lam of a trajectory's last usable solve.
+struct TubeWarm {
+  std::vector<double> x, s, lam;
+  bool valid = false;
+};
+
 struct TubeProblem {
   LinearProblem lp;  // Q, A^-1, 1-D reordering (qcqp_impl:95-117)
   int N = 10, D = 3, S = 0;
@@ -860,7 +867,12 @@ struct TubeProblem {
   // 1 iteration cap / stalled, 2 breakdown, 3 near-optimal at a breakdown.
   static constexpr double kComplFloor = 0.01;
   static constexpr double kKktReg = 1e-10;
-  int solveIPM(double tol, int max_iter, std::vector<double>* xout, int* iters) {
+  // ws (nullable): with a valid state, start from it (x as it was, s and
+  // lam floored at kWarmFloor) instead of the cold start; every usable solve
+  // (status 0, 1, 3) stores its final state there.
+  static constexpr double kWarmFloor = 1e-2;
+  int solveIPM(double tol, int max_iter, std::vector<double>* xout, int* iters,
+               TubeWarm* ws = nullptr) {
     Mat P;
     std::vector<double> q;
     objective(&P, &q);
@@ -873,7 +885,9 @@ struct TubeProblem {
     // derivatives zero (control points on the vertex, strictly inside every
     // tube and sphere).  The device kernel uses the same rule.
     std::vector<double> x(n, 0.0);
-    {
+    const bool warm = ws && ws->valid && static_cast<int>(ws->x.size()) == n &&
+                      static_cast<int>(ws->s.size()) == static_cast<int>(cons.size());
+    if (!warm) {
       Mat L = P;
       if (cholesky(&L)) {
         for (int i = 0; i < n; ++i) x[i] = -q[i];
@@ -889,9 +903,17 @@ struct TubeProblem {
       }
     }
     std::vector<double> s(m), lam(m, 1.0), g(m);
-    for (int k = 0; k < m; ++k) {
-      g[k] = residual(cons[k], x);
-      s[k] = std::max(-g[k], 1.0);
+    if (warm) {
+      x = ws->x;
+      for (int k = 0; k < m; ++k) {
+        s[k] = std::max(ws->s[k], kWarmFloor);
+        lam[k] = std::max(ws->lam[k], kWarmFloor);
+      }
+    } else {
+      for (int k = 0; k < m; ++k) {
+        g[k] = residual(cons[k], x);
+        s[k] = std::max(-g[k], 1.0);
+      }
     }
     double qnorm = 0.0;
     for (int i = 0; i < n; ++i) qnorm = std::max(qnorm, std::fabs(q[i]));
@@ -1033,6 +1055,12 @@ struct TubeProblem {
     }
     *xout = x;
     *iters = it;
+    if (ws && (status == 0 || status == 1 || status == 3)) {
+      ws->x = x;
+      ws->s = s;
+      ws->lam = lam;
+      ws->valid = true;
+    }
     return status;
   }
 };
@@ -1786,17 +1814,30 @@ int orc_tube_residuals(int N, int D, int r, int S, int K, const uint8_t* mask,
   return 0;
 }
 
+static int tubeQcqpSolve(int N, int D, int r, int S, int K, const uint8_t* mask,
+                         const double* vals, const double* times_cp, const double* times,
+                         const double* radii, double tol, int max_iter, double* x_out,
+                         double* coeffs, double* cost, int* iters, TubeWarm* ws);
+
 int orc_tube_qcqp_solve(int N, int D, int r, int S, int K, const uint8_t* mask,
                         const double* vals, const double* times_cp,
                         const double* times, const double* radii, double tol,
                         int max_iter, double* x_out, double* coeffs,
                         double* cost, int* iters) {
+  return tubeQcqpSolve(N, D, r, S, K, mask, vals, times_cp, times, radii, tol, max_iter, x_out,
+                       coeffs, cost, iters, nullptr);
+}
+
+static int tubeQcqpSolve(int N, int D, int r, int S, int K, const uint8_t* mask,
+                         const double* vals, const double* times_cp, const double* times,
+                         const double* radii, double tol, int max_iter, double* x_out,
+                         double* coeffs, double* cost, int* iters, TubeWarm* ws) {
   TubeProblem tp;
   int rc = setupTube(N, D, r, S, K, mask, vals, times_cp, times, radii, &tp);
   if (rc) return rc;
   std::vector<double> x;
   int it = 0;
-  int status = tp.solveIPM(tol, max_iter, &x, &it);
+  int status = tp.solveIPM(tol, max_iter, &x, &it, ws);
   if (status < 0) return status;
   if (status == 2) status = -22;  // numerical breakdown away from the optimum
   tp.recover(x);
@@ -1982,12 +2023,12 @@ static double tubeTimeObjective(int N, int D, int r, int S, int K, const uint8_t
                                 const double* vals, const double* times_cp,
                                 const double* radii, double tol, int max_iter,
                                 double time_penalty, const SoftSpec* soft,
-                                const std::vector<double>& t) {
+                                const std::vector<double>& t, TubeWarm* ws = nullptr) {
   std::vector<double> coeffs(static_cast<size_t>(S) * D * N);
   double c = 0.0;
   int it = 0;
-  const int rc = orc_tube_qcqp_solve(N, D, r, S, K, mask, vals, times_cp, t.data(), radii, tol,
-                                     max_iter, nullptr, coeffs.data(), &c, &it);
+  const int rc = tubeQcqpSolve(N, D, r, S, K, mask, vals, times_cp, t.data(), radii, tol,
+                               max_iter, nullptr, coeffs.data(), &c, &it, ws);
   if (rc < 0) return std::numeric_limits<double>::quiet_NaN();
   double total = 0.0;
   for (double v : t) total += v;  // nonlinear_impl:2768-2774
@@ -2056,13 +2097,16 @@ int orc_tube_time_optimize_sbplx(int N, int D, int r, int S, int K, const uint8_
   const SoftSpec soft{n_soft, soft_derivatives, soft_limits, soft_weight, soft_maximum_cost};
   const std::vector<double> T0(times_io, times_io + S);
   int k = 0;
+  // Consecutive evaluations share the constraints (maps at T0): each solve
+  // warm-starts from the previous usable one (the device's rule).
+  TubeWarm warm;
   auto objective = [&](const double* tp) {
     if (history && k < max_evals)
       std::memcpy(history + static_cast<size_t>(k) * S, tp, sizeof(double) * S);
     ++k;
     const std::vector<double> t(tp, tp + S);
     return tubeTimeObjective(N, D, r, S, K, mask, vals, T0.data(), radii, tol, max_iter,
-                             time_penalty, &soft, t);
+                             time_penalty, &soft, t, &warm);
   };
   std::vector<double> lb(S, 0.1), ub(S), step(S);
   for (int i = 0; i < S; ++i) {
