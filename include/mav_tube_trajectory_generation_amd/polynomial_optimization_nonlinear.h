@@ -11,20 +11,23 @@
 // device.
 //
 // Semantics and deliberate differences:
-//   * inner solve = the linear solve with the vertices' own constraint
-//     pattern (upstream mav_trajectory_generation semantics) by default.
-//     With the build's extension field `solve_time_with_qcqp` the callback
-//     re-solves the tube QCQP instead, as the fork does (solveQCQP at
-//     nonlinear_impl:892; mtg_tube_time_cost / mtg_tube_time_optimize);
+//   * inner solve = the tube QCQP, as the fork does (solveQCQP in
+//     objectiveFunctionTime, nonlinear_impl:892; mtg_tube_time_cost /
+//     mtg_tube_time_optimize_ex) by default (round 6).  The build's
+//     extension field `solve_time_with_qcqp = false` selects the linear solve
+//     with the vertices' own constraint pattern instead (upstream
+//     mav_trajectory_generation semantics; mtg_time_cost /
+//     mtg_time_optimize_ex);
 //   * NLopt (LN_SBPLX, nonlinear_impl:95-107) is absent.  kOptimizeTime with
 //     the default algorithm LN_SBPLX runs the device restatement of NLopt's
-//     Subplex (mtg_time_optimize_ex, optimizer 1: bounds [0.1, 2 T0],
-//     :350-378, initial step initial_stepsize_rel T0, maxeval
-//     max_iterations, :101, ftol f_rel / f_abs, :97-98); any other algorithm
-//     runs the projected central-difference descent (optimizer 0), and so
-//     does the QCQP-inner-solve form.  NLopt itself is absent, so optimiser
-//     parity is pinned to the oracle restatement only; the
-//     callback value is pinned;
+//     Subplex (optimizer 1: bounds [0.1, 2 T0], :350-378, initial step
+//     initial_stepsize_rel T0, maxeval max_iterations, :101, ftol f_rel /
+//     f_abs, :97-98) over either inner solve, and
+//     kOptimizeFreeConstraintsAndTime runs it over [T; d_p]
+//     (mtg_time_free_optimize_ex); any other algorithm runs the projected
+//     descents (optimizer 0).  NLopt itself is absent, so optimiser parity is
+//     pinned to the oracle restatement only; the callback
+//     value is pinned;
 //   * the collision cost reads a dense occupancy grid (setOccupancyGrid) in
 //     place of the supereight octree (setOctree).  kOptimizeFreeConstraints
 //     AndCollision and kOptimizeFreeConstraintsAndCollisionAndTime (the
@@ -144,9 +147,11 @@ struct NonlinearOptimizationParameters {
   VectorXd max_bound = VectorXd::Zero(3);
   bool use_numeric_grad = false;
   // Build extension (not in the reference struct): kOptimizeTime's callback
-  // re-solves the tube QCQP (the fork, nonlinear_impl:892) instead of the
-  // linear problem.  Read.
-  bool solve_time_with_qcqp = false;
+  // re-solves the tube QCQP, as the fork does (solveQCQP in
+  // objectiveFunctionTime, nonlinear_impl:892; the default, round 6), or
+  // with false the linear problem (upstream mav_trajectory_generation
+  // semantics, far cheaper).  Read.
+  bool solve_time_with_qcqp = true;
   bool use_continous_distance = false;
   double increment_time = 0.1;  // read (gradient step)
   double epsilon = 0.5;

@@ -581,6 +581,7 @@ TEST(gpu, TimeCostMatchesOracle) {
   const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
   NonlinearOptimizationParameters p;
   p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.solve_time_with_qcqp = false;  // the upstream linear inner solve
   p.weights.w_c = 0.0;
   PolynomialOptimizationNonLinear<10> opt(f.D, p);
   opt.setupFromVertices(vs, times, std::vector<std::pair<double, double>>(f.S, {0.15, 0.15}),
@@ -604,6 +605,7 @@ TEST(gpu, OptimizeTimeLowersObjective) {
   const std::vector<double> t0 = estimateSegmentTimes(vs, f.vmax, f.amax);
   NonlinearOptimizationParameters p;
   p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.solve_time_with_qcqp = false;  // the upstream linear inner solve
   p.weights.w_c = 0.0;
   p.max_iterations = 50;
   PolynomialOptimizationNonLinear<10> opt(f.D, p);
@@ -729,6 +731,7 @@ TEST(gpu, OptimizeTimeSbplxManySegments) {
   const std::vector<double> t0 = estimateSegmentTimes(vs, f.vmax, f.amax);
   NonlinearOptimizationParameters p;
   p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.solve_time_with_qcqp = false;  // the upstream linear inner solve
   p.weights.w_c = 0.0;
   p.max_iterations = 60;
   PolynomialOptimizationNonLinear<10> opt(f.D, p);
@@ -944,6 +947,7 @@ TEST(gpu, SoftConstraintTimeCost) {
   const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
   NonlinearOptimizationParameters p;
   p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.solve_time_with_qcqp = false;  // the upstream linear inner solve
   p.weights.w_c = 0.0;
   p.max_iterations = 30;
   PolynomialOptimizationNonLinear<10> opt(f.D, p);
@@ -1319,6 +1323,7 @@ TEST(gpu, PrintMatlabSampledTrajectory) {
   const std::vector<double> times = estimateSegmentTimes(vs, f.vmax, f.amax);
   NonlinearOptimizationParameters p;
   p.objective = NonlinearOptimizationParameters::kOptimizeTime;
+  p.solve_time_with_qcqp = false;  // the upstream linear inner solve
   p.weights.w_c = 0.0;
   p.max_iterations = 5;
   PolynomialOptimizationNonLinear<10> opt(3, p);
