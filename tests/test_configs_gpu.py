@@ -151,6 +151,12 @@ def test_config3_tube_at_size(ctx, dev, oracle):
     o_usable = (ost == 0) | (ost == 3)
     assert (~usable).sum() <= (~o_usable).sum(), ((~usable).sum(), (~o_usable).sum())
     assert (~usable).sum() <= 0.0025 * B and (~o_usable).sum() <= 0.0025 * B
+    # Round 6 (regularised retry of a failed KKT factorisation):
+    # every config-3 problem has a usable solution on the GPU (round 5: two
+    # near-optimal stops), and both implementations converge together.
+    assert usable.all(), hist
+    print("config 3 converged on both", int((conv & (ost == 0)).sum()), "of", B)
+    assert (conv & (ost == 0)).sum() >= 0.999 * B
     both = np.nonzero(conv & (ost == 0))[0]
     for b in both[::max(1, len(both) // 32)][:33]:
         r = refs[b]

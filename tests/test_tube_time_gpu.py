@@ -111,14 +111,14 @@ def test_tube_time_cost_repeated_calls(ctx, dev, oracle):
 
 def test_tube_time_optimize_vs_oracle(ctx, dev, oracle):
     """Same steps as the oracle's driver: accepted points, evaluation counts
-    and the final J on at least 2/3 of the problems.  Paths can diverge:
-    accept/reject compares J values that agree only to the QCQP tolerance,
-    and a QCQP breakdown (about 1-2% of random tube solves, in either
-    implementation, depending on rounding: tools/tube_status_agreement.py) ends a
-    path, so at 10 evaluations one problem in four to six takes another path
-    (11-13 of 16 agree across builds that differ only in summation order).
-    Every path is still checked: descent from J(T0), bounds, and the cost
-    equal to the oracle's at the returned times."""
+    and the final J on all but one of 24 problems (a trial landing on a
+    near-tie of two J values that agree only to the QCQP tolerance may take
+    another path).  Round 5 allowed a third to part: a QCQP breakdown at an
+    explored point (1-2 % of random tube solves then, in either
+    implementation) ended a path; with the round-6 IPM (tube-axis start,
+    regularised retry) there is none, and 24 of 24 agree on
+    MI355X.  Every path is also checked: descent from J(T0), bounds, and the
+    cost equal to the oracle's at the returned times."""
     import mav_tube_trajectory_generation_amd as mtg
     S, E = 4, 10
     items = _batch(oracle, S, range(400, 424))
@@ -147,7 +147,8 @@ def test_tube_time_optimize_vs_oracle(ctx, dev, oracle):
                                                max_evals=E)
         if er == ev[b] and np.max(np.abs(T[b] - tr)) <= 1e-6 * np.max(tr):
             agree += 1
-    assert agree >= 2 * len(items) / 3 and breakdowns <= 3, (agree, breakdowns)
+    print(f"tube FD descent: {agree} of {len(items)} paths agree, {breakdowns} breakdowns")
+    assert agree >= len(items) - 1 and breakdowns == 0, (agree, breakdowns)
 
 
 def test_tube_time_rejects_bad_arguments(ctx, dev, oracle):
