@@ -1138,17 +1138,20 @@ struct Tube {
       MTG_TACC(200, tl);
       MTG_TACC(201, tl);
       // A non-positive pivot (lam / s ~ 1e12 on active constraints swamps
-      // the rest of K in rounding) is retried once on K + kKktReg diag(K);
-      // the regularised Newton step still converges to the same optimum,
-      // where stopping left 16 % of the points of the time optimiser's box
-      // [0.1, 2 T0] without a value (the oracle's rule).  One call site, so
-      // the factorisation is instantiated once.
+      // the rest of K in rounding) away from the optimum (brk == 2) is
+      // retried once with a diagonal regularisation (kKktReg); the
+      // regularised Newton step still converges to the same optimum, where
+      // stopping left 16 % of the points of the time optimiser's box
+      // [0.1, 2 T0] without a value.  Near the optimum (brk 1 or 3) the
+      // iterate is kept, as before: going on regularised only stalls the dual
+      // residual to the iteration cap (the oracle's rule).  One call site,
+      // so the factorisation is instantiated once.
       for (double reg = 0.0;; reg = kKktReg) {
         if (tid == 0) *fail = 0;
         __syncthreads();
         factor(fail, true, reg);
         __syncthreads();
-        if (!*fail || reg > 0.0) break;
+        if (!*fail || reg > 0.0 || brk != 2) break;
       }
       MTG_TACC(202, tl);
       if (*fail) {

@@ -974,13 +974,20 @@ struct TubeProblem {
                 lam[k] * c.quad[static_cast<size_t>(u) * ms + v] + w * a[k][u] * a[k][v];
       }
       // A non-positive pivot (lam / s ~ 1e12 on active constraints swamps
-      // the rest of K in rounding) is retried once on K + kKktReg diag(K);
-      // the regularised Newton step still converges (to the same optimum),
-      // where stopping left 16 % of the points of the time optimiser's box
-      // [0.1, 2 T0] without a value (the device kernel uses the same rule).
+      // the rest of K in rounding) away from the optimum (brk == 2) is
+      // retried once on K + kKktReg diag(K); the regularised Newton step
+      // still converges (to the same optimum), where stopping left 16 % of
+      // the points of the time optimiser's box [0.1, 2 T0] without a value.
+      // Near the optimum (brk 1 or 3) the iterate is kept, as before: going
+      // on regularised only stalls the dual residual to the iteration cap.
+      // The device kernel uses the same rule.
       {
         Mat K0 = Kmat;
         if (!cholesky(&Kmat)) {
+          if (brk != 2) {
+            status = brk;
+            break;
+          }
           for (int i = 0; i < n; ++i) K0(i, i) += kKktReg * K0(i, i);
           Kmat = K0;
           if (!cholesky(&Kmat)) {
