@@ -164,6 +164,12 @@ struct TubeArgs {
   // stores its final state and sets the flag (mtg_tube_time.hip, LN_SBPLX).
   double* warm = nullptr;
   int32_t* warm_ok = nullptr;
+  // Optional dispatch order: workgroup i solves problem order[i] (a
+  // permutation of the B problems).  Results do not depend on it; the
+  // LN_SBPLX time optimiser puts the trajectories whose previous solve took
+  // the most iterations first (longest-processing-time first), so the
+  // round's long solves do not form its tail.
+  const int32_t* order = nullptr;
 };
 // Doubles of one problem's warm-start state.
 int64_t tube_warm_doubles(int N, int S);

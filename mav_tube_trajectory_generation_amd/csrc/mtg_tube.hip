@@ -66,9 +66,13 @@ __device__ __attribute__((always_inline)) void tube_solve_body(
     const double* __restrict__ times, const double* __restrict__ radii, double tol,
     int max_iter, const int32_t* __restrict__ skip, double* __restrict__ x_out,
     double* __restrict__ coeffs, double* __restrict__ cost, int32_t* __restrict__ iters,
-    int32_t* __restrict__ status, double* __restrict__ warm, int32_t* __restrict__ warm_ok) {
+    int32_t* __restrict__ status, double* __restrict__ warm, int32_t* __restrict__ warm_ok,
+    const int32_t* __restrict__ order) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int64_t b = xcd_problem(blockIdx.x, gridDim.x);  // mtg_device.h
+  // The problem of this workgroup: order[blockIdx.x] (TubeArgs::order:
+  // workgroups are dispatched in blockIdx order, so the longest solves go
+  // first), else the XCD-contiguous map (mtg_device.h).
+  const int64_t b = order ? order[blockIdx.x] : xcd_problem(blockIdx.x, gridDim.x);
   if (skip && skip[b / rep]) return;  // workgroup-uniform
   const TubeLayout L = make_tube_layout(N, S);
   Tube<N> t = make_tube<N>(&L, smem, S, r, tab);
@@ -137,14 +141,15 @@ __device__ __attribute__((always_inline)) void tube_solve_body(
       const double* __restrict__ times, const double* __restrict__ radii, double tol,          \
       int max_iter, const int32_t* __restrict__ skip, double* __restrict__ x_out,              \
       double* __restrict__ coeffs, double* __restrict__ cost, int32_t* __restrict__ iters,     \
-      int32_t* __restrict__ status, double* __restrict__ warm, int32_t* __restrict__ warm_ok
+      int32_t* __restrict__ status, double* __restrict__ warm, int32_t* __restrict__ warm_ok,  \
+      const int32_t* __restrict__ order
 
 template <int N>
 __global__ __launch_bounds__(tube_threads<N>())
 __attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
 void tube_solve_kernel(MTG_TUBE_SOLVE_PARAMS) {
   tube_solve_body<N>(S, r, rep, tab, positions, fixed_vals, times_cp, times, radii, tol, max_iter,
-                     skip, x_out, coeffs, cost, iters, status, warm, warm_ok);
+                     skip, x_out, coeffs, cost, iters, status, warm, warm_ok, order);
 }
 
 // S a compile-time constant (the argument S is ignored): every layout
@@ -155,7 +160,7 @@ __global__ __launch_bounds__(tube_threads<N>())
 __attribute__((amdgpu_waves_per_eu(tube_threads<N>() / kWave, tube_threads<N>() / kWave)))
 void tube_solve_s_kernel(MTG_TUBE_SOLVE_PARAMS) {
   tube_solve_body<N>(SC, r, rep, tab, positions, fixed_vals, times_cp, times, radii, tol, max_iter,
-                     skip, x_out, coeffs, cost, iters, status, warm, warm_ok);
+                     skip, x_out, coeffs, cost, iters, status, warm, warm_ok, order);
 }
 
 #ifdef MTG_STAMPS
@@ -204,7 +209,8 @@ hipError_t solve_launch(K kernel, int threads, const TubeArgs& a, double tol, in
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(threads), bytes, st, a.S,
                      a.r, a.rep, a.tab, a.positions, a.fixed_vals, a.times_cp, a.times, a.radii,
-                     tol, max_iter, a.skip, x, coeffs, cost, iters, status, a.warm, a.warm_ok);
+                     tol, max_iter, a.skip, x, coeffs, cost, iters, status, a.warm, a.warm_ok,
+                     a.order);
   return hipGetLastError();
 }
 

@@ -85,6 +85,8 @@ struct OptState {
   size_t sb_bytes;
   double* warm;     // LN_SBPLX: the IPM warm-start state per trajectory
   int32_t* warm_ok;
+  int32_t* iters;   // LN_SBPLX: IPM iterations of each trajectory's last solve
+  int32_t* order;   // LN_SBPLX: the next round's dispatch order (TubeArgs::order)
 };
 
 __global__ void tube_time_opt_init_kernel(int S, int64_t B, const double* __restrict__ times,
@@ -247,6 +249,40 @@ __global__ void tube_time_opt_result_kernel(int64_t B, int max_evals, OptState s
   if (b < B) result[b] = s.evals[b] >= max_evals ? sbplx::kMaxEval : sbplx::kXtol;
 }
 
+// The next round's dispatch order (TubeArgs::order): a counting sort of the
+// trajectories by their last solve's IPM iterations, most first, the
+// finished ones last.  A solve's iteration count is the best predictor of
+// the next one's (consecutive points of a trajectory are close and share
+// their constraints), so dispatching longest-first keeps a round's few long
+// solves (up to the 100-iteration cap) from starting last and forming its
+// tail.  Ties are placed in any order: results do not depend on the order.
+constexpr int kOrderKeys = 128;
+__global__ __launch_bounds__(1024) void tube_time_order_kernel(int64_t B,
+                                                               const int32_t* __restrict__ iters,
+                                                               const int32_t* __restrict__ done,
+                                                               int32_t* __restrict__ order) {
+  __shared__ int cnt[kOrderKeys], off[kOrderKeys];
+  const int t = static_cast<int>(threadIdx.x);
+  for (int k = t; k < kOrderKeys; k += blockDim.x) cnt[k] = 0;
+  __syncthreads();
+  auto key = [&](int64_t b) {
+    const int it = iters[b];
+    return done[b] ? 0 : 1 + (it < 0 ? 0 : (it > kOrderKeys - 2 ? kOrderKeys - 2 : it));
+  };
+  for (int64_t b = t; b < B; b += blockDim.x) atomicAdd(&cnt[key(b)], 1);
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int k = kOrderKeys - 1; k >= 0; --k) {
+      off[k] = run;
+      run += cnt[k];
+    }
+  }
+  __syncthreads();
+  for (int64_t b = t; b < B; b += blockDim.x)
+    order[atomicAdd(&off[key(b)], 1)] = static_cast<int32_t>(b);
+}
+
 unsigned blocks_for(int64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
 // Caller-owned workspace (mtg_tube_time_workspace_bytes), carved in a fixed
@@ -295,6 +331,8 @@ size_t carve(void* base, int N, int S, int64_t B, int P, int n_soft, bool optimi
       w->s.sb = c.take<char>(B * static_cast<int64_t>(w->s.sb_bytes));
       w->s.warm = c.take<double>(B * tube_warm_doubles(N, S));
       w->s.warm_ok = c.take<int32_t>(B);
+      w->s.iters = c.take<int32_t>(B);
+      w->s.order = c.take<int32_t>(B);
     }
   }
   return c.off;
@@ -309,7 +347,7 @@ size_t carve(void* base, int N, int S, int64_t B, int P, int n_soft, bool optimi
 hipError_t evaluate_points(const TubeArgs& a, int P, const double* T, double tol, int max_iter,
                            const mtg_time_params& p, const Workspace& w, const int32_t* skip,
                            double* Jall, double* cost, double* grad, int32_t* status,
-                           hipStream_t st) {
+                           hipStream_t st, int32_t* iters = nullptr) {
   const int S = a.S;
   const int64_t BP = a.B * P;
   hipLaunchKernelGGL(tube_time_points_kernel, dim3(blocks_for(BP * S)), dim3(256), 0, st, S,
@@ -321,7 +359,7 @@ hipError_t evaluate_points(const TubeArgs& a, int P, const double* T, double tol
   q.times = w.pts;
   q.rep = P;
   q.skip = skip;
-  e = launch_tube_solve(q, tol, max_iter, nullptr, w.coeffs, w.qcost, nullptr, w.qstatus, st);
+  e = launch_tube_solve(q, tol, max_iter, nullptr, w.coeffs, w.qcost, iters, w.qstatus, st);
   if (e != hipSuccess) return e;
   if (p.n_soft > 0) {
     SoftLimits lim{};
@@ -417,12 +455,18 @@ int tube_time_optimize(const TubeArgs& a, double* times_io, double tol, int max_
     q.warm_ok = s.warm_ok;
   }
   for (int round = 0; round < max_evals; ++round) {
+    // LN_SBPLX: from the second round on, the longest solves go first
+    if (sb) q.order = round > 0 ? s.order : nullptr;
     hipError_t e = evaluate_points(q, P, s.Ttr, tol, max_iter, p, w, s.done, w.Jall, nullptr,
-                                   nullptr, nullptr, st);
+                                   nullptr, nullptr, st, sb ? s.iters : nullptr);
     if (e != hipSuccess) return MTG_ERR_HIP;
-    if (sb)
+    if (sb) {
       hipLaunchKernelGGL(tube_time_sbplx_step_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S,
                          B, round == 0 ? 1 : 0, w.Jall, w.qstatus, s);
+      if (round + 1 < max_evals)
+        hipLaunchKernelGGL(tube_time_order_kernel, dim3(1), dim3(1024), 0, st, B, s.iters,
+                           s.done, s.order);
+    }
     else
       hipLaunchKernelGGL(tube_time_opt_step_kernel, dim3(blocks_for(B)), dim3(256), 0, st, S, B,
                          P, round == 0 ? 1 : 0, max_evals, p.increment, w.Jall, w.qstatus, s);

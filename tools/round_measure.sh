@@ -65,6 +65,8 @@ case "$mode" in
     B --workload time --optimizer sbplx --steps 20 --warmup 3 > gpurun_out/bench_time_sbplx.json 2> gpurun_out/bench_time_sbplx.err
     B --workload time --soft --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_time_soft.json 2> gpurun_out/bench_time_soft.err
     B --workload time-qcqp --steps 5 --warmup 1 > gpurun_out/bench_time_qcqp.json 2> gpurun_out/bench_time_qcqp.err
+    B --workload time-qcqp --optimizer sbplx --steps 3 --warmup 1 > gpurun_out/bench_time_qcqp_sbplx.json 2> gpurun_out/bench_time_qcqp_sbplx.err
+    B --workload time --optimizer sbplx --soft --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bench_time_sbplx_soft.json 2> gpurun_out/bench_time_sbplx_soft.err
     B --workload extrema > gpurun_out/bench_extrema.json 2> gpurun_out/bench_extrema.err
     B --workload sample > gpurun_out/bench_sample.json 2> gpurun_out/bench_sample.err
     B --workload collision --steps 5 --warmup 1 > gpurun_out/bench_collision.json 2> gpurun_out/bench_collision.err
@@ -76,6 +78,7 @@ case "$mode" in
     bash tools/profile.sh tube --workload tube --steps 5 --warmup 1
     bash tools/profile.sh time --workload time --steps 5 --warmup 1
     bash tools/profile.sh time_sbplx --workload time --optimizer sbplx --steps 5 --warmup 1
+    bash tools/profile.sh time_qcqp_sbplx --workload time-qcqp --optimizer sbplx --steps 2 --warmup 1
     bash tools/pmc_sq.sh linear
     bash tools/pmc_sq.sh linear_8192 --batch 8192 --steps 20 --warmup 2
     bash tools/pmc_sq.sh linear_65536 --batch 65536 --steps 20 --warmup 2
@@ -103,7 +106,7 @@ case "$mode" in
       > gpurun_out/tube/tests.log 2>&1
     B --workload tube --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/tube/bench.json 2> gpurun_out/tube/bench.err
     kline gpurun_out/tube/bench.json tube
-    timeout -k 10 300 python tools/tube_status_agreement.py r05 > gpurun_out/tube/agreement.txt 2>&1
+    timeout -k 10 300 python tools/tube_status_agreement.py r06 > gpurun_out/tube/agreement.txt 2>&1
     ;;
   ab)
     env=$1; shift
