@@ -33,6 +33,13 @@ inline mtg_ctx* defaultContext() {
   return ctx;
 }
 
+// The context's device as the calling thread's current device: the shim's
+// buffers and its null-stream launches go there from any thread.
+inline void bindDevice() {
+  MTG_CHECK(hipSetDevice(mtg_ctx_device(defaultContext())) == hipSuccess,
+            "hipSetDevice failed");
+}
+
 inline void checkStatus(int rc, const char* what) {
   MTG_CHECK(rc == MTG_OK, what << " failed: " << mtg_status_string(rc));
 }
@@ -51,7 +58,10 @@ class DeviceBuffer {
     if (n == n_) return;
     release();
     n_ = n;
-    if (n) MTG_CHECK(hipMalloc(&p_, n * sizeof(T)) == hipSuccess, "hipMalloc failed");
+    if (n) {
+      bindDevice();
+      MTG_CHECK(hipMalloc(&p_, n * sizeof(T)) == hipSuccess, "hipMalloc failed");
+    }
   }
   void upload(const T* src, size_t n) {
     resize(n);
@@ -84,6 +94,7 @@ class DeviceBuffer {
 };
 
 inline void synchronize() {
+  bindDevice();
   MTG_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize failed");
 }
 

@@ -81,7 +81,13 @@ const char* mtg_status_string(int status);
 int mtg_version(void);
 
 /* Context = one HIP device.  Replaces nothing in the reference (which has no
- * device); owns the cached constant tables and constraint patterns. */
+ * device); owns the cached constant tables and constraint patterns.
+ * mtg_ctx_create makes `device` the calling thread's current device (the
+ * C++ shim allocates its buffers there).  Allocating calls (plan create /
+ * destroy, the constant tables, the host-memory solve's staging) run on the
+ * context's device and restore the caller's current device; the launching
+ * calls enqueue on the stream they are given (null: the current device's
+ * null stream), whose device must be the context's. */
 int mtg_ctx_create(int device, mtg_ctx** out);
 int mtg_ctx_destroy(mtg_ctx* ctx);
 int mtg_ctx_device(const mtg_ctx* ctx);

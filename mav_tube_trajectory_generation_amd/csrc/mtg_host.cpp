@@ -158,6 +158,20 @@ void build_tables(int N, int r, std::vector<double>* out) {
     }
 }
 
+// Makes `device` current for the calling thread while in scope and restores
+// the caller's device afterwards: allocations and the plan's staging stream
+// land on the context's device whatever device the thread had selected.
+struct DeviceScope {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceScope(int device) {
+    ok = hipGetDevice(&prev) == hipSuccess && hipSetDevice(device) == hipSuccess;
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 int get_tables(mtg_ctx* ctx, int N, int r, const double** out) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   auto key = std::make_pair(N, r);
@@ -169,7 +183,8 @@ int get_tables(mtg_ctx* ctx, int N, int r, const double** out) {
   std::vector<double> host;
   build_tables(N, r, &host);
   double* d = nullptr;
-  if (hipSetDevice(ctx->device) != hipSuccess) return MTG_ERR_HIP;
+  DeviceScope dev(ctx->device);
+  if (!dev.ok) return MTG_ERR_HIP;
   if (hipMalloc(&d, host.size() * sizeof(double)) != hipSuccess) return MTG_ERR_HIP;
   if (hipMemcpy(d, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice) !=
       hipSuccess) {
@@ -223,7 +238,7 @@ int mtg_ctx_create(int device, mtg_ctx** out) {
 
 int mtg_ctx_destroy(mtg_ctx* ctx) {
   if (!ctx) return MTG_ERR_INVALID_ARG;
-  (void)hipSetDevice(ctx->device);
+  DeviceScope dev(ctx->device);
   for (auto& kv : ctx->tables) (void)hipFree(kv.second);
   delete ctx;
   return MTG_OK;
@@ -263,6 +278,8 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fix
   if (rc) return rc;
   std::unique_ptr<mtg_plan> p(new mtg_plan);
   p->ctx = ctx;
+  DeviceScope dev(ctx->device);
+  if (!dev.ok) return MTG_ERR_HIP;
   if (hipMalloc(&p->d_slots, slots.size() * sizeof(int)) != hipSuccess) return MTG_ERR_HIP;
   if (hipMalloc(&p->d_free_map, (free_map.size() + 1) * sizeof(int)) != hipSuccess) {
     (void)hipFree(p->d_slots);
@@ -303,6 +320,8 @@ int mtg_plan_create(mtg_ctx* ctx, int N, int D, int r, int S, const uint8_t* fix
 
 int mtg_plan_destroy(mtg_plan* plan) {
   if (!plan) return MTG_ERR_INVALID_ARG;
+  DeviceScope dev(plan->ctx->device);
+  plan->stage.reset();  // its stream and buffers belong to the plan's device
   (void)hipFree(plan->d_slots);
   (void)hipFree(plan->d_free_map);
   (void)hipFree(plan->d_fixed_map);
@@ -373,9 +392,10 @@ int mtg_linear_solve_host(const mtg_plan* plan, int64_t B, const double* fixed_v
   const size_t total = up(o_st + B * sizeof(int32_t));
   mtg_staging& sg = *plan->stage;
   std::lock_guard<std::mutex> lock(sg.mu);
+  DeviceScope dev(plan->ctx->device);
+  if (!dev.ok) return MTG_ERR_HIP;
   if (!sg.stream) {
-    if (hipSetDevice(plan->ctx->device) != hipSuccess ||
-        hipStreamCreateWithFlags(&sg.stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&sg.stream, hipStreamNonBlocking) != hipSuccess) {
       sg.stream = nullptr;
       return MTG_ERR_HIP;
     }
