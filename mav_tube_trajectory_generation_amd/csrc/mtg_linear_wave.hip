@@ -15,6 +15,14 @@
 namespace mtg {
 namespace wave {
 
+// Trajectories (wavefronts) per workgroup; each wave owns its LDS region and
+// runs independently (no workgroup barrier).  A/B builds: -DMTG_WAVE_WPB=n.
+#ifndef MTG_WAVE_WPB
+#define MTG_WAVE_WPB 1
+#endif
+constexpr int kWpb = MTG_WAVE_WPB;
+static_assert(kWpb >= 1 && kWpb <= 4, "1 to 4 waves per workgroup");
+
 // The problem count nb is an argument in the first 64 bytes (the first 56
 // are preloaded into SGPRs; nb is the one scalar load before the first
 // global load, as gridDim.x was in round 4), and kPrev (this launch carries
@@ -25,26 +33,30 @@ namespace wave {
 // into the preloaded bytes as well (free_vals after it) gave no gain
 // (4.65 - 4.71 us, profiles/r05_kernarg_abl_c2_v2.txt).
 template <int N, int R, int D, int S, bool kPrev>
-__global__ __launch_bounds__(kWave) void linear_wave_kernel(
+__global__ __launch_bounds__(kWave * kWpb) void linear_wave_kernel(
     const double* __restrict__ tab, const double* __restrict__ fixed_vals,
     const double* __restrict__ times, double* __restrict__ coeffs, double* __restrict__ cost,
     double* __restrict__ free_vals, int32_t* __restrict__ status, int nb, SelectArgs sel) {
   using Sv = Solver<N, R, D, S>;
   using G = typename Sv::G;
   constexpr int MF = G::MF, MP = G::MP, NFIX = G::NFIX;
-  __shared__ __attribute__((aligned(16))) double sm[G::L_N];
+  __shared__ __attribute__((aligned(16))) double sm[kWpb * G::L_N];
+  const int nblk = (nb + kWpb - 1) / kWpb;
   // The deferred selection (the previous step's costs) in one extra
   // workgroup after the solves: it runs beside them (about 1 us at
   // B = 1024 against a 3.4 us solve), so it costs no launch of its own.
-  if (kPrev && static_cast<int>(blockIdx.x) == nb) {
-    select_reduce_block<kWave>(sel.prev_cost, sel.prev_count, sel.prev_start, sel.rank,
-                               sel.prev_out, nullptr, nullptr);
+  if (kPrev && static_cast<int>(blockIdx.x) == nblk) {
+    if (threadIdx.x < kWave)
+      select_reduce_block<kWave>(sel.prev_cost, sel.prev_count, sel.prev_start, sel.rank,
+                                 sel.prev_out, nullptr, nullptr);
     return;
   }
+  const int w = kWpb > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0;
+  const int64_t b = xcd_problem(blockIdx.x, nblk) * kWpb + w;
+  if (kWpb > 1 && b >= nb) return;
   Sv sv;
-  sv.init(sm);
+  sv.init(sm + w * G::L_N);
   const int lane = sv.lane;
-  const int64_t b = xcd_problem(blockIdx.x, nb);
   const double* fb = fixed_vals + b * D * NFIX;
   const double* tb = times + b * S;
   MTG_STAMP(0);
@@ -109,12 +121,13 @@ static hipError_t launch_wave_s(int64_t B, const SelectArgs& sel, const double* 
                                 const double* df, const double* times, double* coeffs,
                                 double* cost, double* free_vals, int32_t* status,
                                 hipStream_t st) {
+  const unsigned nblk = static_cast<unsigned>((B + kWpb - 1) / kWpb);
   if (sel.prev_out)
-    hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S, true>), dim3(static_cast<unsigned>(B + 1)),
-                       dim3(kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status, static_cast<int>(B), sel);
+    hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S, true>), dim3(nblk + 1),
+                       dim3(kWave * kWpb), 0, st, tab, df, times, coeffs, cost, free_vals, status, static_cast<int>(B), sel);
   else
-    hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S, false>), dim3(static_cast<unsigned>(B)),
-                       dim3(kWave), 0, st, tab, df, times, coeffs, cost, free_vals, status, static_cast<int>(B), sel);
+    hipLaunchKernelGGL((linear_wave_kernel<10, 4, 3, S, false>), dim3(nblk),
+                       dim3(kWave * kWpb), 0, st, tab, df, times, coeffs, cost, free_vals, status, static_cast<int>(B), sel);
   return hipGetLastError();
 }
 

@@ -154,7 +154,7 @@ struct Solver {
     slots = sm + G::L_SL;
     hh = sm + G::L_H;
     junk = sm + G::L_JUNK;
-    lane = threadIdx.x;
+    lane = threadIdx.x & (kWave - 1);
     ai = lane % MF;
     av = lane / MF + 1 < S - 1 ? lane / MF + 1 : S - 1;
     const int sd = lane < S * D ? lane : S * D - 1;
