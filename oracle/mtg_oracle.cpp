@@ -865,12 +865,13 @@ struct TubeProblem {
   //   min 0.5 x^T P x + q^T x  s.t.  g_k(x) <= 0  (convex QCQP),
   // replacing MSK_optimizetrm (qcqp_impl:700-712).  Status 0 converged,
   // 1 iteration cap / stalled, 2 breakdown, 3 near-optimal at a breakdown.
-  static constexpr double kComplFloor = 0.01;
+  static constexpr double kComplFloor = 1e-3;
   static constexpr double kKktReg = 1e-10;
   // ws (nullable): with a valid state, start from it (x as it was, s and
   // lam floored at kWarmFloor) instead of the cold start; every usable solve
   // (status 0, 1, 3) stores its final state there.
   static constexpr double kWarmFloor = 1e-2;
+  static constexpr double kLamStart = 30.0;
   int solveIPM(double tol, int max_iter, std::vector<double>* xout, int* iters,
                TubeWarm* ws = nullptr) {
     Mat P;
@@ -902,7 +903,24 @@ struct TubeProblem {
           }
       }
     }
-    std::vector<double> s(m), lam(m, 1.0), g(m);
+    // Cold start scaled to the problem (round 6): slacks at least the square
+    // of the largest vertex coordinate (the constraints' units are squared
+    // lengths), multipliers at least 30 |q|_inf (the objective's gradient
+    // scale).  Unit slacks and multipliers started the iteration far below
+    // both scales: 30.6 -> 21.6 IPM iterations on 400 C3 problems, the same
+    // status for every problem of a 432-case sweep over N, S, radii and
+    // coordinate scales, converged costs within tolerance.  The device kernel
+    // uses the same rule.
+    double qnorm = 0.0;
+    for (int i = 0; i < n; ++i) qnorm = std::max(qnorm, std::fabs(q[i]));
+    double pmax = 1.0;
+    for (int v = 0; v <= S; ++v) {
+      std::vector<double> pv;
+      lp.vertices[v].get(0, &pv);
+      for (double c : pv) pmax = std::max(pmax, std::fabs(c));
+    }
+    const double s_start = pmax * pmax, lam_start = std::max(1.0, kLamStart * qnorm);
+    std::vector<double> s(m), lam(m, lam_start), g(m);
     if (warm) {
       x = ws->x;
       for (int k = 0; k < m; ++k) {
@@ -912,11 +930,9 @@ struct TubeProblem {
     } else {
       for (int k = 0; k < m; ++k) {
         g[k] = residual(cons[k], x);
-        s[k] = std::max(-g[k], 1.0);
+        s[k] = std::max(-g[k], s_start);
       }
     }
-    double qnorm = 0.0;
-    for (int i = 0; i < n; ++i) qnorm = std::max(qnorm, std::fabs(q[i]));
     int it = 0;
     int status = 1;
     std::vector<std::vector<double>> a(m);
@@ -1038,7 +1054,11 @@ struct TubeProblem {
       // the dual residual sends lam_k / s_k on the active constraints past
       // 1e12, where the condensed KKT matrix loses its null-space part to
       // rounding and the dual residual stalls (and the factorisation breaks
-      // down: 87 of 400 problems stopped that way before).
+      // down: 87 of 400 problems stopped that way before).  kComplFloor 1e-2
+      // with unit starts (round 5); 1e-3 with the scaled start (round 6):
+      // 30.6 -> 20.0 iterations on 400 C3 problems, all converged, and 420
+      // instead of 373 of a 432-case sweep over N, S, radii and scales
+      // converged (none fewer); 3e-4 and below leave near-optimal stops.
       double sigma = std::pow(mu_aff / mu, 3);
       {
         const double infeas = std::max(rdn / (1.0 + qnorm), rpn);
