@@ -997,7 +997,10 @@ struct Tube {
   // report it near-optimal if every residual is within 1e3 * tol (status 3);
   // with the dual residual within 1e5 * tol instead, not converged
   // (status 1).
-  static constexpr double kComplFloor = 5e-3;
+#ifndef MTG_TUBE_FLOOR  // A/B builds only (tools/build_variant.sh -DMTG_TUBE_FLOOR=...)
+#define MTG_TUBE_FLOOR 2e-2
+#endif
+  static constexpr double kComplFloor = MTG_TUBE_FLOOR;
   static constexpr double kKktReg = 1e-10;
   // Warm start (ws != nullptr: the trajectory's previous solve, x then s
   // then lam in this kernel's own layouts): x as it was, s and lam floored
@@ -1008,8 +1011,8 @@ struct Tube {
   // optimum in about half the iterations (55 -> 30 per evaluation).
   static constexpr double kWarmFloor = 1e-2;
   // Cold-start multipliers: at least kLamStart |q|_inf (the oracle's value;
-  // with the slack scale of ipm() and kComplFloor 30.8 -> 21.1 iterations
-  // on 4100 C3 problems).
+  // with the slack scale of ipm() and kComplFloor 30.8 -> 22.9 iterations
+  // on the 4096 C3 problems).
   static constexpr double kLamStart = 30.0;
   __device__ void warm_start(const double* __restrict__ ws) {
     for (int idx = tid; idx < nv * BS; idx += nthr) sm[L->x + idx] = ws[idx];
@@ -1183,7 +1186,7 @@ struct Tube {
       // running ahead of the dual residual sends lam / s on the active
       // constraints past 1e12, where the condensed KKT matrix loses its
       // null-space part to rounding, the dual residual stalls and the
-      // factorisation breaks down.  kComplFloor = 5e-3 with the scaled start
+      // factorisation breaks down.  kComplFloor = 2e-2 with the scaled start
       // (1e-2 with unit starts, round 5; the oracle's values).
       double sigma = ratio * ratio * ratio;
       {

@@ -865,7 +865,7 @@ struct TubeProblem {
   //   min 0.5 x^T P x + q^T x  s.t.  g_k(x) <= 0  (convex QCQP),
   // replacing MSK_optimizetrm (qcqp_impl:700-712).  Status 0 converged,
   // 1 iteration cap / stalled, 2 breakdown, 3 near-optimal at a breakdown.
-  static constexpr double kComplFloor = 5e-3;
+  static constexpr double kComplFloor = 2e-2;
   static constexpr double kKktReg = 1e-10;
   // ws (nullable): with a valid state, start from it (x as it was, s and
   // lam floored at kWarmFloor) instead of the cold start; every usable solve
@@ -1055,11 +1055,13 @@ struct TubeProblem {
       // 1e12, where the condensed KKT matrix loses its null-space part to
       // rounding and the dual residual stalls (and the factorisation breaks
       // down: 87 of 400 problems stopped that way before).  kComplFloor 1e-2
-      // with unit starts (round 5); 5e-3 with the scaled start (round 6):
-      // 30.8 -> 21.1 iterations on 4100 C3 problems with as many
-      // near-optimal stops (2), 388 instead of 373 of a 432-case sweep over
-      // N, S, radii and scales converged (none fewer); lower floors cut a
-      // further iteration but stop more problems near-optimal (1e-3: 8).
+      // with unit starts (round 5); 2e-2 with the scaled start (round 6):
+      // 30.8 -> 22.9 iterations on 4096 C3 problems, every one converged
+      // (round 5: two near-optimal stops).  Lower floors save up to two more
+      // iterations but stop more problems near-optimal on the device, whose
+      // block LDL^T meets the breakdown where this dense Cholesky does not
+      // (config 3, device / oracle near-optimal: 1e-2 3 / 3 on different
+      // problems, 5e-3 7 / 2, 2e-3 11 / 5; profiles/r06_tube_floor_ab.txt).
       double sigma = std::pow(mu_aff / mu, 3);
       {
         const double infeas = std::max(rdn / (1.0 + qnorm), rpn);
