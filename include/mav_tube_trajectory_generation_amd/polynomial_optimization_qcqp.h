@@ -84,7 +84,8 @@ class PolynomialOptimizationConstrained : public PolynomialOptimization<_N> {
   //                             but is not an optimum.
   // Since round 3 the IPM's complementarity floor turns most
   // former breakdowns into status 0; the remaining near-optimal stops are 4
-  // (about 1 in 1,000 problems).
+  // (2 of the 4,096 config-3 problems with round 6's scaled start, DESIGN.md
+  // 5.3).
   static bool qcqpUsable(int status) {
     return status == MTG_TRAJ_OK || status == MTG_TRAJ_NEAR_OPTIMAL;
   }
